@@ -1,0 +1,130 @@
+/*
+ * coa_verify.h -- C ABI of the MI355X (gfx950) ed25519 / SHA-512 verification
+ * engine for the Narwhal/Tusk fork pwang200/xrpl-coa-prototype.
+ *
+ * This is the drop-in boundary for the reference's `crypto` crate hot path.
+ * Every entry point names the reference interface it replaces.  Plain
+ * pointers and sizes only: no HIP or torch types in the signatures (device
+ * streams are passed as `void*` = hipStream_t).
+ *
+ * Conventions
+ *   - Verdict bytes: 0 = Ok, 1 = Err (the reference's Result<(), CryptoError>;
+ *     CryptoError = ed25519::Error is opaque, crypto/src/lib.rs:18, so callers
+ *     only branch Ok/Err -- primary/src/error.rs:28 maps it to
+ *     DagError::InvalidSignature).
+ *   - Return codes: COA_OK (0) / COA_REJECT (1) for single verdicts; COA_OK for
+ *     a completed many-call; a negative COA_E* on internal failure.  There is
+ *     NO CPU fallback: with no usable GPU every call returns COA_ENODEVICE.
+ *   - Host-pointer calls: inputs are caller-owned and only read during the
+ *     call; outputs are caller-allocated.  Nothing is retained after return.
+ *   - Thread safety: every call takes the engine lock of the devices it uses;
+ *     calls from several threads are serialised per device.
+ *   - Multi-GPU: host-pointer "many" calls shard items by contiguous index
+ *     range over the devices opened by coa_init (no cross-GPU exchange).
+ */
+#ifndef COA_VERIFY_H
+#define COA_VERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define COA_OK 0
+#define COA_REJECT 1
+#define COA_EINVAL (-1)
+#define COA_ENODEVICE (-2)
+#define COA_EHIP (-3)
+#define COA_ENOMEM (-4)
+
+/* ---------------------------------------------------------------- lifecycle
+ * No reference counterpart (dalek is stateless).  Opens `n_gpus` devices
+ * (0 = all visible), builds the fixed-base tables on each.  Idempotent; the
+ * other calls initialise lazily with n_gpus = 0 when it was not called. */
+int coa_init(int n_gpus);
+int coa_shutdown(void);
+int coa_device_count(void);
+/* Human-readable description of the last error on this thread. */
+const char* coa_last_error(void);
+/* Library / ABI version string. */
+const char* coa_version(void);
+
+/* ------------------------------------------------------- Signature::verify
+ * Replaces crypto::Signature::verify (crypto/src/lib.rs:200-204):
+ *   ed25519::Signature::from_bytes(sig)            (:201)
+ *   ed25519_dalek::PublicKey::from_bytes(pk)       (:202)
+ *   PublicKey::verify_strict(msg, sig)             (:203)
+ * called by Header::verify (primary/src/messages.rs:64-66) and Vote::verify
+ * (primary/src/messages.rs:139-141).  msg is the 32-byte Digest.
+ * Returns COA_OK, COA_REJECT or a negative error (latency path). */
+int coa_ed25519_verify_strict(const uint8_t msg[32], const uint8_t pk[32], const uint8_t sig[64]);
+
+/* n independent (msg, pk, sig) triples; msgs are n * msg_len bytes (msg_len
+ * 32 for the crypto API, any length supported), pks n * 32, sigs n * 64
+ * (R || s).  verdicts_out[i] = 0 Ok / 1 Err.  Sharded over all devices. */
+int coa_ed25519_verify_strict_many(const uint8_t* msgs, size_t msg_len, const uint8_t* pks, const uint8_t* sigs,
+                                   size_t n, uint8_t* verdicts_out);
+
+/* Same, with every buffer already resident in the HBM of `device` and the
+ * work enqueued on `stream` (hipStream_t; NULL = the engine's stream for that
+ * device).  Asynchronous: returns after enqueue.  `workspace` may be NULL
+ * (engine-owned) -- otherwise at least coa_verify_workspace_bytes(n) bytes of
+ * device memory on `device`. */
+size_t coa_verify_workspace_bytes(size_t n);
+int coa_ed25519_verify_strict_many_device(int device, const uint8_t* d_msgs, size_t msg_len, const uint8_t* d_pks,
+                                          const uint8_t* d_sigs, size_t n, uint8_t* d_verdicts, void* workspace,
+                                          void* stream);
+
+/* ------------------------------------------------- Signature::verify_batch
+ * Replaces crypto::Signature::verify_batch (crypto/src/lib.rs:206-219) ->
+ * ed25519_dalek::verify_batch (:218), called by Certificate::verify
+ * (primary/src/messages.rs:214).  One group = one certificate: all its votes
+ * sign the same 32-byte digest.
+ *   msgs           n_groups * 32 bytes
+ *   pks, sigs      concatenated votes, group g = [group_offsets[g], group_offsets[g+1])
+ *   group_offsets  n_groups + 1 entries, group_offsets[0] = 0
+ *   group_verdicts_out[g] = 0 Ok / 1 Err
+ * The 128-bit random weights z_i are derived from rng_seed (0 = fresh OS
+ * entropy per call, the dalek behaviour; any other value is reproducible).
+ * Ok iff every s_i < l, every A_i and R_i decompresses and the random linear
+ * combination is the identity -- no small-order rejection, no cofactor,
+ * exactly dalek 1.0.1. */
+int coa_ed25519_verify_batch(const uint8_t msg[32], const uint8_t* pks, const uint8_t* sigs, size_t n,
+                             uint64_t rng_seed);
+int coa_ed25519_verify_batch_groups(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs,
+                                    const uint64_t* group_offsets, size_t n_groups, uint8_t* group_verdicts_out,
+                                    uint64_t rng_seed);
+/* Parity-test form: the z_i are given explicitly (16 little-endian bytes per
+ * signature, in the order of pks/sigs). */
+int coa_ed25519_verify_batch_groups_z(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs,
+                                      const uint64_t* group_offsets, size_t n_groups, const uint8_t* zs,
+                                      uint8_t* group_verdicts_out);
+
+/* ------------------------------------------------------------------ Digest
+ * Replaces Sha512::digest at worker/src/processor.rs:38 (500 KB batch
+ * digests) and the Header/Vote/Certificate digests
+ * (primary/src/messages.rs:70-84,145-153,226-234).  Message i is
+ * data[offsets[i] .. offsets[i+1]); offsets has n + 1 entries.
+ * coa_sha512_many writes 64 bytes per message, coa_sha512_trunc32_many the
+ * 32-byte crypto::Digest prefix. */
+int coa_sha512_many(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out64);
+int coa_sha512_trunc32_many(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out32);
+int coa_sha512_many_device(int device, const uint8_t* d_data, const uint64_t* d_offsets, size_t n, uint8_t* d_out64,
+                           void* stream);
+
+/* --------------------------------------------------------------- signing
+ * RFC 8032 signing == crypto::Signature::new (crypto/src/lib.rs:185-191) /
+ * generate_keypair (:167-175) from 32-byte seeds.  Not on the verification
+ * hot path; used to synthesise benchmark and test inputs on the device. */
+int coa_ed25519_public_keys(const uint8_t* seeds, size_t n, uint8_t* pks_out);
+int coa_ed25519_sign_many(const uint8_t* seeds, const uint8_t* msgs, size_t msg_len, size_t n, uint8_t* pks_out,
+                          uint8_t* sigs_out);
+int coa_ed25519_sign_many_device(int device, const uint8_t* d_seeds, const uint8_t* d_msgs, size_t msg_len, size_t n,
+                                 uint8_t* d_pks_out, uint8_t* d_sigs_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COA_VERIFY_H */

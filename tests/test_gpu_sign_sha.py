@@ -1,0 +1,68 @@
+"""GPU parity: RFC 8032 signing (Signature::new) and SHA-512 digests
+(Sha512::digest at worker/src/processor.rs:38 and the primary digests)."""
+import hashlib
+import struct
+
+import numpy as np
+import pytest
+
+import ed25519_ref as o
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def test_sign_matches_oracle(engine):
+    seeds = [o.sha512(b"coa-key" + struct.pack("<Q", i))[:32] for i in range(40)]
+    msgs = [o.sha512(struct.pack("<Q", i))[:32] for i in range(40)]
+    pks, sigs = engine.sign_many(np.frombuffer(b"".join(seeds), np.uint8).reshape(40, 32),
+                                 np.frombuffer(b"".join(msgs), np.uint8).reshape(40, 32))
+    for i in range(40):
+        assert bytes(pks[i]) == o.public_key(seeds[i])
+        assert bytes(sigs[i]) == o.sign(seeds[i], msgs[i])
+    ref = load_golden("reference_crypto.json")
+    s = np.frombuffer(b"".join(bytes.fromhex(x) for x in ref["seeds"]), np.uint8).reshape(4, 32)
+    assert [bytes(p).hex() for p in engine.public_keys(s)] == ref["public_keys"]
+
+
+@pytest.mark.parametrize("msg_len", [0, 1, 17, 64, 100, 200])
+def test_sign_variable_length(engine, msg_len):
+    rng = np.random.default_rng(msg_len)
+    seeds = rng.integers(0, 256, (8, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, (8, msg_len), dtype=np.uint8)
+    pks, sigs = engine.sign_many(seeds, msgs)
+    for i in range(8):
+        assert bytes(sigs[i]) == o.sign(bytes(seeds[i]), bytes(msgs[i]))
+
+
+def test_sha512_golden(engine):
+    vecs = load_golden("sha512_vectors.json")
+    out = engine.sha512_many([bytes.fromhex(v["msg"]) for v in vecs])
+    for v, d in zip(vecs, out):
+        assert bytes(d).hex() == v["sha512"]
+
+
+def test_sha512_random_lengths_and_alignment(engine):
+    rng = np.random.default_rng(3)
+    msgs = [bytes(rng.integers(0, 256, int(ln), dtype=np.uint8)) for ln in rng.integers(0, 2000, 257)]
+    out = engine.sha512_many(msgs)
+    for m, d in zip(msgs, out):
+        assert bytes(d) == hashlib.sha512(m).digest()
+
+
+def test_reference_batch_digest(engine):
+    ref = load_golden("reference_crypto.json")
+    d = engine.digest_many([bytes.fromhex(ref["serialized_batch"])])[0]
+    assert bytes(d).hex() == ref["batch_digest"]
+    assert engine.digest_many([b"Hello, world!"])[0] == engine.Digest(bytes.fromhex(ref["hello_digest"]))
+
+
+def test_worker_batch_500kb(engine):
+    """C4 shape: bincode WorkerMessage::Batch of 977 x 512 B txs (508,052 B)."""
+    from workloads import worker_batch
+
+    batches = [worker_batch(b) for b in range(6)]
+    assert all(len(b) == 508_052 for b in batches)
+    out = engine.sha512_many(batches)
+    for b, d in zip(batches, out):
+        assert bytes(d) == hashlib.sha512(b).digest()

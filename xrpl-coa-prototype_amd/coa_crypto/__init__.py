@@ -1,0 +1,346 @@
+"""Host-side mirror of the reference `crypto` crate (crypto/src/lib.rs) over
+the MI355X engine's C ABI (include/coa_verify.h).
+
+Same names, same argument meaning, same error behaviour as the Rust API the
+reference's callers use:
+
+    Digest([u8;32])                         crypto/src/lib.rs:20-57
+    PublicKey([u8;32]) + base64 helpers      crypto/src/lib.rs:64-119
+    Signature{part1, part2}                  crypto/src/lib.rs:177-182
+    Signature.verify(digest, public_key)     crypto/src/lib.rs:200-204
+    Signature.verify_batch(digest, votes)    crypto/src/lib.rs:206-219
+    CryptoError (opaque ed25519::Error)      crypto/src/lib.rs:18
+
+`verify`/`verify_batch` raise CryptoError exactly where the Rust functions
+return Err.  All verification runs in the HIP kernels of
+lib/libcoa_verify.so; if that library is missing or no GPU is present the
+calls raise EngineError -- there is no CPU fallback.
+
+Bulk (engine-level) entry points, used by the primary/worker callers'
+batching paths and by the benchmark, take numpy arrays (host) or torch
+tensors (device) -- see verify_strict_many, verify_batch_groups, sha512_many.
+"""
+import base64
+import ctypes
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG, "lib", "libcoa_verify.so")
+
+COA_OK, COA_REJECT = 0, 1
+_ERRORS = {-1: "COA_EINVAL", -2: "COA_ENODEVICE", -3: "COA_EHIP", -4: "COA_ENOMEM"}
+
+
+class CryptoError(Exception):
+    """crypto::CryptoError = ed25519::Error: opaque verification failure."""
+
+
+class EngineError(RuntimeError):
+    """The GPU engine could not run the call (no device, HIP error, bad args)."""
+
+
+_lib = None
+
+
+def _u8p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if a is not None else None
+
+
+def lib():
+    """Load the engine library (fail loudly if it is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EngineError(f"{LIB_PATH} not built (run __graft_entry__.build()); no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    P8 = ctypes.POINTER(ctypes.c_uint8)
+    P64 = ctypes.POINTER(ctypes.c_uint64)
+    sz, vp = ctypes.c_size_t, ctypes.c_void_p
+    sig = {
+        "coa_init": ([ctypes.c_int], ctypes.c_int),
+        "coa_shutdown": ([], ctypes.c_int),
+        "coa_device_count": ([], ctypes.c_int),
+        "coa_last_error": ([], ctypes.c_char_p),
+        "coa_version": ([], ctypes.c_char_p),
+        "coa_ed25519_verify_strict": ([P8, P8, P8], ctypes.c_int),
+        "coa_ed25519_verify_strict_many": ([P8, sz, P8, P8, sz, P8], ctypes.c_int),
+        "coa_verify_workspace_bytes": ([sz], sz),
+        "coa_ed25519_verify_strict_many_device": ([ctypes.c_int, vp, sz, vp, vp, sz, vp, vp, vp], ctypes.c_int),
+        "coa_ed25519_verify_batch": ([P8, P8, P8, sz, ctypes.c_uint64], ctypes.c_int),
+        "coa_ed25519_verify_batch_groups": ([P8, P8, P8, P64, sz, P8, ctypes.c_uint64], ctypes.c_int),
+        "coa_ed25519_verify_batch_groups_z": ([P8, P8, P8, P64, sz, P8, P8], ctypes.c_int),
+        "coa_sha512_many": ([P8, P64, sz, P8], ctypes.c_int),
+        "coa_sha512_trunc32_many": ([P8, P64, sz, P8], ctypes.c_int),
+        "coa_sha512_many_device": ([ctypes.c_int, vp, vp, sz, vp, vp], ctypes.c_int),
+        "coa_ed25519_public_keys": ([P8, sz, P8], ctypes.c_int),
+        "coa_ed25519_sign_many": ([P8, P8, sz, sz, P8, P8], ctypes.c_int),
+        "coa_ed25519_sign_many_device": ([ctypes.c_int, vp, vp, sz, sz, vp, vp, vp], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc < 0:
+        msg = lib().coa_last_error().decode(errors="replace")
+        raise EngineError(f"{_ERRORS.get(rc, rc)}: {msg}")
+    return rc
+
+
+def _bytes_array(items, width):
+    a = np.frombuffer(b"".join(bytes(x) for x in items), dtype=np.uint8) if items else np.zeros(0, np.uint8)
+    if a.size != len(items) * width:
+        raise ValueError(f"every item must be {width} bytes")
+    return np.ascontiguousarray(a).copy()
+
+
+# --------------------------------------------------------------- the types
+class Digest:
+    """crypto::Digest -- 32 bytes (crypto/src/lib.rs:20-57)."""
+
+    __slots__ = ("data",)
+
+    def __init__(self, data=bytes(32)):
+        data = bytes(data)
+        if len(data) != 32:
+            raise ValueError("Digest is 32 bytes")
+        self.data = data
+
+    def to_vec(self):
+        return list(self.data)
+
+    def size(self):
+        return 32
+
+    def __bytes__(self):
+        return self.data
+
+    def __eq__(self, o):
+        return isinstance(o, Digest) and o.data == self.data
+
+    def __lt__(self, o):
+        return self.data < o.data
+
+    def __hash__(self):
+        return hash(self.data)
+
+    def __repr__(self):  # Debug = base64
+        return base64.b64encode(self.data).decode()
+
+    def __str__(self):  # Display = first 16 base64 chars
+        return base64.b64encode(self.data).decode()[:16]
+
+
+class PublicKey:
+    """crypto::PublicKey -- 32-byte compressed point (crypto/src/lib.rs:64-119)."""
+
+    __slots__ = ("data",)
+
+    def __init__(self, data=bytes(32)):
+        data = bytes(data)
+        if len(data) != 32:
+            raise ValueError("PublicKey is 32 bytes")
+        self.data = data
+
+    def encode_base64(self):
+        return base64.b64encode(self.data).decode()
+
+    @staticmethod
+    def decode_base64(s):
+        raw = base64.b64decode(s)
+        if len(raw) < 32:
+            raise ValueError("InvalidLength")
+        return PublicKey(raw[:32])
+
+    def __bytes__(self):
+        return self.data
+
+    def __eq__(self, o):
+        return isinstance(o, PublicKey) and o.data == self.data
+
+    def __lt__(self, o):
+        return self.data < o.data
+
+    def __hash__(self):
+        return hash(self.data)
+
+    def __repr__(self):
+        return self.encode_base64()
+
+    def __str__(self):
+        return self.encode_base64()[:16]
+
+
+class Signature:
+    """crypto::Signature {part1: R, part2: s} (crypto/src/lib.rs:177-219)."""
+
+    __slots__ = ("part1", "part2")
+
+    def __init__(self, part1=bytes(32), part2=bytes(32)):  # Default = 64 zero bytes
+        self.part1, self.part2 = bytes(part1), bytes(part2)
+        if len(self.part1) != 32 or len(self.part2) != 32:
+            raise ValueError("Signature parts are 32 bytes")
+
+    @classmethod
+    def from_bytes(cls, b):
+        b = bytes(b)
+        if len(b) != 64:
+            raise ValueError("Signature is 64 bytes")
+        return cls(b[:32], b[32:])
+
+    def flatten(self):
+        return self.part1 + self.part2
+
+    def verify(self, digest, public_key):
+        """Ok (returns None) or raises CryptoError -- Signature::verify."""
+        d = np.frombuffer(bytes(digest), np.uint8).copy()
+        pk = np.frombuffer(bytes(public_key), np.uint8).copy()
+        sg = np.frombuffer(self.flatten(), np.uint8).copy()
+        rc = _check(lib().coa_ed25519_verify_strict(_u8p(d), _u8p(pk), _u8p(sg)))
+        if rc != COA_OK:
+            raise CryptoError("signature verification failed")
+
+    @staticmethod
+    def verify_batch(digest, votes, rng_seed=0):
+        """Ok or raises CryptoError -- Signature::verify_batch over
+        (PublicKey, Signature) votes that all sign `digest`."""
+        votes = list(votes)
+        d = np.frombuffer(bytes(digest), np.uint8).copy()
+        pks = _bytes_array([bytes(pk) for pk, _ in votes], 32)
+        sgs = _bytes_array([s.flatten() for _, s in votes], 64)
+        rc = _check(lib().coa_ed25519_verify_batch(_u8p(d), _u8p(pks), _u8p(sgs), len(votes), rng_seed))
+        if rc != COA_OK:
+            raise CryptoError("batch verification failed")
+
+    def __repr__(self):
+        return f"Signature({self.flatten().hex()})"
+
+
+# ----------------------------------------------------------- engine level
+def init(n_gpus=0):
+    return _check(lib().coa_init(n_gpus))
+
+
+def device_count():
+    return _check(lib().coa_device_count())
+
+
+def verify_strict_many(msgs, pks, sigs):
+    """msgs: uint8 [n, msg_len]; pks [n, 32]; sigs [n, 64] -> uint8 verdicts
+    (0 = Ok, 1 = Err) from the HIP verify_strict kernel."""
+    msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+    pks = np.ascontiguousarray(pks, dtype=np.uint8)
+    sigs = np.ascontiguousarray(sigs, dtype=np.uint8)
+    n = pks.shape[0]
+    assert pks.shape == (n, 32) and sigs.shape == (n, 64) and msgs.shape[0] == n
+    msg_len = msgs.shape[1] if msgs.ndim == 2 else 0
+    out = np.ones(n, np.uint8)
+    _check(lib().coa_ed25519_verify_strict_many(_u8p(msgs), msg_len, _u8p(pks), _u8p(sigs), n, _u8p(out)))
+    return out
+
+
+def verify_batch_groups(msgs, pks, sigs, group_offsets, zs=None, rng_seed=0):
+    """One verdict per group (certificate).  zs: optional uint8 [n_votes, 16]
+    explicit weights (parity tests); otherwise derived from rng_seed."""
+    msgs = np.ascontiguousarray(msgs, dtype=np.uint8).reshape(-1, 32)
+    pks = np.ascontiguousarray(pks, dtype=np.uint8).reshape(-1, 32)
+    sigs = np.ascontiguousarray(sigs, dtype=np.uint8).reshape(-1, 64)
+    offs = np.ascontiguousarray(group_offsets, dtype=np.uint64)
+    ng = msgs.shape[0]
+    assert offs.shape == (ng + 1,) and int(offs[-1]) == pks.shape[0] == sigs.shape[0]
+    out = np.ones(ng, np.uint8)
+    P64 = ctypes.POINTER(ctypes.c_uint64)
+    op = offs.ctypes.data_as(P64)
+    if zs is not None:
+        zs = np.ascontiguousarray(zs, dtype=np.uint8).reshape(-1, 16)
+        assert zs.shape[0] == pks.shape[0]
+        _check(lib().coa_ed25519_verify_batch_groups_z(_u8p(msgs), _u8p(pks), _u8p(sigs), op, ng, _u8p(zs), _u8p(out)))
+    else:
+        _check(lib().coa_ed25519_verify_batch_groups(_u8p(msgs), _u8p(pks), _u8p(sigs), op, ng, _u8p(out), rng_seed))
+    return out
+
+
+def sha512_many(messages):
+    """list of bytes -> uint8 [n, 64] SHA-512 digests (HIP kernel)."""
+    n = len(messages)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum([len(m) for m in messages]) if n else []
+    data = np.frombuffer(b"".join(bytes(m) for m in messages) + b"\0", np.uint8).copy()
+    out = np.zeros((n, 64), np.uint8)
+    _check(lib().coa_sha512_many(_u8p(data), offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n, _u8p(out)))
+    return out
+
+
+def digest_many(messages):
+    """crypto::Digest of each message: Sha512(bytes)[..32]."""
+    return [Digest(bytes(r[:32])) for r in sha512_many(messages)]
+
+
+def sign_many(seeds, msgs):
+    """RFC 8032 keypairs + signatures on the device: seeds uint8 [n, 32],
+    msgs [n, msg_len] -> (pks [n, 32], sigs [n, 64])."""
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint8)
+    msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+    n = seeds.shape[0]
+    msg_len = msgs.shape[1] if msgs.ndim == 2 else 0
+    pks = np.zeros((n, 32), np.uint8)
+    sigs = np.zeros((n, 64), np.uint8)
+    _check(lib().coa_ed25519_sign_many(_u8p(seeds), _u8p(msgs), msg_len, n, _u8p(pks), _u8p(sigs)))
+    return pks, sigs
+
+
+def public_keys(seeds):
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint8)
+    n = seeds.shape[0]
+    pks = np.zeros((n, 32), np.uint8)
+    _check(lib().coa_ed25519_public_keys(_u8p(seeds), n, _u8p(pks)))
+    return pks
+
+
+# ----------------------------------------------------------- device level
+def verify_workspace_bytes(n):
+    return lib().coa_verify_workspace_bytes(n)
+
+
+def verify_strict_many_device(device, msgs, pks, sigs, verdicts, workspace=None, stream=None):
+    """Enqueue verification of HBM-resident torch uint8 tensors on `stream`
+    (a torch.cuda.Stream or raw handle; None = current torch stream)."""
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    n = pks.shape[0]
+    msg_len = msgs.shape[1] if msgs.dim() == 2 else 0
+    ws = workspace.data_ptr() if workspace is not None else None
+    _check(lib().coa_ed25519_verify_strict_many_device(device, msgs.data_ptr(), msg_len, pks.data_ptr(),
+                                                       sigs.data_ptr(), n, verdicts.data_ptr(), ws, handle))
+
+
+def sign_many_device(device, seeds, msgs, pks_out, sigs_out, stream=None):
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    n = seeds.shape[0]
+    msg_len = msgs.shape[1] if msgs.dim() == 2 else 0
+    _check(lib().coa_ed25519_sign_many_device(device, seeds.data_ptr(), msgs.data_ptr(), msg_len, n,
+                                              pks_out.data_ptr(), sigs_out.data_ptr(), handle))
+
+
+def sha512_many_device(device, data, offsets, out64, stream=None):
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    n = offsets.shape[0] - 1
+    _check(lib().coa_sha512_many_device(device, data.data_ptr(), offsets.data_ptr(), n, out64.data_ptr(), handle))
