@@ -1,0 +1,217 @@
+"""Benchmark: ed25519 verifications/sec on MI355X (BASELINE.json `metric`).
+
+Workload (N=1, BASELINE.json configs[1], "C2"): 65,536 independent
+(32 B digest, pk, sig) triples, all valid, one key per signature, per-signature
+verify (crypto::Signature::verify == dalek verify_strict).  Inputs are
+synthesised with the reference's byte formats (workloads.py), signed on the
+device, and are resident in HBM before the timed region.
+
+A step = one pass of the hot path over the batch: the challenge kernel
+(k = SHA-512(R||A||M) mod l) and the verify kernel.  With N GPUs every rank
+verifies its own 65,536 triples (weak scaling, contiguous index ranges, no
+data-path collective); value = all ranks' verifications / max-over-ranks time.
+
+Also reported:
+  roofline      the dominant kernel (k_verify_strict) against the INT32 VALU
+                issue peak; algorithmic work = the dalek algorithm's field
+                operation count (2,967 mul+sq per verify, frozen by the
+                instrumented C restatement: oracle/coa_oracle.c) x 200 INT32
+                ops per field op (SURVEY.md 8(d) cost model); its time is
+                measured here with HIP events on the stream it runs on.
+  cpu_baseline  the C restatement of dalek's algorithms (oracle/, "port")
+                on this host's cores, rank 0 at N=1 only, on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "xrpl-coa-prototype_amd")
+sys.path.insert(0, PKG)
+
+# dalek algorithm field operations per verify_strict (fe_mul + fe_sq), measured
+# by oracle/_build/libcoa_oracle_count.so over the golden valid vectors.
+FIELD_OPS_PER_VERIFY = 2967
+INT32_OPS_PER_FIELD_OP = 200
+ALG_INT32_OPS_PER_VERIFY = FIELD_OPS_PER_VERIFY * INT32_OPS_PER_FIELD_OP
+# gfx950 full-rate VALU issue: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz
+PEAK_INT32_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+C2_N = 65536
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=C2_N, help="triples per rank")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU sample")
+    return ap.parse_args()
+
+
+def cpu_baseline(msgs, pks, sigs, seconds):
+    """Oracle (C port of dalek's algorithms) on this host: all threads we may
+    use, repeated passes over the workload's first triples until `seconds`."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import coa_oracle
+
+    coa_oracle.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
+    threads = max(1, min(threads, os.cpu_count() or 1, 64))
+    chunk = min(len(pks), 4096 * threads)
+    m, p, s = msgs[:chunk], pks[:chunk], sigs[:chunk]
+    coa_oracle.verify_strict_many(m[:64], p[:64], s[:64], 1)  # table init
+    done, t0 = 0, time.perf_counter()
+    while True:
+        v = coa_oracle.verify_strict_many(m, p, s, threads)
+        assert int(v.sum()) == 0, "CPU oracle rejected a valid benchmark signature"
+        done += chunk
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    t1 = time.perf_counter()
+    one = coa_oracle.verify_strict_many(m[:2048], p[:2048], s[:2048], 1)
+    st = time.perf_counter() - t1
+    assert int(one.sum()) == 0
+    return {
+        "value": done / el,
+        "unit": "verifications/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{done} C2 triples ({done // chunk} passes over the first {chunk}) verify_strict, "
+                  f"{threads} threads, {el:.1f} s wall ({el * threads:.1f} thread-s)",
+        "single_thread_value": 2048 / st,
+    }
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import coa_crypto
+    import workloads
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    coa_crypto.init(0)
+
+    n = args.n
+    base = rank * n  # this rank's contiguous index range of the global set
+    seeds_h = workloads.key_seeds(n, start=base)
+    msgs_h = workloads.messages(n, start=base)
+    seeds = torch.from_numpy(seeds_h).to(dev)
+    msgs = torch.from_numpy(msgs_h).to(dev)
+    pks = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    sigs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    coa_crypto.sign_many_device(local, seeds, msgs, pks, sigs)
+    kbuf = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    verdicts = torch.ones(n, dtype=torch.uint8, device=dev)
+    ws = torch.empty(coa_crypto.verify_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    # an explicit stream: its handle is never NULL (NULL selects the engine's
+    # own stream in the C ABI), so the HIP events below bracket the kernels
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+
+    def step(evs=None):
+        if evs is not None:
+            evs[0].record(stream)
+        coa_crypto.challenge_many_device(local, msgs, pks, sigs, kbuf, stream)
+        if evs is not None:
+            evs[1].record(stream)
+        coa_crypto.verify_prehashed_many_device(local, kbuf, pks, sigs, verdicts, ws, stream)
+        if evs is not None:
+            evs[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ok = int(verdicts.sum().item()) == 0
+    if not ok:
+        raise SystemExit("engine rejected valid benchmark signatures")
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    hram_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    verify_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    ok = ok and int(verdicts.sum().item()) == 0
+
+    total = n * world * args.steps
+    value = total / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    achieved = ALG_INT32_OPS_PER_VERIFY * n / (verify_ms * 1e-3) / 1e12
+    traffic = None
+    tr_path = os.environ.get("COA_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r01_verify_traffic.json"))
+    if os.path.exists(tr_path):
+        try:
+            with open(tr_path) as f:
+                tj = json.load(f)
+            if tj.get("n") == n:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(msgs_h, pks.cpu().numpy(), sigs.cpu().numpy(), args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "ed25519 verifications/sec",
+            "value": round(value, 1),
+            "unit": "verifications/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded RFC 8032 keys/signatures in the reference byte formats, signed on device)",
+            "config": {"workload": "C2: 65,536 independent (32 B digest, pk, sig) triples per GPU, all valid, "
+                                   "per-signature verify_strict",
+                       "triples_per_gpu": n, "parallelism": f"index-range shards x{world}"},
+            "kernel_ms": {"k_hram": round(hram_ms, 4), "k_verify_strict": round(verify_ms, 4)},
+            "verdicts_ok": ok,
+            "roofline": {"bound": "valu-int32", "achieved": round(achieved, 3), "peak": round(PEAK_INT32_TOPS, 2),
+                         "unit": "TOPS", "frac": round(achieved / PEAK_INT32_TOPS, 4), "traffic": traffic,
+                         "kernel": "k_verify_strict",
+                         "alg_int32_ops_per_verify": ALG_INT32_OPS_PER_VERIFY},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -77,6 +77,17 @@ int coa_ed25519_verify_strict_many_device(int device, const uint8_t* d_msgs, siz
                                           const uint8_t* d_sigs, size_t n, uint8_t* d_verdicts, void* workspace,
                                           void* stream);
 
+/* The two device stages of the call above, for callers that already hold k
+ * (e.g. a digest stage fused upstream) and for per-kernel timing:
+ *   challenge:  d_k_out[i] = SHA-512(R_i || A_i || M_i) mod l, 32 bytes LE
+ *               (Scalar::from_hash inside dalek verify_strict)
+ *   prehashed:  verdicts from (k, A, R || s); workspace as above (may be NULL). */
+int coa_ed25519_challenge_many_device(int device, const uint8_t* d_msgs, size_t msg_len, const uint8_t* d_pks,
+                                      const uint8_t* d_sigs, size_t n, uint8_t* d_k_out, void* stream);
+int coa_ed25519_verify_prehashed_many_device(int device, const uint8_t* d_k, const uint8_t* d_pks,
+                                             const uint8_t* d_sigs, size_t n, uint8_t* d_verdicts, void* workspace,
+                                             void* stream);
+
 /* ------------------------------------------------- Signature::verify_batch
  * Replaces crypto::Signature::verify_batch (crypto/src/lib.rs:206-219) ->
  * ed25519_dalek::verify_batch (:218), called by Certificate::verify

@@ -1,0 +1,92 @@
+"""ctypes loader for the C oracle (oracle/coa_oracle.c) -- TEST INFRASTRUCTURE
+and CPU BASELINE ONLY.  Builds oracle/_build/*.so with gcc on first use."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "_build")
+_libs = {}
+
+
+def build():
+    src = os.path.join(HERE, "coa_oracle.c")
+    outs = [os.path.join(BUILD, n) for n in ("libcoa_oracle.so", "libcoa_oracle_count.so")]
+    if all(os.path.exists(o) and os.path.getmtime(o) >= os.path.getmtime(src) for o in outs):
+        return
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib(count=False):
+    key = "count" if count else "plain"
+    if key not in _libs:
+        build()
+        L = ctypes.CDLL(os.path.join(BUILD, "libcoa_oracle_count.so" if count else "libcoa_oracle.so"))
+        P8 = ctypes.POINTER(ctypes.c_uint8)
+        sz = ctypes.c_size_t
+        L.coa_oracle_verify_strict.argtypes = [P8, sz, P8, P8]
+        L.coa_oracle_verify_strict.restype = ctypes.c_int
+        L.coa_oracle_verify_batch.argtypes = [P8, sz, P8, P8, sz, P8]
+        L.coa_oracle_verify_batch.restype = ctypes.c_int
+        L.coa_oracle_verify_strict_many.argtypes = [P8, sz, P8, P8, sz, P8, ctypes.c_int]
+        L.coa_oracle_verify_strict_many.restype = None
+        L.coa_oracle_sha512.argtypes = [P8, sz, P8]
+        L.coa_oracle_sha512.restype = None
+        if count:
+            L.coa_oracle_counts.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 2
+            L.coa_oracle_reset_counts.argtypes = []
+        _libs[key] = L
+    return _libs[key]
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def _arr(b):
+    return np.frombuffer(bytes(b), np.uint8).copy() if len(b) else np.zeros(1, np.uint8)
+
+
+def verify_strict(msg, pk, sig, L=None):
+    L = L or lib()
+    m, p, s = _arr(msg), _arr(pk), _arr(sig)
+    return L.coa_oracle_verify_strict(_p(m), len(msg), _p(p), _p(s)) == 0
+
+
+def verify_batch(msg, pks, sigs, zs):
+    n = len(pks)
+    m = _arr(msg)
+    P = _arr(b"".join(pks)) if n else np.zeros(1, np.uint8)
+    S = _arr(b"".join(sigs)) if n else np.zeros(1, np.uint8)
+    Z = _arr(b"".join(z.to_bytes(16, "little") for z in zs)) if n else np.zeros(1, np.uint8)
+    return lib().coa_oracle_verify_batch(_p(m), len(msg), _p(P), _p(S), n, _p(Z)) == 0
+
+
+def verify_strict_many(msgs, pks, sigs, nthreads=1):
+    msgs = np.ascontiguousarray(msgs, np.uint8)
+    pks = np.ascontiguousarray(pks, np.uint8)
+    sigs = np.ascontiguousarray(sigs, np.uint8)
+    n = pks.shape[0]
+    out = np.ones(n, np.uint8)
+    lib().coa_oracle_verify_strict_many(_p(msgs), msgs.shape[1], _p(pks), _p(sigs), n, _p(out), nthreads)
+    return out
+
+
+def sha512(data):
+    d = _arr(data)
+    out = np.zeros(64, np.uint8)
+    lib().coa_oracle_sha512(_p(d), len(data), _p(out))
+    return bytes(out)
+
+
+def field_op_counts(msg, pk, sig):
+    """(fe_mul, fe_sq) count of one verify_strict in the dalek algorithm."""
+    L = lib(count=True)
+    L.coa_oracle_reset_counts()
+    m, p, s = _arr(msg), _arr(pk), _arr(sig)
+    L.coa_oracle_verify_strict(_p(m), len(msg), _p(p), _p(s))
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    L.coa_oracle_counts(ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value

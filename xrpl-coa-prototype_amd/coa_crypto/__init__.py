@@ -69,6 +69,8 @@ def lib():
         "coa_ed25519_verify_strict_many": ([P8, sz, P8, P8, sz, P8], ctypes.c_int),
         "coa_verify_workspace_bytes": ([sz], sz),
         "coa_ed25519_verify_strict_many_device": ([ctypes.c_int, vp, sz, vp, vp, sz, vp, vp, vp], ctypes.c_int),
+        "coa_ed25519_challenge_many_device": ([ctypes.c_int, vp, sz, vp, vp, sz, vp, vp], ctypes.c_int),
+        "coa_ed25519_verify_prehashed_many_device": ([ctypes.c_int, vp, vp, vp, sz, vp, vp, vp], ctypes.c_int),
         "coa_ed25519_verify_batch": ([P8, P8, P8, sz, ctypes.c_uint64], ctypes.c_int),
         "coa_ed25519_verify_batch_groups": ([P8, P8, P8, P64, sz, P8, ctypes.c_uint64], ctypes.c_int),
         "coa_ed25519_verify_batch_groups_z": ([P8, P8, P8, P64, sz, P8, P8], ctypes.c_int),
@@ -322,6 +324,29 @@ def verify_strict_many_device(device, msgs, pks, sigs, verdicts, workspace=None,
     ws = workspace.data_ptr() if workspace is not None else None
     _check(lib().coa_ed25519_verify_strict_many_device(device, msgs.data_ptr(), msg_len, pks.data_ptr(),
                                                        sigs.data_ptr(), n, verdicts.data_ptr(), ws, handle))
+
+
+def _handle(device, stream):
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+
+
+def challenge_many_device(device, msgs, pks, sigs, k_out, stream=None):
+    """k_out[i] = SHA-512(R_i || A_i || M_i) mod l (uint8 [n, 32] tensor)."""
+    n = pks.shape[0]
+    msg_len = msgs.shape[1] if msgs.dim() == 2 else 0
+    _check(lib().coa_ed25519_challenge_many_device(device, msgs.data_ptr(), msg_len, pks.data_ptr(), sigs.data_ptr(),
+                                                   n, k_out.data_ptr(), _handle(device, stream)))
+
+
+def verify_prehashed_many_device(device, k, pks, sigs, verdicts, workspace=None, stream=None):
+    n = pks.shape[0]
+    ws = workspace.data_ptr() if workspace is not None else None
+    _check(lib().coa_ed25519_verify_prehashed_many_device(device, k.data_ptr(), pks.data_ptr(), sigs.data_ptr(), n,
+                                                          verdicts.data_ptr(), ws, _handle(device, stream)))
 
 
 def sign_many_device(device, seeds, msgs, pks_out, sigs_out, stream=None):

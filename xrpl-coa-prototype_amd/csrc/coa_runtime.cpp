@@ -362,6 +362,49 @@ int coa_ed25519_verify_strict_many_device(int device, const uint8_t* d_msgs, siz
   return COA_OK;
 }
 
+int coa_ed25519_challenge_many_device(int device, const uint8_t* d_msgs, size_t msg_len, const uint8_t* d_pks,
+                                      const uint8_t* d_sigs, size_t n, uint8_t* d_k_out, void* stream) {
+  int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  if (n == 0) return COA_OK;
+  if ((!d_msgs && msg_len) || !d_pks || !d_sigs || !d_k_out) return fail(COA_EINVAL, "null argument");
+  if (check_n(n) != COA_OK) return COA_EINVAL;
+  Dev* d = dev_by_id(device);
+  if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  HIP_TRY(coa_launch_hram(d_msgs, (uint32_t)msg_len, msg_len, nullptr, d_pks, d_sigs, (uint32_t)n,
+                          reinterpret_cast<uint32_t*>(d_k_out), s));
+  return COA_OK;
+}
+
+int coa_ed25519_verify_prehashed_many_device(int device, const uint8_t* d_k, const uint8_t* d_pks,
+                                             const uint8_t* d_sigs, size_t n, uint8_t* d_verdicts, void* workspace,
+                                             void* stream) {
+  int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  if (n == 0) return COA_OK;
+  if (!d_k || !d_pks || !d_sigs || !d_verdicts) return fail(COA_EINVAL, "null argument");
+  if (check_n(n) != COA_OK) return COA_EINVAL;
+  Dev* d = dev_by_id(device);
+  if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
+  HIP_TRY(hipSetDevice(device));
+  const uint32_t lanes = verify_lanes(n);
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  const uint32_t* k = reinterpret_cast<const uint32_t*>(d_k);
+  if (workspace) {
+    uint32_t* scr = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(workspace) + align_up(n * 32, 256));
+    HIP_TRY(coa_launch_verify_strict(d_pks, d_sigs, k, (uint32_t)n, d_verdicts, scr, lanes, d->btab, s));
+    return COA_OK;
+  }
+  std::lock_guard<std::mutex> l(d->mu);
+  HIP_TRY(d->scratch.ensure((size_t)lanes * 1024));
+  HIP_TRY(coa_launch_verify_strict(d_pks, d_sigs, k, (uint32_t)n, d_verdicts, d->scratch.as<uint32_t>(), lanes,
+                                   d->btab, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return COA_OK;
+}
+
 int coa_ed25519_verify_batch_groups(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs,
                                     const uint64_t* group_offsets, size_t n_groups, uint8_t* group_verdicts_out,
                                     uint64_t rng_seed) {
