@@ -74,6 +74,54 @@ __device__ __forceinline__ void fe_sq_asm(fe& r, const fe& a) {
   t[15] = (uint32_t)acc;
   fe_reduce512(r, t);
 }
+
+__device__ __forceinline__ void mac0(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
+  uint64_t sc;
+  asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32 %2, %1, 0, 0, %1"
+      : "+v"(acc), "=&s"(sc), "=v"(c2) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void fe_mul_asm2(fe& r, const fe& a, const fe& b) {
+  uint32_t t[16];
+  uint64_t acc = 0; uint32_t c2 = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+    bool first = true;
+#pragma unroll
+    for (int i = 0; i < 8; i++) { int j = k - i; if (j < 0 || j > 7) continue;
+      if (first) { mac0(acc, c2, a.v[i], b.v[j]); first = false; } else mac(acc, c2, a.v[i], b.v[j]); }
+    t[k] = (uint32_t)acc; acc = (acc >> 32) | ((uint64_t)c2 << 32);
+  }
+  t[15] = (uint32_t)acc;
+  fe_reduce512(r, t);
+}
+__device__ __forceinline__ uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t& cout) {
+  unsigned int c; uint32_t r = __builtin_addc(a, b, cin, &c); cout = c; return r;
+}
+__device__ __forceinline__ void fe_sq2(fe& r, const fe& a) {
+  uint32_t t[16];
+  t[0] = 0;
+  uint64_t acc = 0; uint32_t c2 = 0;
+#pragma unroll
+  for (int k = 1; k < 14; k++) {
+    bool first = true;
+#pragma unroll
+    for (int i = 0; i < 8; i++) { int j = k - i; if (j <= i || j > 7) continue;
+      if (first) { mac0(acc, c2, a.v[i], a.v[j]); first = false; } else mac(acc, c2, a.v[i], a.v[j]); }
+    t[k] = (uint32_t)acc; acc = (acc >> 32) | ((uint64_t)c2 << 32);
+  }
+  t[14] = (uint32_t)acc; t[15] = (uint32_t)(acc >> 32);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = addc32(t[i], t[i], c, c);
+  uint32_t d[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { uint64_t p = (uint64_t)a.v[i] * a.v[i]; d[2*i] = (uint32_t)p; d[2*i+1] = (uint32_t)(p >> 32); }
+  c = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = addc32(t[i], d[i], c, c);
+  fe_reduce512(r, t);
+}
+
 template <int V>
 __global__ void k(fe* x, int n) {
   int id = blockIdx.x * blockDim.x + threadIdx.x;
@@ -83,6 +131,8 @@ __global__ void k(fe* x, int n) {
     if (V == 1) fe_mul_c(a, a, b);
     if (V == 2) fe_mul_os(a, a, b);
     if (V == 3) fe_sq_asm(a, a);
+    if (V == 4) fe_mul_asm2(a, a, b);
+    if (V == 5) fe_sq2(a, a);
   }
   x[id] = a;
 }
@@ -119,17 +169,17 @@ int main() {
   for (int i = 0; i < nthreads; i++) for (int j = 0; j < 8; j++) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; h0[i].v[j] = (uint32_t)s; }
   for (int i = 0; i < 64; i++) { for (int j = 0; j < 8; j++) h0[i].v[j] = 0xffffffffu; } // extremes
   fe* d; hipMalloc(&d, sizeof(fe) * nthreads);
-  void (*ks[4])(fe*, int) = {k<0>, k<1>, k<2>, k<3>};
-  const char* names[4] = {"mul_asm_comba", "mul_c_comba", "mul_operand_scan", "sq_asm_comba"};
+  void (*ks[6])(fe*, int) = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>};
+  const char* names[6] = {"mul_asm_comba", "mul_c_comba", "mul_operand_scan", "sq_asm_comba", "mul_asm2", "sq2"};
   // correctness with n=3
-  for (int v = 0; v < 4; v++) {
+  for (int v = 0; v < 6; v++) {
     hipMemcpy(d, h0, sizeof(fe) * nthreads, hipMemcpyHostToDevice);
     hipLaunchKernelGGL(ks[v], dim3(nthreads / 256), dim3(256), 0, 0, d, 3);
     hipMemcpy(h, d, sizeof(fe) * nthreads, hipMemcpyDeviceToHost);
     int bad = 0;
     for (int i = 0; i < 4096; i++) {
       uint32_t a[8], b[8]; for (int j=0;j<8;j++){a[j]=h0[i].v[j]; b[j]=h0[i^1].v[j];}
-      for (int r = 0; r < 3; r++) { uint32_t t[8]; if (v==3) ref_mul(t, a, a); else ref_mul(t, a, b); for (int j=0;j<8;j++) a[j]=t[j]; }
+      for (int r = 0; r < 3; r++) { uint32_t t[8]; if (v==3 || v==5) ref_mul(t, a, a); else ref_mul(t, a, b); for (int j=0;j<8;j++) a[j]=t[j]; }
       uint32_t g[8]; for (int j=0;j<8;j++) g[j]=h[i].v[j]; canon(g);
       for (int j=0;j<8;j++) if (g[j]!=a[j]) { bad++; break; }
     }
@@ -137,7 +187,7 @@ int main() {
   }
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   const int N = 2000;
-  for (int v = 0; v < 4; v++) {
+  for (int v = 0; v < 6; v++) {
     hipLaunchKernelGGL(ks[v], dim3(nthreads / 256), dim3(256), 0, 0, d, 10); hipDeviceSynchronize();
     hipEventRecord(e0);
     hipLaunchKernelGGL(ks[v], dim3(nthreads / 256), dim3(256), 0, 0, d, N);

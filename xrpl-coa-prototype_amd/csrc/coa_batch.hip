@@ -33,15 +33,16 @@
 
 namespace {
 
-// per-lane tables j·P (j = 1..8) for two bases, cached form, lane-contiguous:
-//   uint4 index = ((tab * 64 + entry * 8 + quad) * lanes + lane)
+// per-lane tables j·P (j = 1..8) for two bases, cached form, lane-major
+// (2 KiB per lane; one 128-byte line per lookup, as in coa_kernels.hip):
+//   uint4 index = ((lane * 16 + tab * 8 + entry) * 8 + quad)
 COA_DEV void tab_store(uint32_t* scr, uint32_t lanes, uint32_t lane, int tab, int entry, const ge_cached& q) {
   const fe* f[4] = {&q.YplusX, &q.YminusX, &q.Z, &q.T2d};
 #pragma unroll
   for (int c = 0; c < 4; c++)
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-      uint4* dst = reinterpret_cast<uint4*>(scr) + ((uint64_t)(tab * 64 + entry * 8 + c * 2 + h) * lanes + lane);
+      uint4* dst = reinterpret_cast<uint4*>(scr) + (((uint64_t)lane * 16 + tab * 8 + entry) * 8 + c * 2 + h);
       *dst = make_uint4(f[c]->v[4 * h], f[c]->v[4 * h + 1], f[c]->v[4 * h + 2], f[c]->v[4 * h + 3]);
     }
 }
@@ -55,7 +56,7 @@ COA_DEV void tab_select(ge_cached& q, const uint32_t* scr, uint32_t lanes, uint3
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const uint4 v =
-          reinterpret_cast<const uint4*>(scr)[(uint64_t)(tab * 64 + entry * 8 + c * 2 + h) * lanes + lane];
+          reinterpret_cast<const uint4*>(scr)[((uint64_t)lane * 16 + tab * 8 + entry) * 8 + c * 2 + h];
       f[c]->v[4 * h] = v.x;
       f[c]->v[4 * h + 1] = v.y;
       f[c]->v[4 * h + 2] = v.z;
@@ -166,7 +167,7 @@ __global__ void __launch_bounds__(256) k_batch_z(const uint32_t* __restrict__ kb
 }
 
 // Per vote: flag (1 = valid encoding), P = [z]R + [z·h mod l]A + [-(z·s) mod l]B.
-__global__ void __launch_bounds__(BATCH_BLOCK) k_batch_terms(const uint8_t* __restrict__ pks,
+__global__ void __launch_bounds__(BATCH_BLOCK, 2) k_batch_terms(const uint8_t* __restrict__ pks,
                                                              const uint8_t* __restrict__ sigs,
                                                              const uint32_t* __restrict__ kbuf,
                                                              const uint32_t* __restrict__ zs, uint32_t n,

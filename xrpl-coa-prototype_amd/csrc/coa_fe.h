@@ -12,7 +12,8 @@
 // them per schoolbook product beat the 100 of a 10 x 25.5-bit layout.  The
 // column (comba) accumulation keeps a 96-bit accumulator (64-bit pair + carry
 // word) and takes the mad's own carry-out, so each partial product costs one
-// v_mad_u64_u32 + one v_addc_co_u32.
+// v_mad_u64_u32 + one v_addc_co_u32 (tools/ubench_fe.hip: 214 VALU
+// instructions per multiply, 176 per squaring; profiles/r01_ubench_fe*.txt).
 //
 // Reduction uses 2^256 == 38 (mod p).
 #pragma once
@@ -46,6 +47,16 @@ COA_DEV void mac(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
   asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
       "v_addc_co_u32 %2, %1, %2, 0, %1"
       : "+v"(acc), "=&s"(sc), "+v"(c2)
+      : "v"(a), "v"(b));
+}
+
+// First product of a column: the carry word starts from the mad's carry-out
+// instead of a separately zeroed register.
+COA_DEV void mac0(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
+  uint64_t sc;
+  asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
+      "v_addc_co_u32 %2, %1, 0, 0, %1"
+      : "+v"(acc), "=&s"(sc), "=v"(c2)
       : "v"(a), "v"(b));
 }
 
@@ -113,45 +124,58 @@ COA_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
   uint32_t c2 = 0;
 #pragma unroll
   for (int k = 0; k < 15; k++) {
+    bool first = true;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = k - i;
       if (j < 0 || j > 7) continue;
-      mac(acc, c2, a.v[i], b.v[j]);
+      if (first) mac0(acc, c2, a.v[i], b.v[j]);
+      else mac(acc, c2, a.v[i], b.v[j]);
+      first = false;
     }
     t[k] = (uint32_t)acc;
     acc = (acc >> 32) | ((uint64_t)c2 << 32);
-    c2 = 0;
   }
   t[15] = (uint32_t)acc;
   fe_reduce512(r, t);
 }
 
-// Squaring: each cross product once, the column doubled, the diagonal added.
+// Squaring: the 28 cross products by comba, doubled with one carry chain,
+// then the 8 squares added with a second chain (44 mads vs 72 for fe_mul).
 COA_DEV void fe_sq(fe& r, const fe& a) {
   uint32_t t[16];
+  t[0] = 0;
   uint64_t acc = 0;
   uint32_t c2 = 0;
 #pragma unroll
-  for (int k = 0; k < 15; k++) {
-    uint64_t x = 0;
-    uint32_t x2 = 0;
+  for (int k = 1; k < 14; k++) {
+    bool first = true;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = k - i;
       if (j <= i || j > 7) continue;
-      mac(x, x2, a.v[i], a.v[j]);
+      if (first) mac0(acc, c2, a.v[i], a.v[j]);
+      else mac(acc, c2, a.v[i], a.v[j]);
+      first = false;
     }
-    x2 = (x2 << 1) | (uint32_t)(x >> 63);
-    x <<= 1;
-    if ((k & 1) == 0) mac(x, x2, a.v[k >> 1], a.v[k >> 1]);
-    uint64_t s = acc + x;
-    x2 += c2 + (s < x ? 1u : 0u);
-    t[k] = (uint32_t)s;
-    acc = (s >> 32) | ((uint64_t)x2 << 32);
-    c2 = 0;
+    t[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)c2 << 32);
   }
-  t[15] = (uint32_t)acc;
+  t[14] = (uint32_t)acc;
+  t[15] = (uint32_t)(acc >> 32);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = addc32(t[i], t[i], c, c);
+  uint32_t d[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t p = (uint64_t)a.v[i] * a.v[i];
+    d[2 * i] = (uint32_t)p;
+    d[2 * i + 1] = (uint32_t)(p >> 32);
+  }
+  c = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = addc32(t[i], d[i], c, c);
   fe_reduce512(r, t);
 }
 

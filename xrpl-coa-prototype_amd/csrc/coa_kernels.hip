@@ -145,10 +145,13 @@ __global__ void __launch_bounds__(256) k_hram(const uint8_t* __restrict__ msgs, 
 }
 
 // ---------------------------------------------------------------------------
-// Per-lane table of j·(-A), j = 1..8, in cached form: 8 entries x 32 dwords,
-// stored in a global scratch slab with a lane-contiguous layout so that each
-// dwordx4 access of a wave is one 1 KiB coalesced transaction:
-//   dword index = ((entry * 8 + quad) * lanes + lane) * 4
+// Per-lane table of j·(-A), j = 1..8, in cached form: 8 entries x 32 dwords
+// in a global scratch slab, lane-major: lane L's table is the 1 KiB at
+// L * 1024 and entry e is the 128-byte line at + e * 128.  Lookups are
+// data-dependent per lane, so this makes every lookup exactly one fully used
+// cache line (an entry-major layout made each wave instruction touch up to 8
+// rows: ~5x the fabric traffic, profiles/r01_v0_verify_traffic.json).
+//   uint4 index = (lane * 8 + entry) * 8 + quad
 // ---------------------------------------------------------------------------
 COA_DEV void atab_store(uint32_t* __restrict__ scr, uint32_t lanes, uint32_t lane, int entry,
                         const ge_cached& q) {
@@ -158,7 +161,7 @@ COA_DEV void atab_store(uint32_t* __restrict__ scr, uint32_t lanes, uint32_t lan
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int quad = c * 2 + h;
-      uint4* dst = reinterpret_cast<uint4*>(scr) + ((uint64_t)(entry * 8 + quad) * lanes + lane);
+      uint4* dst = reinterpret_cast<uint4*>(scr) + (((uint64_t)lane * 8 + entry) * 8 + quad);
       *dst = make_uint4(f[c]->v[4 * h], f[c]->v[4 * h + 1], f[c]->v[4 * h + 2], f[c]->v[4 * h + 3]);
     }
   }
@@ -174,7 +177,7 @@ COA_DEV void atab_select(ge_cached& q, const uint32_t* __restrict__ scr, uint32_
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int quad = c * 2 + h;
-      const uint4 v = reinterpret_cast<const uint4*>(scr)[(uint64_t)(entry * 8 + quad) * lanes + lane];
+      const uint4 v = reinterpret_cast<const uint4*>(scr)[((uint64_t)lane * 8 + entry) * 8 + quad];
       f[c]->v[4 * h] = v.x;
       f[c]->v[4 * h + 1] = v.y;
       f[c]->v[4 * h + 2] = v.z;
@@ -234,7 +237,7 @@ COA_DEV void double_scalar_mul(ge_p2& out, const uint32_t* kk, const uint32_t* s
 // crypto::Signature::verify == dalek 1.0.1 verify_strict, one lane per
 // signature.  verdict 0 = Ok, 1 = Err.  k_in from k_hram.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_verify_strict(const uint8_t* __restrict__ pks,
+__global__ void __launch_bounds__(256, 2) k_verify_strict(const uint8_t* __restrict__ pks,
                                                        const uint8_t* __restrict__ sigs,
                                                        const uint32_t* __restrict__ k_in, uint32_t n,
                                                        uint8_t* __restrict__ verdicts, uint32_t* __restrict__ scr,
