@@ -96,6 +96,7 @@ def main():
     import torch.distributed as dist
 
     import coa_crypto
+    import sharding
     import workloads
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,7 +111,7 @@ def main():
     coa_crypto.init(0)
 
     n = args.n
-    base = rank * n  # this rank's contiguous index range of the global set
+    base, _ = sharding.rank_slice(rank, world, n)  # this rank's contiguous index range
     seeds_h = workloads.key_seeds(n, start=base)
     msgs_h = workloads.messages(n, start=base)
     seeds = torch.from_numpy(seeds_h).to(dev)
@@ -156,10 +157,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = sharding.max_over_ranks(elapsed, dist, dev)
     hram_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     verify_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     ok = ok and int(verdicts.sum().item()) == 0

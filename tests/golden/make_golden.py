@@ -307,6 +307,23 @@ def batch_vectors():
     return groups
 
 
+def mixed_order_pool(n=64):
+    """Class 8 of SURVEY 8(d): mixed-order A = aB + T8 with a torsion-matched
+    R; dalek verify_strict ACCEPTS these.  Used to seed large adversarial
+    mixes (workloads.adversarial_mix) whose expected verdicts come from the
+    oracle."""
+    rng = random.Random(0x8888)
+    T8 = torsion_gen()
+    out = []
+    for i in range(n):
+        seed = H(b"coa-mixed" + struct.pack("<Q", i))[:32]
+        m = H(b"coa-mixed-msg" + struct.pack("<Q", i))[:32]
+        Ab, sg = mixed_order_signature(seed, m, T8, rng)
+        assert o.verify_strict(m, Ab, sg) and sodium_verify(m, Ab, sg)
+        out.append({"msg": m.hex(), "pk": Ab.hex(), "sig": sg.hex()})
+    return out
+
+
 def sha_vectors():
     rng = random.Random(0x5A5A)
     out = []
@@ -322,6 +339,7 @@ def main():
         "verify_vectors.json": verify_vectors(),
         "batch_vectors.json": batch_vectors(),
         "sha512_vectors.json": sha_vectors(),
+        "mixed_order_pool.json": mixed_order_pool(),
     }
     for name, data in files.items():
         with open(os.path.join(HERE, name), "w") as f:
