@@ -54,3 +54,19 @@ def test_adversarial_device_path(engine):
     engine.verify_strict_many_device(0, t[0], t[1], t[2], out, ws, s)
     s.synchronize()
     assert (out.cpu().numpy() == exp).all()
+
+
+@pytest.mark.parametrize("impl", ["halved", "full"])
+def test_both_verify_kernels_agree(engine, impl, monkeypatch):
+    """The halved-scalar kernel (default) and the full-length kernel
+    (COA_VERIFY_IMPL=full) both match the oracle on the same adversarial mix."""
+    from workloads import adversarial_mix, key_seeds, messages
+
+    if impl == "full":
+        monkeypatch.setenv("COA_VERIFY_IMPL", "full")
+    n = 20_000
+    pks, sigs = engine.sign_many(key_seeds(n, 7), messages(n, 7))
+    msgs, pks, sigs, cls = adversarial_mix(messages(n, 7), pks, sigs, frac=0.05, seed=77, mixed_pool=_pool())
+    got = engine.verify_strict_many(msgs, pks, sigs)
+    exp = co.verify_strict_many(msgs, pks, sigs, min(16, os.cpu_count() or 1))
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]

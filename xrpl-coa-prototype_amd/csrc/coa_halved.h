@@ -1,0 +1,18 @@
+// Internal launch wrappers for the halved-scalar verification path
+// (coa_halved.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define COA_COMB_ENTRIES (32 * 128)
+#define COA_COMB_DWORDS (COA_COMB_ENTRIES * 24)
+// k_halve record per signature: c[8] | |d|[8] | e[8] | meta | pad[7]
+#define COA_HALVE_REC_BYTES 128
+// per-lane scratch of k_verify_halved: j*(-A) and j*(-/+R), 8 entries each
+#define COA_HALVED_SCRATCH_PER_LANE 2048
+
+hipError_t coa_launch_build_comb(uint32_t* comb, const uint32_t* btab, hipStream_t s);
+hipError_t coa_launch_halve(const uint32_t* kbuf, const uint8_t* sigs, uint32_t n, uint32_t* rec, hipStream_t s);
+hipError_t coa_launch_verify_halved(const uint8_t* pks, const uint8_t* sigs, const uint32_t* rec, uint32_t n,
+                                    uint8_t* verdicts, uint32_t* scratch, uint32_t scratch_lanes,
+                                    const uint32_t* comb, hipStream_t s);

@@ -1,0 +1,523 @@
+// Halved-scalar per-signature verification (crypto::Signature::verify ==
+// ed25519-dalek 1.0.1 verify_strict, crypto/src/lib.rs:200-204) for gfx950.
+//
+// dalek checks P := [s]B - [k]A - R == O.  We check instead
+//     Q := [e]B - [c]A - [d]R == O,   e = d*s mod l,
+// where (c, d) is a short vector of the lattice {(c, d) : c == d*k (mod 8l)}
+// with d odd (k_halve: a half-gcd on (8l, k) by the extended Euclidean
+// algorithm with f64 quotient estimates).  Because A and R lie in
+// a group of order 8l, [c]A == [d*k]A and [d*s mod l]B == [d*s]B exactly, so
+// Q == [d]P for EVERY input, torsion components included; d odd and
+// 0 < |d| < l make [d]P == O equivalent to P == O.  The verdict is therefore
+// dalek's bit for bit, while c and d have ~128 bits instead of 253: the joint
+// Horner pass needs ~33 signed radix-16 digits (132 doublings) instead of 64,
+// and [e]B uses a doubling-free comb (32 byte positions x 128 multiples).
+// When no short odd vector exists (adversarially ground k), k_halve falls
+// back to (c, d) = (k, 1) -- the full-length check -- so correctness never
+// depends on the reduction succeeding.
+//
+// Kernels:
+//   k_build_comb     comb table: entry (j, v) = (v+1)*256^j*B, affine Niels
+//   k_halve          (k, s) -> (c, |d|, e, H, sign d)
+//   k_verify_halved  decompression + small-order checks + Q == O
+#include "coa_halved.h"
+#include "coa_kernels.h"
+
+#include "coa_fe.h"
+#include "coa_ge.h"
+#include "coa_sc.h"
+#include "coa_smul.h"
+
+namespace {
+
+// ---------------------------------------------------------------- bigints
+COA_DEV int bitlen(const uint32_t* x, int nl) {
+  int bl = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if (i < nl) bl = x[i] ? 32 * i + 32 - __builtin_clz(x[i]) : bl;
+  return bl;
+}
+
+// out = x << s (0 <= s < 256), 8 limbs, bits above 256 dropped.
+COA_DEV void shl8(uint32_t* out, const uint32_t* x, int s) {
+  uint32_t t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = x[i];
+  const int q = s >> 5;
+#pragma unroll
+  for (int st = 1; st < 8; st <<= 1) {
+    const bool on = (q & st) != 0;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) t[i] = on ? (i >= st ? t[i - st] : 0u) : t[i];
+  }
+  const int r = s & 31;
+#pragma unroll
+  for (int i = 7; i >= 0; i--) {
+    const uint32_t lo = i ? t[i - 1] : 0u;
+    out[i] = r ? __builtin_amdgcn_alignbit(t[i], lo, 32 - r) : t[i];
+  }
+}
+
+COA_DEV void shr1_8(uint32_t* x) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[i] = __builtin_amdgcn_alignbit(i < 7 ? x[i + 1] : 0u, x[i], 1);
+}
+
+COA_DEV uint32_t sub8(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+  uint32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r[i] = subb32(a[i], b[i], bw, bw);
+  return bw;
+}
+COA_DEV uint32_t add8(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r[i] = addc32(a[i], b[i], c, c);
+  return c;
+}
+
+COA_DEV double to_f64(const uint32_t* x) {
+  double d = (double)x[7];
+#pragma unroll
+  for (int i = 6; i >= 0; i--) d = fma(d, 4294967296.0, (double)x[i]);
+  return d;
+}
+
+// r = a - q*b (mod 2^288); returns the borrow (1 if a < q*b).
+COA_DEV uint32_t submul8(uint32_t* r, const uint32_t* a, const uint32_t* b, uint32_t q) {
+  uint32_t pr[9];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    acc = (uint64_t)b[i] * q + (acc >> 32);
+    pr[i] = (uint32_t)acc;
+  }
+  pr[8] = (uint32_t)(acc >> 32);
+  uint32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r[i] = subb32(a[i], pr[i], bw, bw);
+  uint32_t top = subb32(0u, pr[8], bw, bw);
+  (void)top;
+  return bw;
+}
+
+COA_DEV void madd5(uint32_t* r, const uint32_t* a, const uint32_t* b, uint32_t q) {  // r = a + q*b
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    acc = (uint64_t)b[i] * q + a[i] + (acc >> 32);
+    r[i] = (uint32_t)acc;
+  }
+}
+
+// Track the best lattice vector (c, t) with t odd: cost = max(bits(c), bits(t)).
+COA_DEV void consider(uint32_t* c_out, uint32_t* d_out, int& best, bool& best_neg, const uint32_t* c,
+                      const uint32_t* t, bool neg) {
+  if (!(t[0] & 1)) return;
+  const int cost = max(bitlen(c, 8), bitlen(t, 8));
+  if (cost < best) {
+    best = cost;
+    best_neg = neg;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      c_out[i] = c[i];
+      d_out[i] = t[i];
+    }
+  }
+}
+
+// Half-gcd on (8l, k) by the extended Euclidean algorithm: remainders
+// r_i == t_i * k (mod 8l) with |r_{i-1} t_i| + |r_i t_{i-1}| = 8l, so once
+// r_i < 2^128, |t_i| <= 2^127.  Quotients come from an f64 estimate of a/b
+// (exact to 2^-52 relative) corrected by at most a few exact add-backs; a
+// quotient >= 2^31 (probability ~2^-31 per step) takes a shift-subtract
+// step instead.  Returns the lattice vector (c, |d|, sign d) with d odd that
+// minimises max(bits(c), bits(d)) among the last remainders and their
+// neighbours; (k, 1) if none is shorter.
+COA_DEV void halve(uint32_t* c_out, uint32_t* d_out, int& cost_out, bool& neg_out, const uint32_t* k) {
+  uint32_t a[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0, 0, 0, 0x80000000u};  // 8l
+  uint32_t b[8], ma[8], mb[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    b[i] = k[i];
+    ma[i] = 0;
+    mb[i] = i == 0 ? 1u : 0u;
+    c_out[i] = k[i];
+    d_out[i] = i == 0 ? 1u : 0u;
+  }
+  bool tb_neg = false;  // sign of t_b; t_a has the opposite sign
+  int best = max(bitlen(k, 8), 1);
+  bool best_neg = false;
+  for (int guard = 0; guard < 400; guard++) {
+    const int lb = bitlen(b, 8);
+    if (lb <= 118) break;
+    const double qd = floor(to_f64(a) / to_f64(b));
+    uint32_t r[8], mr[8];
+    if (qd < 2147483648.0) {
+      uint32_t q = (uint32_t)qd;
+      if (submul8(r, a, b, q)) {  // overestimated: add b back (at most twice)
+#pragma unroll 1
+        for (int fix = 0; fix < 2; fix++) {
+          uint32_t c = 0;
+#pragma unroll
+          for (int i = 0; i < 8; i++) r[i] = addc32(r[i], b[i], c, c);
+          q -= 1;
+          if (c) break;  // crossed back to >= 0
+        }
+      }
+      uint32_t tmp[8];
+#pragma unroll 1
+      for (int fix = 0; fix < 2; fix++) {  // underestimated: r >= b
+        if (sub8(tmp, r, b)) break;
+#pragma unroll
+        for (int i = 0; i < 8; i++) r[i] = tmp[i];
+        q += 1;
+      }
+      madd5(mr, ma, mb, q);
+    } else {  // huge quotient: one shift-subtract step, keep a as the larger
+      const int s = bitlen(a, 8) - lb - 1;
+      uint32_t t[8], u[8];
+      shl8(t, b, s);
+      (void)sub8(r, a, t);
+      shl8(u, mb, s);
+      (void)add8(mr, ma, u);
+      uint32_t tmp[8];
+      if (!sub8(tmp, r, b)) {  // still >= b: stay, the next step continues on (r, b)
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          a[i] = r[i];
+          ma[i] = mr[i];
+        }
+        continue;
+      }
+    }
+    // (a, b) <- (b, r); t_r = t_a - q t_b has the sign of t_a
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      a[i] = b[i];
+      ma[i] = mb[i];
+      b[i] = r[i];
+      mb[i] = mr[i];
+    }
+    tb_neg = !tb_neg;
+    if (bitlen(b, 8) <= 136) {
+      consider(c_out, d_out, best, best_neg, b, mb, tb_neg);
+      consider(c_out, d_out, best, best_neg, a, ma, !tb_neg);
+      if ((ma[0] ^ mb[0]) & 1) {
+        uint32_t cd[8], dd[8];
+        (void)sub8(cd, a, b);
+        (void)add8(dd, ma, mb);
+        consider(c_out, d_out, best, best_neg, cd, dd, !tb_neg);
+      }
+    }
+  }
+  cost_out = best;
+  neg_out = best_neg;
+}
+
+// per-lane tables j*P, j = 1..8, for two bases; lane-major, 2 KiB per lane
+COA_DEV void tab2_store(uint32_t* scr, uint32_t lane, int tab, int entry, const ge_cached& q) {
+  const fe* f[4] = {&q.YplusX, &q.YminusX, &q.Z, &q.T2d};
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+      reinterpret_cast<uint4*>(scr)[((uint64_t)lane * 16 + tab * 8 + entry) * 8 + c * 2 + h] =
+          make_uint4(f[c]->v[4 * h], f[c]->v[4 * h + 1], f[c]->v[4 * h + 2], f[c]->v[4 * h + 3]);
+}
+
+COA_DEV void tab2_select(ge_cached& q, const uint32_t* scr, uint32_t lane, int tab, int d) {
+  const int m = d < 0 ? -d : d;
+  const int entry = m == 0 ? 0 : m - 1;
+  fe* f[4] = {&q.YplusX, &q.YminusX, &q.Z, &q.T2d};
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint4 v = reinterpret_cast<const uint4*>(scr)[((uint64_t)lane * 16 + tab * 8 + entry) * 8 + c * 2 + h];
+      f[c]->v[4 * h] = v.x;
+      f[c]->v[4 * h + 1] = v.y;
+      f[c]->v[4 * h + 2] = v.z;
+      f[c]->v[4 * h + 3] = v.w;
+    }
+  if (m == 0) ge_cached_identity(q);
+  ge_cached_cneg(q, d < 0);
+}
+
+COA_DEV void tab2_build(uint32_t* scr, uint32_t lane, int tab, const ge_p3& P) {
+  ge_cached c1;
+  ge_p3_to_cached(c1, P);
+  tab2_store(scr, lane, tab, 0, c1);
+  ge_p3 cur = P;
+#pragma unroll 1
+  for (int j = 1; j < 8; j++) {
+    ge_p1p1 t;
+    ge_add(t, cur, c1);
+    ge_p1p1_to_p3(cur, t);
+    ge_cached cj;
+    ge_p3_to_cached(cj, cur);
+    tab2_store(scr, lane, tab, j, cj);
+  }
+}
+
+COA_DEV int wave_max(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// Comb entry (j, |e|): signed radix-256 digit e of byte position j -> ±|e|*256^j*B.
+COA_DEV void comb_select(ge_niels& q, const uint32_t* __restrict__ comb, int j, int e) {
+  const int m = e < 0 ? -e : e;
+  const int idx = m == 0 ? 0 : m - 1;
+  const uint4* src = reinterpret_cast<const uint4*>(comb + ((uint64_t)j * 128 + idx) * 24);
+  uint32_t w[24];
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    const uint4 v = src[i];
+    w[4 * i] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    q.yplusx.v[i] = w[i];
+    q.yminusx.v[i] = w[8 + i];
+    q.xy2d.v[i] = w[16 + i];
+  }
+  if (m == 0) ge_niels_identity(q);
+  ge_niels_cneg(q, e < 0);
+}
+
+COA_DEV uint32_t take_low_byte(uint32_t* x) {
+  const uint32_t lo = x[0] & 0xffu;
+#pragma unroll
+  for (int i = 0; i < 7; i++) x[i] = __builtin_amdgcn_alignbit(x[i + 1], x[i], 8);
+  x[7] >>= 8;
+  return lo;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_build_comb(uint32_t* __restrict__ comb, const uint32_t* __restrict__ btab_g) {
+  __shared__ __attribute__((aligned(16))) uint32_t btab[BTAB_DWORDS];
+  lds_load_btable(btab, btab_g);
+  const int id = blockIdx.x * blockDim.x + threadIdx.x;  // 0 .. 4095
+  const int j = id >> 7, v = id & 127;
+  uint32_t wide[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) wide[i] = 0;
+  // (v + 1) << (8 j) as a 512-bit value, reduced mod l
+  const int bitpos = 8 * j;
+  const uint64_t m = (uint64_t)(v + 1) << (bitpos & 31);
+  for (int i = 0; i < 16; i++) {
+    if (i == (bitpos >> 5)) wide[i] = (uint32_t)m;
+    if (i == (bitpos >> 5) + 1) wide[i] = (uint32_t)(m >> 32);
+  }
+  sc x;
+  sc_reduce512(x, wide);
+  ge_p2 P;
+  fixed_base_mul(P, x.v, btab);
+  fe zi, xx, yy, xy, d2, n0, n1, n2;
+  fe_invert(zi, P.Z);
+  fe_mul(xx, P.X, zi);
+  fe_mul(yy, P.Y, zi);
+  fe_mul(xy, xx, yy);
+  fe_const_d2(d2);
+  fe_add(n0, yy, xx);
+  fe_sub(n1, yy, xx);
+  fe_mul(n2, xy, d2);
+  fe_canon(n0, n0);
+  fe_canon(n1, n1);
+  fe_canon(n2, n2);
+  uint32_t* e = comb + (uint64_t)id * 24;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    e[i] = n0.v[i];
+    e[8 + i] = n1.v[i];
+    e[16 + i] = n2.v[i];
+  }
+}
+
+// (k, s) -> record {c'[8], d'[8], e[8], meta, pad[7]}: c' = c + 0x88..8,
+// d' = |d| + 0x88..8 (signed radix-16 recodings), meta = H | (d < 0) << 31.
+__global__ void __launch_bounds__(256) k_halve(const uint32_t* __restrict__ kbuf, const uint8_t* __restrict__ sigs,
+                                               uint32_t n, uint32_t* __restrict__ rec) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint32_t k[8], s[8];
+    const uint4* kq = reinterpret_cast<const uint4*>(kbuf + (uint64_t)i * 8);
+    const uint4* sq = reinterpret_cast<const uint4*>(sigs + (uint64_t)i * 64 + 32);
+    uint4 v0 = kq[0], v1 = kq[1];
+    k[0] = v0.x; k[1] = v0.y; k[2] = v0.z; k[3] = v0.w;
+    k[4] = v1.x; k[5] = v1.y; k[6] = v1.z; k[7] = v1.w;
+    v0 = sq[0];
+    v1 = sq[1];
+    s[0] = v0.x; s[1] = v0.y; s[2] = v0.z; s[3] = v0.w;
+    s[4] = v1.x; s[5] = v1.y; s[6] = v1.z; s[7] = v1.w;
+    uint32_t c[8], d[8];
+    int cost;
+    bool neg;
+    halve(c, d, cost, neg, k);
+    sc e;
+    sc_mul(e, d, s);  // s may be non-canonical here; the verify kernel rejects those lanes
+    if (neg) {
+      sc en;
+      sc_neg(en, e.v);
+      e = en;
+    }
+    const int H = (cost + 2 + 3) / 4;  // c, d < 2^(4H - 2)
+    // signed radix-16 recoding offset over all 64 nibbles: nibble p of
+    // c + 0x88..8 minus 8 is digit p, and every digit at p >= H is 0
+    add_const_word(c, 0x88888888u);
+    add_const_word(d, 0x88888888u);
+    uint4* o = reinterpret_cast<uint4*>(rec + (uint64_t)i * 32);
+    o[0] = make_uint4(c[0], c[1], c[2], c[3]);
+    o[1] = make_uint4(c[4], c[5], c[6], c[7]);
+    o[2] = make_uint4(d[0], d[1], d[2], d[3]);
+    o[3] = make_uint4(d[4], d[5], d[6], d[7]);
+    o[4] = make_uint4(e.v[0], e.v[1], e.v[2], e.v[3]);
+    o[5] = make_uint4(e.v[4], e.v[5], e.v[6], e.v[7]);
+    o[6] = make_uint4((uint32_t)H | (neg ? 0x80000000u : 0u), 0, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(256, 2) k_verify_halved(const uint8_t* __restrict__ pks,
+                                                          const uint8_t* __restrict__ sigs,
+                                                          const uint32_t* __restrict__ rec, uint32_t n,
+                                                          uint8_t* __restrict__ verdicts, uint32_t* __restrict__ scr,
+                                                          const uint32_t* __restrict__ comb) {
+  const uint32_t lanes = gridDim.x * blockDim.x;
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  // grid-stride with a wave-uniform trip count (wave_max below needs all lanes)
+  const uint32_t wave0 = lane & ~63u;
+  for (uint32_t base = wave0; base < n; base += lanes) {
+    const uint32_t i = base + (lane & 63);
+    const bool live = i < n;
+    uint32_t aw[8], rw[8], sw[8];
+    uint32_t meta = 0;
+    const uint32_t* myrec = rec + (uint64_t)(live ? i : 0) * 32;
+    if (live) {
+      const uint4* p = reinterpret_cast<const uint4*>(pks + (uint64_t)i * 32);
+      const uint4* g = reinterpret_cast<const uint4*>(sigs + (uint64_t)i * 64);
+      const uint4* r = reinterpret_cast<const uint4*>(rec + (uint64_t)i * 32);
+      uint4 v;
+#define LD8(dst, src, o)                                                   \
+  v = src[o];                                                              \
+  dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;                  \
+  v = src[o + 1];                                                          \
+  dst[4] = v.x; dst[5] = v.y; dst[6] = v.z; dst[7] = v.w;
+      LD8(aw, p, 0);
+      LD8(rw, g, 0);
+      LD8(sw, g, 2);
+#undef LD8
+      meta = r[6].x;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; j++) aw[j] = rw[j] = sw[j] = 0;
+    }
+    // 1. s < l; 2./3. decompress A and R (dalek rules); 4. neither small order
+    bool ok = live && sc_is_canonical(sw);
+    ge_p3 A, R;
+#pragma unroll 1
+    for (int which = 0; which < 2; which++) {
+      uint32_t w[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) w[j] = which ? rw[j] : aw[j];
+      ge_p3 P;
+      const bool dec = ge_decompress(P, w);
+      const bool small = ge_is_small_order(P);
+      ok = ok && dec && !small;
+      if (which == 0) A = P;
+      else R = P;
+    }
+    const int H = wave_max(ok ? (int)(meta & 0xffu) : 0);
+    const bool dneg = (meta >> 31) != 0;
+    uint8_t verdict = 1;
+    if (ok) {
+      // Q = [c](-A) + [|d|](-sign(d) R) + [e]B
+      ge_p3 PA = A, PR = R;
+      fe_neg(PA.X, A.X);
+      fe_neg(PA.T, A.T);
+      if (!dneg) {
+        fe_neg(PR.X, R.X);
+        fe_neg(PR.T, R.T);
+      }
+      tab2_build(scr, lane, 0, PA);
+      tab2_build(scr, lane, 1, PR);
+      ge_p3 acc3;
+      ge_p2 acc2;
+      ge_p1p1 t;
+      ge_p3_identity(acc3);
+#pragma unroll 1
+      for (int pos = H - 1; pos >= 0; pos--) {
+        const int sh = 4 * (pos & 7);
+        const int dc = (int)((myrec[pos >> 3] >> sh) & 15u) - 8;
+        const int dd = (int)((myrec[8 + (pos >> 3)] >> sh) & 15u) - 8;
+        if (pos != H - 1) {
+#pragma unroll 1
+          for (int k = 0; k < 3; k++) {
+            ge_p2_dbl(t, acc2);
+            ge_p1p1_to_p2(acc2, t);
+          }
+          ge_p2_dbl(t, acc2);
+          ge_p1p1_to_p3(acc3, t);
+        }
+        ge_cached q;
+        tab2_select(q, scr, lane, 0, dc);
+        ge_add(t, acc3, q);
+        ge_p1p1_to_p3(acc3, t);
+        tab2_select(q, scr, lane, 1, dd);
+        ge_add(t, acc3, q);
+        if (pos != 0) ge_p1p1_to_p2(acc2, t);
+      }
+      ge_p1p1_to_p3(acc3, t);
+      // [e]B by the doubling-free comb
+      uint32_t e[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) e[j] = myrec[16 + j];
+      add_const_word(e, 0x80808080u);
+#pragma unroll 1
+      for (int j = 0; j < 32; j++) {
+        const int ej = (int)take_low_byte(e) - 128;
+        ge_niels qb;
+        comb_select(qb, comb, j, ej);
+        ge_madd(t, acc3, qb);
+        ge_p1p1_to_p3(acc3, t);
+      }
+      ge_p2 q2;
+      ge_p3_to_p2(q2, acc3);
+      verdict = ge_p2_is_identity(q2) ? 0 : 1;
+    }
+    if (live) verdicts[i] = verdict;
+  }
+}
+
+// ---------------------------------------------------------------------------
+hipError_t coa_launch_build_comb(uint32_t* comb, const uint32_t* btab, hipStream_t s) {
+  hipLaunchKernelGGL(k_build_comb, dim3(COA_COMB_ENTRIES / 256), dim3(256), 0, s, comb, btab);
+  return hipGetLastError();
+}
+
+hipError_t coa_launch_halve(const uint32_t* kbuf, const uint8_t* sigs, uint32_t n, uint32_t* rec, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_halve, dim3((uint32_t)blocks), dim3(256), 0, s, kbuf, sigs, n, rec);
+  return hipGetLastError();
+}
+
+hipError_t coa_launch_verify_halved(const uint8_t* pks, const uint8_t* sigs, const uint32_t* rec, uint32_t n,
+                                    uint8_t* verdicts, uint32_t* scratch, uint32_t scratch_lanes,
+                                    const uint32_t* comb, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = ((uint64_t)n + COA_VERIFY_BLOCK - 1) / COA_VERIFY_BLOCK;
+  const uint64_t maxb = scratch_lanes / COA_VERIFY_BLOCK;
+  if (blocks > maxb) blocks = maxb;
+  hipLaunchKernelGGL(k_verify_halved, dim3((uint32_t)blocks), dim3(COA_VERIFY_BLOCK), 0, s, pks, sigs, rec, n,
+                     verdicts, scratch, comb);
+  return hipGetLastError();
+}

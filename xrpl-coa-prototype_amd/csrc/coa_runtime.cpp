@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -23,6 +24,7 @@
 #include <vector>
 
 #include "coa_batch.h"
+#include "coa_halved.h"
 #include "coa_kernels.h"
 
 namespace {
@@ -67,14 +69,22 @@ struct DevBuf {
 struct Dev {
   int id = 0;
   hipStream_t stream = nullptr;
-  uint32_t* btab = nullptr;
-  DevBuf msgs, pks, sigs, kbuf, verdicts, scratch, aux, rbuf, seeds, offs, data, out, idx, zs, terms, flags;
+  uint32_t* btab = nullptr;  // 128 x (j+1)B, radix-256 fixed-base table (12 KiB)
+  uint32_t* comb = nullptr;  // 32 x 128 x (v+1)256^j B comb for k_verify_halved (384 KiB)
+  DevBuf msgs, pks, sigs, kbuf, rec, verdicts, scratch, aux, rbuf, seeds, offs, data, out, idx, zs, terms, flags;
   std::mutex mu;
   std::vector<DevBuf*> all() {
-    return {&msgs, &pks,  &sigs, &kbuf, &verdicts, &scratch, &aux,   &rbuf,
-            &seeds, &offs, &data, &out,  &idx,      &zs,      &terms, &flags};
+    return {&msgs, &pks,  &sigs, &kbuf, &rec, &verdicts, &scratch, &aux,  &rbuf,
+            &seeds, &offs, &data, &out,  &idx, &zs,       &terms,   &flags};
   }
 };
+
+// COA_VERIFY_IMPL=full selects the full-length k_verify_strict kernel (A/B
+// and parity runs; read per call); the default is the halved-scalar path.
+bool full_impl() {
+  const char* impl = getenv("COA_VERIFY_IMPL");
+  return impl && std::string(impl) == "full";
+}
 
 std::mutex g_init_mu;
 std::vector<std::unique_ptr<Dev>> g_devs;
@@ -94,6 +104,8 @@ int init_locked(int n_gpus) {
     HIP_TRY(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
     HIP_TRY(hipMalloc(&dev->btab, COA_BTAB_DWORDS * sizeof(uint32_t)));
     HIP_TRY(coa_launch_build_btable(dev->btab, dev->stream));
+    HIP_TRY(hipMalloc(&dev->comb, COA_COMB_DWORDS * sizeof(uint32_t)));
+    HIP_TRY(coa_launch_build_comb(dev->comb, dev->btab, dev->stream));
     HIP_TRY(hipStreamSynchronize(dev->stream));
     g_devs.push_back(std::move(dev));
   }
@@ -135,13 +147,48 @@ std::vector<Range> shard(size_t n) {
   return r;
 }
 
-// Enqueue k = H(R||A||M) then verify_strict for device-resident inputs.
-int enqueue_verify(Dev& d, const uint8_t* d_msgs, size_t msg_len, const uint8_t* d_pks, const uint8_t* d_sigs,
-                   size_t n, uint8_t* d_verdicts, uint32_t* d_k, uint32_t* d_scratch, uint32_t lanes,
-                   hipStream_t s) {
-  HIP_TRY(coa_launch_hram(d_msgs, (uint32_t)msg_len, msg_len, nullptr, d_pks, d_sigs, (uint32_t)n, d_k, s));
-  HIP_TRY(coa_launch_verify_strict(d_pks, d_sigs, d_k, (uint32_t)n, d_verdicts, d_scratch, lanes, d.btab, s));
+// Workspace layout for n items: k [n][32] | rec [n][128] | scratch [lanes][2 KiB]
+struct Workspace {
+  uint32_t* k;
+  uint32_t* rec;
+  uint32_t* scratch;
+};
+size_t ws_bytes(size_t n) {
+  n = std::max<size_t>(n, 1);
+  return align_up(n * 32, 256) + align_up(n * COA_HALVE_REC_BYTES, 256) +
+         (size_t)verify_lanes(n) * COA_HALVED_SCRATCH_PER_LANE;
+}
+Workspace ws_carve(void* base, size_t n) {
+  n = std::max<size_t>(n, 1);
+  uint8_t* p = static_cast<uint8_t*>(base);
+  Workspace w;
+  w.k = reinterpret_cast<uint32_t*>(p);
+  p += align_up(n * 32, 256);
+  w.rec = reinterpret_cast<uint32_t*>(p);
+  p += align_up(n * COA_HALVE_REC_BYTES, 256);
+  w.scratch = reinterpret_cast<uint32_t*>(p);
+  return w;
+}
+
+// Verify with k already in w.k: halved path (k_halve + k_verify_halved) or
+// the full-length k_verify_strict.
+int enqueue_verify_prehashed(Dev& d, const uint8_t* d_pks, const uint8_t* d_sigs, size_t n, uint8_t* d_verdicts,
+                             const uint32_t* d_k, const Workspace& w, hipStream_t s) {
+  const uint32_t lanes = verify_lanes(n);
+  if (full_impl()) {
+    HIP_TRY(coa_launch_verify_strict(d_pks, d_sigs, d_k, (uint32_t)n, d_verdicts, w.scratch, lanes, d.btab, s));
+    return COA_OK;
+  }
+  HIP_TRY(coa_launch_halve(d_k, d_sigs, (uint32_t)n, w.rec, s));
+  HIP_TRY(coa_launch_verify_halved(d_pks, d_sigs, w.rec, (uint32_t)n, d_verdicts, w.scratch, lanes, d.comb, s));
   return COA_OK;
+}
+
+// Enqueue k = H(R||A||M) then the verification for device-resident inputs.
+int enqueue_verify(Dev& d, const uint8_t* d_msgs, size_t msg_len, const uint8_t* d_pks, const uint8_t* d_sigs,
+                   size_t n, uint8_t* d_verdicts, const Workspace& w, hipStream_t s) {
+  HIP_TRY(coa_launch_hram(d_msgs, (uint32_t)msg_len, msg_len, nullptr, d_pks, d_sigs, (uint32_t)n, w.k, s));
+  return enqueue_verify_prehashed(d, d_pks, d_sigs, n, d_verdicts, w.k, w, s);
 }
 
 int check_n(size_t n) {
@@ -281,6 +328,7 @@ int coa_shutdown(void) {
     (void)hipStreamSynchronize(d->stream);
     for (DevBuf* b : d->all()) b->release();
     if (d->btab) (void)hipFree(d->btab);
+    if (d->comb) (void)hipFree(d->comb);
     (void)hipStreamDestroy(d->stream);
   }
   g_devs.clear();
@@ -294,9 +342,7 @@ int coa_device_count(void) {
   return (int)g_devs.size();
 }
 
-size_t coa_verify_workspace_bytes(size_t n) {
-  return align_up(std::max<size_t>(n, 1) * 32, 256) + (size_t)verify_lanes(n) * 1024;
-}
+size_t coa_verify_workspace_bytes(size_t n) { return ws_bytes(n); }
 
 int coa_ed25519_verify_strict_many(const uint8_t* msgs, size_t msg_len, const uint8_t* pks, const uint8_t* sigs,
                                    size_t n, uint8_t* verdicts_out) {
@@ -307,19 +353,17 @@ int coa_ed25519_verify_strict_many(const uint8_t* msgs, size_t msg_len, const ui
   if (check_n(n) != COA_OK) return COA_EINVAL;
   return for_shards(n, [&](Dev& d, size_t lo, size_t hi) -> int {
     const size_t cnt = hi - lo;
-    const uint32_t lanes = verify_lanes(cnt);
     hipStream_t s = d.stream;
     HIP_TRY(d.msgs.ensure(cnt * msg_len + 4));
     HIP_TRY(d.pks.ensure(cnt * 32));
     HIP_TRY(d.sigs.ensure(cnt * 64));
-    HIP_TRY(d.kbuf.ensure(cnt * 32));
+    HIP_TRY(d.scratch.ensure(ws_bytes(cnt)));
     HIP_TRY(d.verdicts.ensure(cnt));
-    HIP_TRY(d.scratch.ensure((size_t)lanes * 1024));
     if (msg_len) HIP_TRY(hipMemcpyAsync(d.msgs.p, msgs + lo * msg_len, cnt * msg_len, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d.pks.p, pks + lo * 32, cnt * 32, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d.sigs.p, sigs + lo * 64, cnt * 64, hipMemcpyHostToDevice, s));
     int r = enqueue_verify(d, d.msgs.as<uint8_t>(), msg_len, d.pks.as<uint8_t>(), d.sigs.as<uint8_t>(), cnt,
-                           d.verdicts.as<uint8_t>(), d.kbuf.as<uint32_t>(), d.scratch.as<uint32_t>(), lanes, s);
+                           d.verdicts.as<uint8_t>(), ws_carve(d.scratch.p, cnt), s);
     if (r != COA_OK) return r;
     HIP_TRY(hipMemcpyAsync(verdicts_out + lo, d.verdicts.p, cnt, hipMemcpyDeviceToHost, s));
     return COA_OK;
@@ -344,19 +388,11 @@ int coa_ed25519_verify_strict_many_device(int device, const uint8_t* d_msgs, siz
   Dev* d = dev_by_id(device);
   if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
   HIP_TRY(hipSetDevice(device));
-  const uint32_t lanes = verify_lanes(n);
   hipStream_t s = stream ? (hipStream_t)stream : d->stream;
-  if (workspace) {
-    uint8_t* ws = static_cast<uint8_t*>(workspace);
-    uint32_t* k = reinterpret_cast<uint32_t*>(ws);
-    uint32_t* scr = reinterpret_cast<uint32_t*>(ws + align_up(n * 32, 256));
-    return enqueue_verify(*d, d_msgs, msg_len, d_pks, d_sigs, n, d_verdicts, k, scr, lanes, s);
-  }
+  if (workspace) return enqueue_verify(*d, d_msgs, msg_len, d_pks, d_sigs, n, d_verdicts, ws_carve(workspace, n), s);
   std::lock_guard<std::mutex> l(d->mu);
-  HIP_TRY(d->kbuf.ensure(n * 32));
-  HIP_TRY(d->scratch.ensure((size_t)lanes * 1024));
-  rc = enqueue_verify(*d, d_msgs, msg_len, d_pks, d_sigs, n, d_verdicts, d->kbuf.as<uint32_t>(),
-                      d->scratch.as<uint32_t>(), lanes, s);
+  HIP_TRY(d->scratch.ensure(ws_bytes(n)));
+  rc = enqueue_verify(*d, d_msgs, msg_len, d_pks, d_sigs, n, d_verdicts, ws_carve(d->scratch.p, n), s);
   if (rc != COA_OK) return rc;
   HIP_TRY(hipStreamSynchronize(s));  // engine-owned workspace: drain before release
   return COA_OK;
@@ -389,18 +425,13 @@ int coa_ed25519_verify_prehashed_many_device(int device, const uint8_t* d_k, con
   Dev* d = dev_by_id(device);
   if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
   HIP_TRY(hipSetDevice(device));
-  const uint32_t lanes = verify_lanes(n);
   hipStream_t s = stream ? (hipStream_t)stream : d->stream;
   const uint32_t* k = reinterpret_cast<const uint32_t*>(d_k);
-  if (workspace) {
-    uint32_t* scr = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(workspace) + align_up(n * 32, 256));
-    HIP_TRY(coa_launch_verify_strict(d_pks, d_sigs, k, (uint32_t)n, d_verdicts, scr, lanes, d->btab, s));
-    return COA_OK;
-  }
+  if (workspace) return enqueue_verify_prehashed(*d, d_pks, d_sigs, n, d_verdicts, k, ws_carve(workspace, n), s);
   std::lock_guard<std::mutex> l(d->mu);
-  HIP_TRY(d->scratch.ensure((size_t)lanes * 1024));
-  HIP_TRY(coa_launch_verify_strict(d_pks, d_sigs, k, (uint32_t)n, d_verdicts, d->scratch.as<uint32_t>(), lanes,
-                                   d->btab, s));
+  HIP_TRY(d->scratch.ensure(ws_bytes(n)));
+  rc = enqueue_verify_prehashed(*d, d_pks, d_sigs, n, d_verdicts, k, ws_carve(d->scratch.p, n), s);
+  if (rc != COA_OK) return rc;
   HIP_TRY(hipStreamSynchronize(s));
   return COA_OK;
 }

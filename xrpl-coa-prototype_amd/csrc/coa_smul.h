@@ -1,0 +1,93 @@
+// Shared scalar-multiplication helpers: the radix-256 fixed-base B table
+// (LDS), signed-digit recoding read MSB-first from registers, and the
+// fixed-base multiplication used for signing and table building.
+#pragma once
+#include "coa_fe.h"
+#include "coa_ge.h"
+
+// ---------------------------------------------------------------------------
+// Fixed-base table: entry j (0..127) = (j+1)·B as affine Niels
+// (y+x, y-x, 2d·x·y), 24 dwords each, 12 KiB total.  Verification kernels
+// copy it into LDS once per workgroup.
+// ---------------------------------------------------------------------------
+#define BTAB_ENTRIES 128
+#define BTAB_DWORDS (BTAB_ENTRIES * 24)
+
+COA_DEV void lds_load_btable(uint32_t* lds, const uint32_t* __restrict__ tab) {
+  for (int i = threadIdx.x; i < BTAB_DWORDS / 4; i += blockDim.x)
+    reinterpret_cast<uint4*>(lds)[i] = reinterpret_cast<const uint4*>(tab)[i];
+  __syncthreads();
+}
+
+// Signed radix-256 digit e in [-128, 127] -> ±|e|·B (identity for 0).
+COA_DEV void btab_select(ge_niels& q, const uint32_t* lds, int e) {
+  const int m = e < 0 ? -e : e;
+  const int idx = m == 0 ? 0 : m - 1;
+  const uint4* src = reinterpret_cast<const uint4*>(lds + idx * 24);
+  uint32_t w[24];
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    const uint4 v = src[i];
+    w[4 * i] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    q.yplusx.v[i] = w[i];
+    q.yminusx.v[i] = w[8 + i];
+    q.xy2d.v[i] = w[16 + i];
+  }
+  if (m == 0) ge_niels_identity(q);
+  ge_niels_cneg(q, e < 0);
+}
+
+// ----------------------------------------------------------- scalar digits
+// Signed radix-16 digits of k (< 2^253) are the nibbles of k + 0x88..8 minus 8;
+// signed radix-256 digits of s (< 2^253) are the bytes of s + 0x8080..80
+// minus 128.  Both sums stay < 2^256, so the recoding is exact and can be read
+// most-significant digit first straight from registers.
+COA_DEV void add_const_word(uint32_t* x, uint32_t c) {
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[i] = addc32(x[i], c, cy, cy);
+}
+COA_DEV uint32_t take_top_bits(uint32_t* x, int nb) {
+  const uint32_t top = x[7] >> (32 - nb);
+#pragma unroll
+  for (int i = 7; i > 0; i--) x[i] = (x[i] << nb) | (x[i - 1] >> (32 - nb));
+  x[0] <<= nb;
+  return top;
+}
+
+// [x]B for x < l with the radix-256 B table.
+COA_DEV void fixed_base_mul(ge_p2& out, const uint32_t* x, const uint32_t* btab) {
+  uint32_t sp[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) sp[i] = x[i];
+  add_const_word(sp, 0x80808080u);
+  ge_p3 acc3;
+  ge_p2 acc2;
+  ge_p1p1 t;
+  ge_p3_identity(acc3);
+#pragma unroll 1
+  for (int j = 31; j >= 0; j--) {
+    if (j != 31) {
+#pragma unroll 1
+      for (int dd = 0; dd < 7; dd++) {
+        ge_p2_dbl(t, acc2);
+        ge_p1p1_to_p2(acc2, t);
+      }
+      ge_p2_dbl(t, acc2);
+      ge_p1p1_to_p3(acc3, t);
+    }
+    const int e = (int)take_top_bits(sp, 8) - 128;
+    ge_niels qb;
+    btab_select(qb, btab, e);
+    ge_madd(t, acc3, qb);
+    ge_p1p1_to_p2(acc2, t);
+  }
+  out = acc2;
+}
+
