@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--n", type=int, default=C2_N, help="triples per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU sample")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C3/C4 secondary measurements")
+    ap.add_argument("--c3-certs", type=int, default=2000)
+    ap.add_argument("--c4-batches", type=str, default="1024,16384")
     return ap.parse_args()
 
 
@@ -87,6 +90,123 @@ def cpu_baseline(msgs, pks, sigs, seconds):
                   f"{threads} threads, {el:.1f} s wall ({el * threads:.1f} thread-s)",
         "single_thread_value": 2048 / st,
     }
+
+
+def worker_batches_on_device(nb, dev):
+    """nb bincode WorkerMessage::Batch buffers (977 x 512 B txs, 508,052 B,
+    workloads.worker_batch format) built directly in HBM."""
+    import torch
+
+    from workloads import TX_SIZE, TXS_PER_BATCH
+
+    rec = 8 + TX_SIZE
+    blen = 12 + TXS_PER_BATCH * rec
+    data = torch.zeros((nb, blen), dtype=torch.uint8, device=dev)
+    data[:, 4] = TXS_PER_BATCH & 0xFF
+    data[:, 5] = TXS_PER_BATCH >> 8
+    t = torch.arange(TXS_PER_BATCH, device=dev)
+    pos = 12 + t * rec
+    data[:, pos + 1] = TX_SIZE >> 8  # u64 LE length 512
+    data[:, pos + 8] = (t != 0).to(torch.uint8)  # tag: sample tx 0, standard 1
+    ctr = torch.arange(nb, device=dev)[:, None] * TXS_PER_BATCH + t[None, :]
+    for k in range(8):  # u64 big-endian counter
+        data[:, pos + 9 + k] = ((ctr >> (8 * (7 - k))) & 0xFF).to(torch.uint8)
+    offs = torch.arange(nb + 1, device=dev, dtype=torch.int64) * blen
+    return data.reshape(-1), offs, blen
+
+
+def c4_sha512(local, dev, stream, counts, steps, cpu_threads):
+    """C4: SHA-512 Digest over 500 KB worker batches (worker/src/processor.rs:38)."""
+    import hashlib
+
+    import numpy as np
+    import torch
+
+    import coa_crypto
+    import workloads
+
+    out = {"workload": "C4: Sha512 digest of bincode WorkerMessage::Batch (977 x 512 B txs = 508,052 B)"}
+    for nb in counts:
+        data, offs, blen = worker_batches_on_device(nb, dev)
+        dig = torch.empty((nb, 64), dtype=torch.uint8, device=dev)
+        coa_crypto.sha512_many_device(local, data, offs, dig, stream)
+        torch.cuda.synchronize()
+        d = dig.cpu().numpy()
+        for b in (0, nb - 1):
+            assert bytes(d[b]) == hashlib.sha512(workloads.worker_batch(b)).digest(), "C4 digest mismatch"
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            coa_crypto.sha512_many_device(local, data, offs, dig, stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / steps
+        out[f"batches_{nb}"] = {"ms_per_launch": round(ms, 3), "GBps": round(nb * blen / (ms * 1e-3) / 1e9, 2),
+                                "batches_per_s": round(nb / (ms * 1e-3), 1)}
+        del data, dig
+        torch.cuda.empty_cache()
+    # CPU: the C SHA-512 over host copies, all threads
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coa_oracle
+
+    nbc = 8 * cpu_threads
+    host = np.frombuffer(b"".join(workloads.worker_batch(b) for b in range(nbc)), np.uint8)
+    hoffs = np.arange(nbc + 1, dtype=np.uint64) * 508052
+    t0 = time.perf_counter()
+    coa_oracle.sha512_many(host, hoffs, cpu_threads)
+    el = time.perf_counter() - t0
+    out["cpu_baseline"] = {"GBps": round(host.size / el / 1e9, 3), "cores": cpu_threads, "kind": "port",
+                           "sample": f"{nbc} batches, {cpu_threads} threads"}
+    return out
+
+
+def c3_certificates(n_certs, latency_samples, cpu_threads):
+    """C3: committee of 100, 67 votes per certificate: Certificate::verify
+    throughput (batched over a round) and single-certificate p50/p99 latency,
+    both end to end through the host-pointer C ABI (PCIe included)."""
+    import numpy as np
+
+    import certificates as C
+
+    committee, batch = C.synth_certificates(n_certs, committee_size=100, n_payload=32, seed=3)
+    v = C.verify_certificate_batch(batch, committee)  # warm-up + correctness
+    assert int(v.sum()) == 0, "C3 certificates rejected"
+    t0 = time.perf_counter()
+    v = C.verify_certificate_batch(batch, committee)
+    el = time.perf_counter() - t0
+    lat = []
+    for i in range(latency_samples):
+        cert = batch.certificate(i % n_certs)
+        t1 = time.perf_counter()
+        cert.verify(committee)
+        lat.append(time.perf_counter() - t1)
+    lat = np.array(lat) * 1e3
+    res = {"workload": "C3: committee 100, 67 votes/certificate, header 32 payload + 67 parents",
+           "certificates": n_certs, "votes": int(batch.offsets[-1]),
+           "certs_per_s": round(n_certs / el, 1), "round_ms": round(el * 1e3, 2),
+           "p50_ms": round(float(np.percentile(lat, 50)), 3), "p99_ms": round(float(np.percentile(lat, 99)), 3)}
+    # CPU: Certificate::verify crypto (dalek algorithms) on one core
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import random
+
+    import coa_oracle
+
+    rnd = random.Random(1)
+    cl = []
+    for i in range(min(30, n_certs)):
+        lo, hi = int(batch.offsets[i]), int(batch.offsets[i + 1])
+        zs = [rnd.getrandbits(128) for _ in range(hi - lo)]
+        t1 = time.perf_counter()
+        ok = coa_oracle.certificate_verify(batch.header_inputs[i], batch.ids[i], batch.authors[i],
+                                           batch.header_sigs[i], batch.round, batch.vote_pks[lo:hi],
+                                           batch.vote_sigs[lo:hi], zs)
+        cl.append(time.perf_counter() - t1)
+        assert ok
+    cl = np.array(cl) * 1e3
+    res["cpu_baseline"] = {"p50_ms": round(float(np.percentile(cl, 50)), 3), "cores": 1, "kind": "port",
+                           "certs_per_s_all_cores_est": round(cpu_threads / (float(np.mean(cl)) * 1e-3), 1),
+                           "sample": f"{len(cl)} certificates, single thread"}
+    return res
 
 
 def main():
@@ -180,6 +300,16 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(msgs_h, pks.cpu().numpy(), sigs.cpu().numpy(), args.cpu_seconds)
+    secondary = None
+    if rank == 0 and world == 1 and not args.no_secondary:
+        threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1, 64))
+        del kbuf, ws
+        torch.cuda.empty_cache()
+        secondary = {
+            "c4_sha512": c4_sha512(local, dev, stream, [int(x) for x in args.c4_batches.split(",") if x], 2,
+                                   threads),
+            "c3_certificate_verify": c3_certificates(args.c3_certs, 100, threads),
+        }
 
     if rank == 0:
         line = {
@@ -205,6 +335,7 @@ def main():
                          "kernel": "k_halve+k_verify_halved (prehashed verify stage)",
                          "alg_int32_ops_per_verify": ALG_INT32_OPS_PER_VERIFY},
             "cpu_baseline": cpu,
+            "secondary": secondary,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -135,6 +135,28 @@ int coa_ed25519_sign_many(const uint8_t* seeds, const uint8_t* msgs, size_t msg_
 int coa_ed25519_sign_many_device(int device, const uint8_t* d_seeds, const uint8_t* d_msgs, size_t msg_len, size_t n,
                                  uint8_t* d_pks_out, uint8_t* d_sigs_out, void* stream);
 
+/* ------------------------------------------------ aggregation queue (f1)
+ * Pre-verification stage for Core::run (primary/src/core.rs:349-389), which
+ * verifies one message at a time: producers submit header/vote signatures
+ * and certificate vote batches; the queue's worker thread coalesces them into
+ * coa_ed25519_verify_strict_many / coa_ed25519_verify_batch_groups launches
+ * (when max_batch signatures are pending, when the oldest request is
+ * max_delay_us old, or on flush) and replies per request through the
+ * callback -- the SignatureService request/oneshot idiom of
+ * crypto/src/lib.rs:222-250.  Inputs are copied at submission.  The callback
+ * runs on the worker thread with status (COA_OK or a negative engine error)
+ * and the request's verdict byte(s). */
+typedef struct coa_queue coa_queue;
+typedef void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n);
+coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us);
+int coa_queue_submit_verify(coa_queue* q, const uint8_t msg[32], const uint8_t pk[32], const uint8_t sig[64],
+                            coa_verdict_cb cb, void* user);
+int coa_queue_submit_batch(coa_queue* q, const uint8_t msg[32], const uint8_t* pks, const uint8_t* sigs, size_t n,
+                           coa_verdict_cb cb, void* user);
+int coa_queue_flush(coa_queue* q);
+int coa_queue_stats(coa_queue* q, uint64_t* launches, uint64_t* items, uint64_t* groups);
+int coa_queue_destroy(coa_queue* q);
+
 #ifdef __cplusplus
 }
 #endif

@@ -776,3 +776,29 @@ void coa_oracle_counts(uint64_t* nmul, uint64_t* nsq) {
 }
 void coa_oracle_reset_counts(void) { g_nmul = g_nsq = 0; }
 #endif
+
+/* ------------------------------------------- SHA-512 multithreaded driver */
+typedef struct {
+  const uint8_t* data;
+  const uint64_t* off;
+  size_t lo, hi;
+  uint8_t* out;
+} shajob_t;
+
+static void* sha_worker(void* p) {
+  shajob_t* j = (shajob_t*)p;
+  for (size_t i = j->lo; i < j->hi; i++) coa_oracle_sha512(j->data + j->off[i], j->off[i + 1] - j->off[i], j->out + 64 * i);
+  return NULL;
+}
+
+void coa_oracle_sha512_many_mt(const uint8_t* data, const uint64_t* off, size_t n, uint8_t* out64, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  shajob_t jobs[256];
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = (shajob_t){data, off, n * t / nthreads, n * (t + 1) / nthreads, out64};
+    pthread_create(&th[t], NULL, sha_worker, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}

@@ -34,6 +34,8 @@ def lib(count=False):
         L.coa_oracle_verify_strict_many.restype = None
         L.coa_oracle_sha512.argtypes = [P8, sz, P8]
         L.coa_oracle_sha512.restype = None
+        L.coa_oracle_sha512_many_mt.argtypes = [P8, ctypes.POINTER(ctypes.c_uint64), sz, P8, ctypes.c_int]
+        L.coa_oracle_sha512_many_mt.restype = None
         if count:
             L.coa_oracle_counts.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 2
             L.coa_oracle_reset_counts.argtypes = []
@@ -90,3 +92,28 @@ def field_op_counts(msg, pk, sig):
     a, b = ctypes.c_uint64(), ctypes.c_uint64()
     L.coa_oracle_counts(ctypes.byref(a), ctypes.byref(b))
     return a.value, b.value
+
+
+def sha512_many(data, offsets, nthreads=1):
+    """data: uint8 array, offsets: uint64 [n+1] -> uint8 [n, 64]."""
+    data = np.ascontiguousarray(data, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = offsets.shape[0] - 1
+    out = np.zeros((n, 64), np.uint8)
+    lib().coa_oracle_sha512_many_mt(_p(data), offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n, _p(out),
+                                    nthreads)
+    return out
+
+
+def certificate_verify(header_input, header_id, author, header_sig, round_, vote_pks, vote_sigs, zs):
+    """Certificate::verify crypto as the reference runs it on one core:
+    Header::digest == id, Signature::verify(id, author), Certificate::digest,
+    verify_batch(digest, votes) (primary/src/messages.rs:48-84,189-234)."""
+    import struct as _st
+
+    if sha512(header_input)[:32] != bytes(header_id):
+        return False
+    if not verify_strict(bytes(header_id), bytes(author), bytes(header_sig)):
+        return False
+    d = sha512(bytes(header_id) + _st.pack("<Q", round_) + bytes(author))[:32]
+    return verify_batch(d, [bytes(p) for p in vote_pks], [bytes(s) for s in vote_sigs], zs)

@@ -23,26 +23,26 @@ if [[ $STEPS == *bench* ]]; then
   cat gpurun_out/bench.json
 fi
 if [[ $STEPS == *big* ]]; then
-  run bench_big && timeout -k 10 300 python bench.py --n 524288 --steps 10 --no-cpu-baseline > gpurun_out/bench_big.json 2> gpurun_out/bench_big.err \
+  run bench_big && timeout -k 10 300 python bench.py --n 524288 --steps 10 --no-cpu-baseline --no-secondary > gpurun_out/bench_big.json 2> gpurun_out/bench_big.err \
     || { tail -30 gpurun_out/bench_big.err; exit 1; }
   cat gpurun_out/bench_big.json
 fi
 if [[ $STEPS == *prof* ]]; then
   run prof && timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof -o run --output-format csv \
-      -- python3 bench.py --no-cpu-baseline --steps 10 > gpurun_out/bench_prof.json 2> gpurun_out/prof.err \
+      -- python3 bench.py --no-cpu-baseline --no-secondary --steps 10 > gpurun_out/bench_prof.json 2> gpurun_out/prof.err \
     || { tail -30 gpurun_out/prof.err; exit 1; }
   find gpurun_out/prof -name "*stats*" | head
   for f in $(find gpurun_out/prof -name "*kernel_stats.csv"); do cat "$f"; done
 fi
 if [[ $STEPS == *sq* ]]; then
   run "pmc SQ" && timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -T -d gpurun_out/pmc_SQ -o run --output-format csv \
-      -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/pmc_SQ.json 2> gpurun_out/pmc_SQ.err \
+      -- python3 bench.py --no-cpu-baseline --no-secondary --steps 3 --warmup 1 > gpurun_out/pmc_SQ.json 2> gpurun_out/pmc_SQ.err \
     || { tail -30 gpurun_out/pmc_SQ.err; exit 1; }
 fi
 if [[ $STEPS == *pmc* ]]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     run "pmc $c" && timeout -k 10 300 rocprofv3 --pmc $c -T -d gpurun_out/pmc_$c -o run --output-format csv \
-        -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err \
+        -- python3 bench.py --no-cpu-baseline --no-secondary --steps 3 --warmup 1 > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err \
       || { tail -30 gpurun_out/pmc_$c.err; exit 1; }
   done
   find gpurun_out -path "*pmc_*" -name "*.csv" | head

@@ -3,7 +3,7 @@ bytes for one kernel (MI355X_MICROARCH.md HBM section: FETCH_SIZE and
 WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide
 coalesced reads, so the read side is doubled).
 
-usage: python tools/pmc_traffic.py <gpurun_out dir> <kernel> <n> <out.json>
+usage: python tools/pmc_traffic.py <gpurun_out dir> <kernel[,kernel...]> <n> <out.json>
 """
 import csv
 import glob
@@ -26,16 +26,22 @@ def per_dispatch(root, counter, kernel):
 
 
 def main():
-    root, kernel, n, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    fetch = per_dispatch(root, "FETCH_SIZE", kernel)
-    write = per_dispatch(root, "WRITE_SIZE", kernel)
-    if not fetch or not write:
-        raise SystemExit(f"no {kernel} rows found under {root}")
-    f_kib, w_kib = statistics.median(fetch), statistics.median(write)
+    root, kernels, n, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    f_kib = w_kib = 0.0
+    nd = []
+    for kernel in kernels.split(","):  # a stage of several kernels: sum of per-kernel medians
+        fetch = per_dispatch(root, "FETCH_SIZE", kernel)
+        write = per_dispatch(root, "WRITE_SIZE", kernel)
+        if not fetch or not write:
+            raise SystemExit(f"no {kernel} rows found under {root}")
+        f_kib += statistics.median(fetch)
+        w_kib += statistics.median(write)
+        nd.append([len(fetch), len(write)])
+    kernel = kernels
     res = {
         "kernel": kernel,
         "n": n,
-        "dispatches": [len(fetch), len(write)],
+        "dispatches": nd,
         "fetch_size_kib_raw": f_kib,
         "write_size_kib": w_kib,
         "hbm_read_bytes_corrected": 2 * f_kib * 1024,

@@ -42,6 +42,8 @@ class EngineError(RuntimeError):
 
 
 _lib = None
+# void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n)
+VERDICT_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t)
 
 
 def _u8p(a):
@@ -80,6 +82,12 @@ def lib():
         "coa_ed25519_public_keys": ([P8, sz, P8], ctypes.c_int),
         "coa_ed25519_sign_many": ([P8, P8, sz, sz, P8, P8], ctypes.c_int),
         "coa_ed25519_sign_many_device": ([ctypes.c_int, vp, vp, sz, sz, vp, vp, vp], ctypes.c_int),
+        "coa_queue_create": ([sz, ctypes.c_uint32], vp),
+        "coa_queue_submit_verify": ([vp, P8, P8, P8, VERDICT_CB, vp], ctypes.c_int),
+        "coa_queue_submit_batch": ([vp, P8, P8, P8, sz, VERDICT_CB, vp], ctypes.c_int),
+        "coa_queue_flush": ([vp], ctypes.c_int),
+        "coa_queue_stats": ([vp, P64, P64, P64], ctypes.c_int),
+        "coa_queue_destroy": ([vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -369,3 +377,83 @@ def sha512_many_device(device, data, offsets, out64, stream=None):
     handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
     n = offsets.shape[0] - 1
     _check(lib().coa_sha512_many_device(device, data.data_ptr(), offsets.data_ptr(), n, out64.data_ptr(), handle))
+
+
+# --------------------------------------------------------- aggregation queue
+class AggregationQueue:
+    """Python face of the native coalescing stage (coa_queue_*): submit
+    header/vote signatures and certificate vote batches from any thread, get
+    a concurrent.futures.Future per request resolving to True (Ok) / False
+    (Err); the engine error status raises EngineError in the future."""
+
+    def __init__(self, max_batch=65536, max_delay_us=500):
+        import concurrent.futures as cf
+        import threading
+
+        self._cf = cf
+        self._lock = threading.Lock()
+        self._pending = {}
+        self._next = 1
+        self._cb = VERDICT_CB(self._on_verdict)  # keep alive for the queue's lifetime
+        self._q = lib().coa_queue_create(max_batch, max_delay_us)
+
+    def _on_verdict(self, user, status, verdicts, n):
+        with self._lock:
+            fut = self._pending.pop(user)
+        if status < 0:
+            fut.set_exception(EngineError(f"{_ERRORS.get(status, status)}"))
+        else:
+            fut.set_result(verdicts[0] == 0)
+
+    def _register(self):
+        fut = self._cf.Future()
+        with self._lock:
+            key = self._next
+            self._next += 1
+            self._pending[key] = fut
+        return key, fut
+
+    def submit_verify(self, digest, public_key, signature):
+        key, fut = self._register()
+        d = np.frombuffer(bytes(digest), np.uint8).copy()
+        pk = np.frombuffer(bytes(public_key), np.uint8).copy()
+        sg = np.frombuffer(signature.flatten() if isinstance(signature, Signature) else bytes(signature),
+                           np.uint8).copy()
+        rc = lib().coa_queue_submit_verify(self._q, _u8p(d), _u8p(pk), _u8p(sg), self._cb, key)
+        if rc < 0:
+            with self._lock:
+                self._pending.pop(key, None)
+            _check(rc)
+        return fut
+
+    def submit_batch(self, digest, votes):
+        key, fut = self._register()
+        votes = list(votes)
+        d = np.frombuffer(bytes(digest), np.uint8).copy()
+        pks = _bytes_array([bytes(pk) for pk, _ in votes], 32) if votes else np.zeros(32, np.uint8)
+        sgs = _bytes_array([s.flatten() for _, s in votes], 64) if votes else np.zeros(64, np.uint8)
+        rc = lib().coa_queue_submit_batch(self._q, _u8p(d), _u8p(pks), _u8p(sgs), len(votes), self._cb, key)
+        if rc < 0:
+            with self._lock:
+                self._pending.pop(key, None)
+            _check(rc)
+        return fut
+
+    def flush(self):
+        _check(lib().coa_queue_flush(self._q))
+
+    def stats(self):
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().coa_queue_stats(self._q, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return {"launches": a.value, "signatures": b.value, "batches": c.value}
+
+    def close(self):
+        if self._q:
+            lib().coa_queue_destroy(self._q)
+            self._q = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
