@@ -15,4 +15,4 @@ hipError_t coa_launch_build_comb(uint32_t* comb, const uint32_t* btab, hipStream
 hipError_t coa_launch_halve(const uint32_t* kbuf, const uint8_t* sigs, uint32_t n, uint32_t* rec, hipStream_t s);
 hipError_t coa_launch_verify_halved(const uint8_t* pks, const uint8_t* sigs, const uint32_t* rec, uint32_t n,
                                     uint8_t* verdicts, uint32_t* scratch, uint32_t scratch_lanes,
-                                    const uint32_t* comb, hipStream_t s);
+                                    const uint32_t* comb, int waves, hipStream_t s);

@@ -385,7 +385,8 @@ __global__ void __launch_bounds__(256) k_halve(const uint32_t* __restrict__ kbuf
   }
 }
 
-__global__ void __launch_bounds__(256, 2) k_verify_halved(const uint8_t* __restrict__ pks,
+template <int WAVES>
+__global__ void __launch_bounds__(256, WAVES) k_verify_halved(const uint8_t* __restrict__ pks,
                                                           const uint8_t* __restrict__ sigs,
                                                           const uint32_t* __restrict__ rec, uint32_t n,
                                                           uint8_t* __restrict__ verdicts, uint32_t* __restrict__ scr,
@@ -510,14 +511,19 @@ hipError_t coa_launch_halve(const uint32_t* kbuf, const uint8_t* sigs, uint32_t 
   return hipGetLastError();
 }
 
+// waves: register bound of the instance (2 = 256 VGPRs, 3 = 168 with spills)
 hipError_t coa_launch_verify_halved(const uint8_t* pks, const uint8_t* sigs, const uint32_t* rec, uint32_t n,
                                     uint8_t* verdicts, uint32_t* scratch, uint32_t scratch_lanes,
-                                    const uint32_t* comb, hipStream_t s) {
+                                    const uint32_t* comb, int waves, hipStream_t s) {
   if (n == 0) return hipSuccess;
   uint64_t blocks = ((uint64_t)n + COA_VERIFY_BLOCK - 1) / COA_VERIFY_BLOCK;
   const uint64_t maxb = scratch_lanes / COA_VERIFY_BLOCK;
   if (blocks > maxb) blocks = maxb;
-  hipLaunchKernelGGL(k_verify_halved, dim3((uint32_t)blocks), dim3(COA_VERIFY_BLOCK), 0, s, pks, sigs, rec, n,
-                     verdicts, scratch, comb);
+  if (waves == 3)
+    hipLaunchKernelGGL(k_verify_halved<3>, dim3((uint32_t)blocks), dim3(COA_VERIFY_BLOCK), 0, s, pks, sigs, rec, n,
+                       verdicts, scratch, comb);
+  else
+    hipLaunchKernelGGL(k_verify_halved<2>, dim3((uint32_t)blocks), dim3(COA_VERIFY_BLOCK), 0, s, pks, sigs, rec, n,
+                       verdicts, scratch, comb);
   return hipGetLastError();
 }

@@ -85,6 +85,11 @@ bool full_impl() {
   const char* impl = getenv("COA_VERIFY_IMPL");
   return impl && std::string(impl) == "full";
 }
+// COA_VERIFY_WAVES=3 selects the 168-VGPR instance of k_verify_halved.
+int verify_waves() {
+  const char* w = getenv("COA_VERIFY_WAVES");
+  return (w && std::string(w) == "3") ? 3 : 2;
+}
 
 std::mutex g_init_mu;
 std::vector<std::unique_ptr<Dev>> g_devs;
@@ -180,7 +185,8 @@ int enqueue_verify_prehashed(Dev& d, const uint8_t* d_pks, const uint8_t* d_sigs
     return COA_OK;
   }
   HIP_TRY(coa_launch_halve(d_k, d_sigs, (uint32_t)n, w.rec, s));
-  HIP_TRY(coa_launch_verify_halved(d_pks, d_sigs, w.rec, (uint32_t)n, d_verdicts, w.scratch, lanes, d.comb, s));
+  HIP_TRY(coa_launch_verify_halved(d_pks, d_sigs, w.rec, (uint32_t)n, d_verdicts, w.scratch, lanes, d.comb,
+                                   verify_waves(), s));
   return COA_OK;
 }
 
