@@ -16,6 +16,19 @@
 // instructions per multiply, 176 per squaring; profiles/r01_ubench_fe*.txt).
 //
 // Reduction uses 2^256 == 38 (mod p).
+//
+// Carry chains are inline-asm strings.  hipcc's gfx950 hazard model pads
+// every VALU write of VCC/an SGPR that a later VALU reads (carry-in
+// included) with two wait states, and every asm statement with one more
+// before the first reader of its outputs; at one wave per SIMD those pads are
+// exposed issue slots.  Here each comba column, each add/sub/fold chain and
+// the squaring's diagonal add is one string whose carries pass through VCC
+// between adjacent instructions (the VOP2 carry-in read), so the static
+// s_nop count of k_verify_halved fell from 8763 to ~680 and its instruction
+// count from 33.8K to 25.3K (tools/isa_stats.py).  The unpadded hand-off is
+// checked bit-exact against host ports at 1, 4 and 8 waves per SIMD
+// (tools/ubench_carry.hip, tools/ubench_fe3.hip; profiles/r01_ubench_*.txt)
+// and by the whole GPU parity suite.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -40,24 +53,100 @@ COA_DEV uint32_t subb32(uint32_t a, uint32_t b, uint32_t bin, uint32_t& bout) {
   return r;
 }
 
-// (acc:64, c2:32) += a * b.  v_mad_u64_u32 writes its carry-out to an SGPR
-// pair (one bit per lane), which v_addc_co_u32 folds into the third word.
+// (acc:64, c2:32) += a * b.  v_mad_u64_u32 writes its carry-out to VCC (one
+// bit per lane), which the 4-byte VOP2 v_addc_co_u32 reads implicitly as its
+// carry-in and folds into the third word.  A VALU VCC write read as carry-in
+// needs no wait states, so nothing is padded inside the string.
 COA_DEV void mac(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
-  uint64_t sc;
-  asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
-      "v_addc_co_u32 %2, %1, %2, 0, %1"
-      : "+v"(acc), "=&s"(sc), "+v"(c2)
-      : "v"(a), "v"(b));
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(c2)
+      : "v"(a), "v"(b)
+      : "vcc");
 }
 
-// First product of a column: the carry word starts from the mad's carry-out
-// instead of a separately zeroed register.
-COA_DEV void mac0(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
-  uint64_t sc;
-  asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
-      "v_addc_co_u32 %2, %1, 0, 0, %1"
-      : "+v"(acc), "=&s"(sc), "=v"(c2)
-      : "v"(a), "v"(b));
+// One whole comba column in a single asm statement: (acc, c2) = acc +
+// sum_p x[p] * y[p], where c2 starts from the first product's carry-out.
+// hipcc pads every inline-asm statement with an `s_nop 0` before the next
+// VALU that reads its outputs; one statement per column instead of one per
+// product removes ~50 of those issue slots from every fe_mul
+// (tools/ubench_fe3.hip, profiles/r01_ubench_fe3.txt: 1104 -> 913 cycles per
+// multiply at one wave per SIMD).  Operands: %0 acc, %1 c2, %2 a zero VGPR
+// (the VOP2 addc takes its second source from a VGPR), %3.. the x/y pairs.
+#define COA_MAD0(X, Y)                                   \
+  "v_mad_u64_u32 %0, vcc, %" #X ", %" #Y ", %0\n\t"      \
+  "v_addc_co_u32_e32 %1, vcc, 0, %2, vcc\n\t"
+#define COA_MADC(X, Y)                                   \
+  "v_mad_u64_u32 %0, vcc, %" #X ", %" #Y ", %0\n\t"      \
+  "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+#define COA_COL_OUT "+v"(acc), "=&v"(c2)
+
+template <int P>
+COA_DEV void col(uint64_t& acc, uint32_t& c2, const uint32_t* x, const uint32_t* y) {
+  const uint32_t z = 0;
+  static_assert(P >= 1 && P <= 8, "column width");
+  if constexpr (P == 1) {
+    asm(COA_MAD0(3, 4) : COA_COL_OUT : "v"(z), "v"(x[0]), "v"(y[0]) : "vcc");
+  } else if constexpr (P == 2) {
+    asm(COA_MAD0(3, 4) COA_MADC(5, 6) : COA_COL_OUT : "v"(z), "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]) : "vcc");
+  } else if constexpr (P == 3) {
+    asm(COA_MAD0(3, 4) COA_MADC(5, 6) COA_MADC(7, 8)
+        : COA_COL_OUT
+        : "v"(z), "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]) : "vcc");
+  } else if constexpr (P == 4) {
+    asm(COA_MAD0(3, 4) COA_MADC(5, 6) COA_MADC(7, 8) COA_MADC(9, 10)
+        : COA_COL_OUT
+        : "v"(z), "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]), "v"(x[3]), "v"(y[3]) : "vcc");
+  } else if constexpr (P == 5) {
+    asm(COA_MAD0(3, 4) COA_MADC(5, 6) COA_MADC(7, 8) COA_MADC(9, 10) COA_MADC(11, 12)
+        : COA_COL_OUT
+        : "v"(z), "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]), "v"(x[3]), "v"(y[3]), "v"(x[4]),
+          "v"(y[4]) : "vcc");
+  } else if constexpr (P == 6) {
+    asm(COA_MAD0(3, 4) COA_MADC(5, 6) COA_MADC(7, 8) COA_MADC(9, 10) COA_MADC(11, 12) COA_MADC(13, 14)
+        : COA_COL_OUT
+        : "v"(z), "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]), "v"(x[3]), "v"(y[3]), "v"(x[4]),
+          "v"(y[4]), "v"(x[5]), "v"(y[5]) : "vcc");
+  } else if constexpr (P == 7) {
+    asm(COA_MAD0(3, 4) COA_MADC(5, 6) COA_MADC(7, 8) COA_MADC(9, 10) COA_MADC(11, 12) COA_MADC(13, 14)
+            COA_MADC(15, 16)
+        : COA_COL_OUT
+        : "v"(z), "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]), "v"(x[3]), "v"(y[3]), "v"(x[4]),
+          "v"(y[4]), "v"(x[5]), "v"(y[5]), "v"(x[6]), "v"(y[6]) : "vcc");
+  } else {
+    asm(COA_MAD0(3, 4) COA_MADC(5, 6) COA_MADC(7, 8) COA_MADC(9, 10) COA_MADC(11, 12) COA_MADC(13, 14)
+            COA_MADC(15, 16) COA_MADC(17, 18)
+        : COA_COL_OUT
+        : "v"(z), "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]), "v"(x[3]), "v"(y[3]), "v"(x[4]),
+          "v"(y[4]), "v"(x[5]), "v"(y[5]), "v"(x[6]), "v"(y[6]), "v"(x[7]), "v"(y[7]) : "vcc");
+  }
+}
+
+// Column k of a product: the pairs (i, k - i), 0 <= i, k - i < 8; for a
+// squaring only the cross products i < k - i.
+template <int K, bool SQ>
+COA_DEV void mul_col(uint64_t& acc, uint32_t& c2, const fe& a, const fe& b) {
+  constexpr int lo = K < 8 ? 0 : K - 7;
+  constexpr int hi = SQ ? (K - 1) / 2 : (K < 8 ? K : 7);
+  constexpr int P = hi - lo + 1;
+  uint32_t x[P > 0 ? P : 1], y[P > 0 ? P : 1];
+#pragma unroll
+  for (int p = 0; p < P; p++) {
+    x[p] = a.v[lo + p];
+    y[p] = b.v[K - lo - p];
+  }
+  if constexpr (P > 0) col<P>(acc, c2, x, y);
+}
+
+template <bool SQ, int K = SQ ? 1 : 0>
+COA_DEV void mul_cols(uint32_t* t, uint64_t& acc, const fe& a, const fe& b) {
+  if constexpr (K < (SQ ? 14 : 15)) {
+    uint32_t c2;
+    mul_col<K, SQ>(acc, c2, a, b);
+    t[K] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)c2 << 32);
+    mul_cols<SQ, K + 1>(t, acc, a, b);
+  }
 }
 
 COA_DEV void fe_set(fe& r, uint32_t x) {
@@ -67,31 +156,105 @@ COA_DEV void fe_set(fe& r, uint32_t x) {
 }
 
 // ------------------------------------------------------- add / sub / neg
-// r = a + b (mod p), result < 2^256.
+// Carry chains are written as unpadded VOP2 strings: each v_addc/v_subb
+// takes its carry-in from VCC, written by the instruction before it.  hipcc's
+// own code pads every such hand-off with `s_nop 1` on gfx950; at one wave per
+// SIMD (the C2 occupancy) that costs 1.6x (tools/ubench_carry.hip,
+// profiles/r01_ubench_carry.txt: 241 -> 153 cycles per fe_add, bit-exact on
+// 3.4e7 lanes x 128 chained adds at 1, 4 and 8 waves per SIMD).
+#define COA_FOLD38_TAIL(R0, R1, R2, R3, R4, R5, R6, R7, T, Z)               \
+  "v_addc_co_u32_e32 %" #T ", vcc, 0, %" #Z ", vcc\n\t"                      \
+  "v_mul_u32_u24_e32 %" #T ", 38, %" #T "\n\t"                               \
+  "v_add_co_u32_e32 %" #R0 ", vcc, %" #R0 ", %" #T "\n\t"                    \
+  "v_addc_co_u32_e32 %" #R1 ", vcc, 0, %" #R1 ", vcc\n\t"                    \
+  "v_addc_co_u32_e32 %" #R2 ", vcc, 0, %" #R2 ", vcc\n\t"                    \
+  "v_addc_co_u32_e32 %" #R3 ", vcc, 0, %" #R3 ", vcc\n\t"                    \
+  "v_addc_co_u32_e32 %" #R4 ", vcc, 0, %" #R4 ", vcc\n\t"                    \
+  "v_addc_co_u32_e32 %" #R5 ", vcc, 0, %" #R5 ", vcc\n\t"                    \
+  "v_addc_co_u32_e32 %" #R6 ", vcc, 0, %" #R6 ", vcc\n\t"                    \
+  "v_addc_co_u32_e32 %" #R7 ", vcc, 0, %" #R7 ", vcc\n\t"                    \
+  "v_addc_co_u32_e32 %" #T ", vcc, 0, %" #Z ", vcc\n\t"                      \
+  "v_mul_u32_u24_e32 %" #T ", 38, %" #T "\n\t"                               \
+  "v_add_u32_e32 %" #R0 ", %" #R0 ", %" #T
+#define COA_R8_INOUT(r)                                                                                    \
+  "+&v"(r.v[0]), "+&v"(r.v[1]), "+&v"(r.v[2]), "+&v"(r.v[3]), "+&v"(r.v[4]), "+&v"(r.v[5]), "+&v"(r.v[6]), \
+      "+&v"(r.v[7])
+#define COA_B8_IN(b) \
+  "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]), "v"(b.v[7])
+
+// r = a + b (mod p), result < 2^256.  2^256 == 38: the carry is folded back
+// in; a second carry can only occur when the sum wrapped to a value < 38, so
+// the last fold cannot carry.
 COA_DEV void fe_add(fe& r, const fe& a, const fe& b) {
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = addc32(a.v[i], b.v[i], c, c);
-  // 2^256 == 38: fold the carry; a second carry can only occur when the sum
-  // wrapped to a value < 38, so the last fold cannot carry.
-  uint32_t c2 = 0;
-  r.v[0] = addc32(r.v[0], c * 38u, 0, c2);
-#pragma unroll
-  for (int i = 1; i < 8; i++) r.v[i] = addc32(r.v[i], 0, c2, c2);
-  r.v[0] += c2 * 38u;
+  fe x = a;
+  uint32_t t;
+  const uint32_t z = 0;
+  asm("v_add_co_u32_e32 %0, vcc, %0, %10\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %1, %11, vcc\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %2, %12, vcc\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %3, %13, vcc\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %4, %14, vcc\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %5, %15, vcc\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %6, %16, vcc\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %7, %17, vcc\n\t"
+      COA_FOLD38_TAIL(0, 1, 2, 3, 4, 5, 6, 7, 8, 9)
+      : COA_R8_INOUT(x), "=&v"(t)
+      : "v"(z), COA_B8_IN(b)
+      : "vcc");
+  r = x;
 }
 
-// r = a - b (mod p), result < 2^256.
+// r = a - b (mod p), result < 2^256: a - b + 2^256 is computed, then
+// 2^256 == 38 subtracted once per borrow.
 COA_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
-  uint32_t bw = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = subb32(a.v[i], b.v[i], bw, bw);
-  // a - b + 2^256 was computed: subtract 2^256 == 38.
-  uint32_t b2 = 0;
-  r.v[0] = subb32(r.v[0], bw * 38u, 0, b2);
-#pragma unroll
-  for (int i = 1; i < 8; i++) r.v[i] = subb32(r.v[i], 0, b2, b2);
-  r.v[0] -= b2 * 38u;
+  fe x = a;
+  uint32_t t;
+  const uint32_t z = 0;
+  asm("v_sub_co_u32_e32 %0, vcc, %0, %10\n\t"
+      "v_subb_co_u32_e32 %1, vcc, %1, %11, vcc\n\t"
+      "v_subb_co_u32_e32 %2, vcc, %2, %12, vcc\n\t"
+      "v_subb_co_u32_e32 %3, vcc, %3, %13, vcc\n\t"
+      "v_subb_co_u32_e32 %4, vcc, %4, %14, vcc\n\t"
+      "v_subb_co_u32_e32 %5, vcc, %5, %15, vcc\n\t"
+      "v_subb_co_u32_e32 %6, vcc, %6, %16, vcc\n\t"
+      "v_subb_co_u32_e32 %7, vcc, %7, %17, vcc\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %9, vcc\n\t"
+      "v_mul_u32_u24_e32 %8, 38, %8\n\t"
+      "v_sub_co_u32_e32 %0, vcc, %0, %8\n\t"
+      "v_subb_co_u32_e32 %1, vcc, %1, %9, vcc\n\t"
+      "v_subb_co_u32_e32 %2, vcc, %2, %9, vcc\n\t"
+      "v_subb_co_u32_e32 %3, vcc, %3, %9, vcc\n\t"
+      "v_subb_co_u32_e32 %4, vcc, %4, %9, vcc\n\t"
+      "v_subb_co_u32_e32 %5, vcc, %5, %9, vcc\n\t"
+      "v_subb_co_u32_e32 %6, vcc, %6, %9, vcc\n\t"
+      "v_subb_co_u32_e32 %7, vcc, %7, %9, vcc\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %9, vcc\n\t"
+      "v_mul_u32_u24_e32 %8, 38, %8\n\t"
+      "v_sub_u32_e32 %0, %0, %8"
+      : COA_R8_INOUT(x), "=&v"(t)
+      : "v"(z), COA_B8_IN(b)
+      : "vcc");
+  r = x;
+}
+
+
+// r += w (w < 2^32 - 2^10), then the carry folded as 38; result < 2^256.
+COA_DEV void fe_fold_word(fe& r, uint32_t w) {
+  asm("v_add_co_u32_e32 %0, vcc, %0, %8\n\t"
+      "v_mov_b32_e32 %8, 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
+      "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
+      "v_addc_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
+      "v_addc_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
+      "v_addc_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
+      "v_addc_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %8, vcc\n\t"
+      "v_mul_u32_u24_e32 %8, 38, %8\n\t"
+      "v_add_u32_e32 %0, %0, %8"
+      : COA_R8_INOUT(r), "+&v"(w)
+      :
+      : "vcc");
 }
 
 COA_DEV void fe_neg(fe& r, const fe& a) {
@@ -101,71 +264,71 @@ COA_DEV void fe_neg(fe& r, const fe& a) {
 }
 
 // ------------------------------------------------------------- reduction
-// r = t[0..15] (512-bit) mod p, result < 2^256.
+// r = t[0..15] (512-bit) mod p, result < 2^256.  The eight limb products
+// u_i = 38 t[8+i] + t[i] < 39 * 2^32 are independent mads (no carries, so
+// nothing to pad); one VCC chain then adds the high words one limb up, and a
+// second folds the top word (< 40) as 38 and its carry as 38 again.
 COA_DEV void fe_reduce512(fe& r, const uint32_t* t) {
-  uint64_t c = 0;
+  uint32_t lo[8], hi[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    c = (uint64_t)t[8 + i] * 38u + (c >> 32) + t[i];
-    r.v[i] = (uint32_t)c;
+    const uint64_t u = (uint64_t)t[8 + i] * 38u + t[i];
+    lo[i] = (uint32_t)u;
+    hi[i] = (uint32_t)(u >> 32);
   }
-  uint32_t hi = (uint32_t)(c >> 32) * 38u;  // < 39 * 38
-  uint32_t cc = 0;
-  r.v[0] = addc32(r.v[0], hi, 0, cc);
-#pragma unroll
-  for (int i = 1; i < 8; i++) r.v[i] = addc32(r.v[i], 0, cc, cc);
-  r.v[0] += cc * 38u;
+  uint32_t w;
+  asm("v_add_co_u32_e32 %1, vcc, %10, %17\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %11, %18, vcc\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %12, %19, vcc\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %13, %20, vcc\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %14, %21, vcc\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %15, %22, vcc\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %16, %23, vcc\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %24, vcc\n\t"
+      "v_mul_u32_u24_e32 %8, 38, %8\n\t"
+      "v_add_co_u32_e32 %0, vcc, %9, %8\n\t"
+      "v_mov_b32_e32 %8, 0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
+      "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
+      "v_addc_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
+      "v_addc_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
+      "v_addc_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
+      "v_addc_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %8, vcc\n\t"
+      "v_mul_u32_u24_e32 %8, 38, %8\n\t"
+      "v_add_u32_e32 %0, %0, %8"
+      : "=&v"(r.v[0]), "=&v"(r.v[1]), "=&v"(r.v[2]), "=&v"(r.v[3]), "=&v"(r.v[4]), "=&v"(r.v[5]), "=&v"(r.v[6]),
+        "=&v"(r.v[7]), "=&v"(w)
+      : "v"(lo[0]), "v"(lo[1]), "v"(lo[2]), "v"(lo[3]), "v"(lo[4]), "v"(lo[5]), "v"(lo[6]), "v"(lo[7]), "v"(hi[0]),
+        "v"(hi[1]), "v"(hi[2]), "v"(hi[3]), "v"(hi[4]), "v"(hi[5]), "v"(hi[6]), "v"(hi[7])
+      : "vcc");
 }
 
 // ------------------------------------------------------------ multiply
 COA_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
   uint32_t t[16];
   uint64_t acc = 0;
-  uint32_t c2 = 0;
-#pragma unroll
-  for (int k = 0; k < 15; k++) {
-    bool first = true;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int j = k - i;
-      if (j < 0 || j > 7) continue;
-      if (first) mac0(acc, c2, a.v[i], b.v[j]);
-      else mac(acc, c2, a.v[i], b.v[j]);
-      first = false;
-    }
-    t[k] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)c2 << 32);
-  }
+  mul_cols<false>(t, acc, a, b);
   t[15] = (uint32_t)acc;
   fe_reduce512(r, t);
 }
 
-// Squaring: the 28 cross products by comba, doubled with one carry chain,
-// then the 8 squares added with a second chain (44 mads vs 72 for fe_mul).
+// Squaring: the 28 cross products by comba, doubled by a funnel shift (no
+// carry chain), then the 8 squares added with one unpadded VCC chain (44 mads
+// vs 72 for fe_mul).  The doubled cross sum is < 2^511, so the shift loses
+// nothing and the final chain cannot carry out.
 COA_DEV void fe_sq(fe& r, const fe& a) {
   uint32_t t[16];
   t[0] = 0;
   uint64_t acc = 0;
-  uint32_t c2 = 0;
-#pragma unroll
-  for (int k = 1; k < 14; k++) {
-    bool first = true;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int j = k - i;
-      if (j <= i || j > 7) continue;
-      if (first) mac0(acc, c2, a.v[i], a.v[j]);
-      else mac(acc, c2, a.v[i], a.v[j]);
-      first = false;
-    }
-    t[k] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)c2 << 32);
-  }
+  mul_cols<true>(t, acc, a, a);
   t[14] = (uint32_t)acc;
   t[15] = (uint32_t)(acc >> 32);
-  uint32_t c = 0;
+  uint32_t u[16];
 #pragma unroll
-  for (int i = 0; i < 16; i++) t[i] = addc32(t[i], t[i], c, c);
+  for (int i = 15; i >= 2; i--) u[i] = __builtin_amdgcn_alignbit(t[i], t[i - 1], 31);
+  u[1] = t[1] << 1;
   uint32_t d[16];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -173,11 +336,30 @@ COA_DEV void fe_sq(fe& r, const fe& a) {
     d[2 * i] = (uint32_t)p;
     d[2 * i + 1] = (uint32_t)(p >> 32);
   }
-  c = 0;
-#pragma unroll
-  for (int i = 0; i < 16; i++) t[i] = addc32(t[i], d[i], c, c);
-  fe_reduce512(r, t);
+  u[0] = d[0];
+  asm("v_add_co_u32_e32 %0, vcc, %0, %15\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %1, %16, vcc\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %2, %17, vcc\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %3, %18, vcc\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %4, %19, vcc\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %5, %20, vcc\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %6, %21, vcc\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %7, %22, vcc\n\t"
+      "v_addc_co_u32_e32 %8, vcc, %8, %23, vcc\n\t"
+      "v_addc_co_u32_e32 %9, vcc, %9, %24, vcc\n\t"
+      "v_addc_co_u32_e32 %10, vcc, %10, %25, vcc\n\t"
+      "v_addc_co_u32_e32 %11, vcc, %11, %26, vcc\n\t"
+      "v_addc_co_u32_e32 %12, vcc, %12, %27, vcc\n\t"
+      "v_addc_co_u32_e32 %13, vcc, %13, %28, vcc\n\t"
+      "v_addc_co_u32_e32 %14, vcc, %14, %29, vcc"
+      : "+&v"(u[1]), "+&v"(u[2]), "+&v"(u[3]), "+&v"(u[4]), "+&v"(u[5]), "+&v"(u[6]), "+&v"(u[7]), "+&v"(u[8]),
+        "+&v"(u[9]), "+&v"(u[10]), "+&v"(u[11]), "+&v"(u[12]), "+&v"(u[13]), "+&v"(u[14]), "+&v"(u[15])
+      : "v"(d[1]), "v"(d[2]), "v"(d[3]), "v"(d[4]), "v"(d[5]), "v"(d[6]), "v"(d[7]), "v"(d[8]), "v"(d[9]),
+        "v"(d[10]), "v"(d[11]), "v"(d[12]), "v"(d[13]), "v"(d[14]), "v"(d[15])
+      : "vcc");
+  fe_reduce512(r, u);
 }
+
 
 COA_DEV void fe_sqn(fe& r, const fe& a, int n) {
   fe_sq(r, a);
@@ -192,12 +374,7 @@ COA_DEV void fe_mul_small(fe& r, const fe& a, uint32_t c) {
     acc = (uint64_t)a.v[i] * c + (acc >> 32);
     r.v[i] = (uint32_t)acc;
   }
-  uint32_t hi = (uint32_t)(acc >> 32) * 38u;
-  uint32_t cc = 0;
-  r.v[0] = addc32(r.v[0], hi, 0, cc);
-#pragma unroll
-  for (int i = 1; i < 8; i++) r.v[i] = addc32(r.v[i], 0, cc, cc);
-  r.v[0] += cc * 38u;
+  fe_fold_word(r, (uint32_t)(acc >> 32) * 38u);  // c < 2^26: < 2^32 - 2^10
 }
 
 // ------------------------------------------------------------ canonical
