@@ -125,6 +125,73 @@ int coa_sha512_trunc32_many(const uint8_t* data, const uint64_t* offsets, size_t
 int coa_sha512_many_device(int device, const uint8_t* d_data, const uint64_t* d_offsets, size_t n, uint8_t* d_out64,
                            void* stream);
 
+/* ------------------------------------------------ committee key cache (f2)
+ * No reference counterpart: the reference decompresses every voter key on
+ * every call (crypto/src/lib.rs:202,216) although the keys are fixed per
+ * config::Committee (config/src/lib.rs:140-143, loaded once in
+ * node/src/main.rs).  Registers the committee's n public keys (32 B each;
+ * duplicates collapse) on every device: decompression verdict, small-order
+ * and torsion flags and a 384 KiB comb of -A per key, so certificate checks
+ * need no doubling.  Replaces any previous committee; n = 0 clears it.
+ * Verdict-neutral: keys outside the committee still verify, through the
+ * uncached kernels.  Returns the number of distinct keys registered or a
+ * negative error. */
+int coa_committee_register(const uint8_t* pks, size_t n);
+/* Key flags of the registered committee in its internal (sorted) order:
+ * bit0 decompresses, bit1 small order, bit2 torsion free.  Returns the
+ * committee size; copies min(size, cap) words.  Diagnostics / tests. */
+int coa_committee_key_flags(uint32_t* flags_out, size_t cap);
+
+/* --------------------------------------- Certificate::verify crypto (f3)
+ * The crypto of Certificate::verify (primary/src/messages.rs:189-215) in one
+ * fused launch for registered committees:
+ *   COA_CERT_BAD_HEADER_ID   SHA-512(header digest bytes)[..32] != header.id
+ *                            (Header::verify, messages.rs:49-51; the bytes are
+ *                            Header::digest's input, messages.rs:70-84)
+ *   COA_CERT_BAD_HEADER_SIG  Signature::verify(header.id, author) fails
+ *                            (messages.rs:64-66, dalek verify_strict)
+ *   COA_CERT_BAD_VOTES       Signature::verify_batch(Certificate::digest,
+ *                            votes) fails (messages.rs:214; the digest is
+ *                            SHA-512(id || round u64 LE || origin)[..32],
+ *                            messages.rs:226-234, computed on the device)
+ * The non-crypto checks (genesis, stake, worker ids, quorum) stay with the
+ * caller, which applies them in the reference's order with these bits
+ * (INTEGRATION.md).  Votes are checked per signature with the committee
+ * combs; when every vote holds its own cofactorless equation and every key is
+ * torsion free, dalek's batch verdict is Ok for any weights.  Any other
+ * well-formed outcome is re-decided by the exact random-linear-combination
+ * kernels (weights from rng_seed, 0 = OS entropy, as verify_batch), and
+ * certificates with keys outside the committee take the uncached kernels:
+ * the verdict is always dalek's.
+ *   header_data/header_offsets  n + 1 offsets into the concatenated headers
+ *   ids, origins                n * 32 (header.id, header.author)
+ *   header_sigs                 n * 64;  rounds: n
+ *   vote_pks, vote_sigs         concatenated votes; certificate c owns
+ *                               [vote_offsets[c], vote_offsets[c+1])
+ *   status_out[c]               0 = all crypto Ok, else COA_CERT_* bits */
+#define COA_CERT_BAD_HEADER_ID 1
+#define COA_CERT_BAD_HEADER_SIG 2
+#define COA_CERT_BAD_VOTES 4
+int coa_certificate_verify_many(const uint8_t* header_data, const uint64_t* header_offsets, const uint8_t* ids,
+                                const uint8_t* origins, const uint8_t* header_sigs, const uint64_t* rounds,
+                                const uint8_t* vote_pks, const uint8_t* vote_sigs, const uint64_t* vote_offsets,
+                                size_t n, uint64_t rng_seed, uint8_t* status_out);
+/* One certificate (the latency path: one H2D, one launch with one wavefront
+ * per signature, one D2H).  Returns the COA_CERT_* bits (>= 0) or a negative
+ * error. */
+int coa_certificate_verify(const uint8_t* header_data, size_t header_len, const uint8_t id[32],
+                           const uint8_t origin[32], const uint8_t header_sig[64], uint64_t round,
+                           const uint8_t* vote_pks, const uint8_t* vote_sigs, size_t n_votes, uint64_t rng_seed);
+/* Device-resident form (asynchronous on `stream`): d_status[c] receives the
+ * raw status word -- COA_CERT_* bits plus 8 = votes need the exact RLC check
+ * (coa_ed25519_verify_batch_groups) and 16 = a key is not registered (use the
+ * uncached entry points).  The host-pointer calls above resolve both. */
+int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data, const uint64_t* d_header_offsets,
+                                       const uint8_t* d_ids, const uint8_t* d_origins, const uint8_t* d_header_sigs,
+                                       const uint64_t* d_rounds, const uint8_t* d_vote_pks,
+                                       const uint8_t* d_vote_sigs, const uint64_t* d_vote_offsets, size_t n,
+                                       size_t n_votes, uint32_t* d_status, void* stream);
+
 /* --------------------------------------------------------------- signing
  * RFC 8032 signing == crypto::Signature::new (crypto/src/lib.rs:185-191) /
  * generate_keypair (:167-175) from 32-byte seeds.  Not on the verification

@@ -7,12 +7,16 @@ top of the engine's batched C ABI -- SURVEY.md 8(a) rows a7-a9.
     Committee::quorum_threshold    config/src/lib.rs:168-173 (2N/3 + 1 of stake)
 
 `Certificate.verify` follows the reference's check order exactly and raises
-the same error kinds (DagError variants, primary/src/error.rs).  The batched
-`verify_certificates` runs the crypto of many certificates in three GPU
-launches -- header digests (SHA-512), header signatures (verify_strict) and
-vote batches (verify_batch, one group per certificate) -- and applies the
-per-certificate protocol checks on the host, returning one result per
-certificate in input order.
+the same error kinds (DagError variants, primary/src/error.rs).  Its crypto
+(header digest, header signature, vote batch) is ONE engine call,
+coa_certificate_verify (fused kernel over the registered committee's key
+combs -- `Committee.register()`); the status bits it
+returns are then consumed in the reference's order, interleaved with the
+host-side protocol checks, so the error raised is the reference's.
+`verify_stepwise` is the same method over the per-primitive entry points
+(verify_strict / verify_batch / Digest), kept for cross-checks.
+`verify_certificates` / `verify_certificate_batch` do the same for many
+certificates with one coa_certificate_verify_many call.
 """
 import struct
 
@@ -70,6 +74,11 @@ class Committee:
 
     def authorities(self):
         return sorted(self.stakes)
+
+    def register(self):
+        """Hand the committee's keys to the engine's key cache (f2).  Needed
+        for speed only: verdicts do not depend on it."""
+        return coa_crypto.committee_register(np.array([list(bytes(k)) for k in self.authorities()], np.uint8))
 
 
 class Header:
@@ -165,6 +174,19 @@ class Certificate:
             raise CertificateRequiresQuorum()
 
     def verify(self, committee, rng_seed=0):
+        """Certificate::verify (primary/src/messages.rs:189-215): one fused
+        engine call for the crypto, checks raised in the reference's order."""
+        if self.is_genesis(committee):
+            return
+        h = self.header
+        vp = np.array([list(bytes(pk)) for pk, _ in self.votes], np.uint8).reshape(-1, 32)
+        vs = np.array([list(sg.flatten()) for _, sg in self.votes], np.uint8).reshape(-1, 64)
+        st = coa_crypto.certificate_verify(h.digest_input(), h.id, h.author, h.signature.flatten(), h.round, vp, vs,
+                                           rng_seed=rng_seed)
+        _raise_in_order(self, committee, st)
+
+    def verify_stepwise(self, committee, rng_seed=0):
+        """The same checks through the per-primitive entry points."""
         if self.is_genesis(committee):
             return
         self.header.verify(committee)
@@ -175,62 +197,49 @@ class Certificate:
             raise InvalidSignature() from e
 
 
+def _raise_in_order(cert, committee, st):
+    """Apply Certificate::verify's checks in the reference's order, the crypto
+    ones read from the engine's status bits (include/coa_verify.h)."""
+    h = cert.header
+    if st & coa_crypto.CERT_BAD_HEADER_ID:                      # messages.rs:49-51
+        raise InvalidHeaderId(h.id)
+    if committee.stake(h.author) <= 0:                          # :53-56
+        raise UnknownAuthority(h.author)
+    for wid in h.payload.values():                              # :58-62
+        if not committee.has_worker(h.author, wid):
+            raise MalformedHeader(h.id)
+    if st & coa_crypto.CERT_BAD_HEADER_SIG:                     # :64-66
+        raise InvalidSignature()
+    cert.quorum_check(committee)                                # :196-211
+    if st & coa_crypto.CERT_BAD_VOTES:                          # :214
+        raise InvalidSignature()
+
+
 def verify_certificates(certs, committee, rng_seed=0):
-    """Certificate::verify for many certificates; crypto batched on the GPU.
-    Returns a list with None (Ok) or the DagError instance per certificate."""
+    """Certificate::verify for many certificates: the crypto of all of them in
+    one coa_certificate_verify_many call, then the checks in the reference's
+    order.  Returns a list with None (Ok) or the DagError instance."""
     n = len(certs)
     res = [None] * n
     todo = [i for i, c in enumerate(certs) if not c.is_genesis(committee)]
     if not todo:
         return res
-    # GPU: header digests and certificate digests (SHA-512)
-    hdr = coa_crypto.sha512_many([certs[i].header.digest_input() for i in todo])
-    cdg = coa_crypto.sha512_many([certs[i].digest_input() for i in todo])
-    live = []
+    hs = [certs[i].header for i in todo]
+    ids = np.array([list(bytes(h.id)) for h in hs], np.uint8)
+    origins = np.array([list(bytes(h.author)) for h in hs], np.uint8)
+    hsigs = np.array([list(h.signature.flatten()) for h in hs], np.uint8)
+    rounds = np.array([h.round for h in hs], np.uint64)
+    vp = np.array([list(bytes(pk)) for i in todo for pk, _ in certs[i].votes], np.uint8).reshape(-1, 32)
+    vs = np.array([list(sg.flatten()) for i in todo for _, sg in certs[i].votes], np.uint8).reshape(-1, 64)
+    offs = np.zeros(len(todo) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(certs[i].votes) for i in todo])
+    st = coa_crypto.certificate_verify_many([h.digest_input() for h in hs], ids, origins, hsigs, rounds, vp, vs, offs,
+                                            rng_seed=rng_seed)
     for j, i in enumerate(todo):
-        c = certs[i]
         try:
-            if bytes(hdr[j][:32]) != bytes(c.header.id):
-                raise InvalidHeaderId(c.header.id)
-            if committee.stake(c.header.author) <= 0:
-                raise UnknownAuthority(c.header.author)
-            for wid in c.header.payload.values():
-                if not committee.has_worker(c.header.author, wid):
-                    raise MalformedHeader(c.header.id)
-            live.append((i, j))
+            _raise_in_order(certs[i], committee, int(st[j]))
         except DagError as e:
             res[i] = e
-    if not live:
-        return res
-    # GPU: header signatures
-    msgs = np.array([list(bytes(certs[i].header.id)) for i, _ in live], np.uint8)
-    pks = np.array([list(bytes(certs[i].header.author)) for i, _ in live], np.uint8)
-    sgs = np.array([list(certs[i].header.signature.flatten()) for i, _ in live], np.uint8)
-    hv = coa_crypto.verify_strict_many(msgs, pks, sgs)
-    groups = []
-    for (i, j), v in zip(live, hv):
-        if v:
-            res[i] = InvalidSignature()
-            continue
-        try:
-            certs[i].quorum_check(committee)
-            groups.append((i, j))
-        except DagError as e:
-            res[i] = e
-    if not groups:
-        return res
-    # GPU: vote batches, one group per certificate
-    gm = np.array([list(cdg[j][:32]) for _, j in groups], np.uint8)
-    vp = b"".join(bytes(pk) for i, _ in groups for pk, _ in certs[i].votes)
-    vs = b"".join(sg.flatten() for i, _ in groups for _, sg in certs[i].votes)
-    offs = np.zeros(len(groups) + 1, np.uint64)
-    offs[1:] = np.cumsum([len(certs[i].votes) for i, _ in groups])
-    nv = int(offs[-1])
-    gv = coa_crypto.verify_batch_groups(gm, np.frombuffer(vp, np.uint8).reshape(nv, 32),
-                                        np.frombuffer(vs, np.uint8).reshape(nv, 64), offs, rng_seed=rng_seed)
-    for (i, _), v in zip(groups, gv):
-        if v:
-            res[i] = InvalidSignature()
     return res
 
 
@@ -310,16 +319,16 @@ def synth_certificates(n_certs, committee_size=100, n_votes=None, n_payload=32, 
 
 
 def verify_certificate_batch(batch, committee, rng_seed=0):
-    """Certificate::verify over a CertificateBatch: three GPU calls (header
-    digests, header signatures, vote batches) + vectorised protocol checks.
+    """Certificate::verify over a CertificateBatch: one fused engine call
+    (coa_certificate_verify_many) + vectorised protocol checks.
     Returns uint8 [n]: 0 Ok, 1 Err."""
     n = len(batch)
-    err = np.zeros(n, np.uint8)
-    hd = coa_crypto.sha512_many(batch.header_inputs)[:, :32]
-    err |= (hd != batch.ids).any(axis=1).astype(np.uint8)                      # InvalidHeaderId
+    rounds = np.full(n, batch.round, np.uint64)
+    st = coa_crypto.certificate_verify_many(batch.header_inputs, batch.ids, batch.authors, batch.header_sigs, rounds,
+                                            batch.vote_pks, batch.vote_sigs, batch.offsets, rng_seed=rng_seed)
+    err = (st != 0).astype(np.uint8)
     stake = np.array([committee.stake(PublicKey(bytes(p))) for p in batch.authors])
     err |= (stake <= 0).astype(np.uint8)                                        # UnknownAuthority
-    err |= coa_crypto.verify_strict_many(batch.ids, batch.authors, batch.header_sigs)  # header signature
     # quorum: distinct voters with stake, total >= 2N/3 + 1
     keys = committee.authorities()
     kstake = np.array([committee.stake(k) for k in keys])
@@ -328,7 +337,25 @@ def verify_certificate_batch(batch, committee, rng_seed=0):
         v = batch.voter_idx[lo:hi]
         if len(np.unique(v)) != len(v) or kstake[v].sum() < committee.quorum_threshold():
             err[i] = 1
-    # certificate digest, then the vote batches
+    return err
+
+
+def verify_certificate_batch_stepwise(batch, committee, rng_seed=0):
+    """The same over the per-primitive entry points (four engine calls)."""
+    n = len(batch)
+    err = np.zeros(n, np.uint8)
+    hd = coa_crypto.sha512_many(batch.header_inputs)[:, :32]
+    err |= (hd != batch.ids).any(axis=1).astype(np.uint8)
+    stake = np.array([committee.stake(PublicKey(bytes(p))) for p in batch.authors])
+    err |= (stake <= 0).astype(np.uint8)
+    err |= coa_crypto.verify_strict_many(batch.ids, batch.authors, batch.header_sigs)
+    keys = committee.authorities()
+    kstake = np.array([committee.stake(k) for k in keys])
+    for i in range(n):
+        lo, hi = int(batch.offsets[i]), int(batch.offsets[i + 1])
+        v = batch.voter_idx[lo:hi]
+        if len(np.unique(v)) != len(v) or kstake[v].sum() < committee.quorum_threshold():
+            err[i] = 1
     cin = [bytes(batch.ids[c]) + struct.pack("<Q", batch.round) + bytes(batch.authors[c]) for c in range(n)]
     cd = coa_crypto.sha512_many(cin)[:, :32]
     gv = coa_crypto.verify_batch_groups(cd, batch.vote_pks, batch.vote_sigs, batch.offsets, rng_seed=rng_seed)

@@ -82,6 +82,13 @@ def lib():
         "coa_ed25519_public_keys": ([P8, sz, P8], ctypes.c_int),
         "coa_ed25519_sign_many": ([P8, P8, sz, sz, P8, P8], ctypes.c_int),
         "coa_ed25519_sign_many_device": ([ctypes.c_int, vp, vp, sz, sz, vp, vp, vp], ctypes.c_int),
+        "coa_committee_register": ([P8, sz], ctypes.c_int),
+        "coa_committee_key_flags": ([ctypes.POINTER(ctypes.c_uint32), sz], ctypes.c_int),
+        "coa_certificate_verify_many": ([P8, P64, P8, P8, P8, P64, P8, P8, P64, sz, ctypes.c_uint64, P8],
+                                        ctypes.c_int),
+        "coa_certificate_verify": ([P8, sz, P8, P8, P8, ctypes.c_uint64, P8, P8, sz, ctypes.c_uint64], ctypes.c_int),
+        "coa_certificate_verify_many_device": ([ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, sz, vp, vp],
+                                               ctypes.c_int),
         "coa_queue_create": ([sz, ctypes.c_uint32], vp),
         "coa_queue_submit_verify": ([vp, P8, P8, P8, VERDICT_CB, vp], ctypes.c_int),
         "coa_queue_submit_batch": ([vp, P8, P8, P8, sz, VERDICT_CB, vp], ctypes.c_int),
@@ -377,6 +384,79 @@ def sha512_many_device(device, data, offsets, out64, stream=None):
     handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
     n = offsets.shape[0] - 1
     _check(lib().coa_sha512_many_device(device, data.data_ptr(), offsets.data_ptr(), n, out64.data_ptr(), handle))
+
+
+# ------------------------------------------- committee cache / certificates
+CERT_BAD_HEADER_ID, CERT_BAD_HEADER_SIG, CERT_BAD_VOTES = 1, 2, 4
+CERT_NEEDS_EXACT, CERT_UNCACHED = 8, 16  # raw device status bits only
+KEY_DECOMPRESSES, KEY_SMALL_ORDER, KEY_TORSION_FREE = 1, 2, 4
+
+
+def committee_register(pks):
+    """Register the committee's public keys (f2 key cache); returns the number
+    of distinct keys.  Verdict-neutral."""
+    pks = np.ascontiguousarray(np.asarray(pks, dtype=np.uint8).reshape(-1, 32))
+    return _check(lib().coa_committee_register(_u8p(pks), pks.shape[0]))
+
+
+def committee_key_flags():
+    """Flags of the registered keys, in the engine's sorted key order."""
+    n = _check(lib().coa_committee_key_flags(None, 0))
+    out = np.zeros(max(n, 1), np.uint32)
+    _check(lib().coa_committee_key_flags(out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n))
+    return out[:n]
+
+
+def _u64p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+
+def certificate_verify_many(header_inputs, ids, origins, header_sigs, rounds, vote_pks, vote_sigs, vote_offsets,
+                            rng_seed=0):
+    """Crypto of Certificate::verify for n certificates (fused kernel for the
+    registered committee, exact fallbacks otherwise).  Returns uint8 [n] of
+    CERT_BAD_* bits (0 = every crypto check Ok)."""
+    n = len(header_inputs)
+    hdata = np.frombuffer(b"".join(header_inputs), np.uint8) if n else np.zeros(0, np.uint8)
+    hoff = np.zeros(n + 1, np.uint64)
+    hoff[1:] = np.cumsum([len(h) for h in header_inputs])
+    ids = np.ascontiguousarray(ids, dtype=np.uint8)
+    origins = np.ascontiguousarray(origins, dtype=np.uint8)
+    hsigs = np.ascontiguousarray(header_sigs, dtype=np.uint8)
+    rounds = np.ascontiguousarray(np.broadcast_to(np.asarray(rounds, np.uint64), (n,)))
+    vpks = np.ascontiguousarray(vote_pks, dtype=np.uint8)
+    vsigs = np.ascontiguousarray(vote_sigs, dtype=np.uint8)
+    voff = np.ascontiguousarray(vote_offsets, dtype=np.uint64)
+    out = np.zeros(max(n, 1), np.uint8)
+    _check(lib().coa_certificate_verify_many(_u8p(hdata), _u64p(hoff), _u8p(ids), _u8p(origins), _u8p(hsigs),
+                                             _u64p(rounds), _u8p(vpks), _u8p(vsigs), _u64p(voff), n, rng_seed,
+                                             _u8p(out)))
+    return out[:n]
+
+
+def certificate_verify(header_input, id_, origin, header_sig, round_, vote_pks, vote_sigs, rng_seed=0):
+    """One certificate through the latency path; returns the CERT_BAD_* bits."""
+    h = np.frombuffer(bytes(header_input), np.uint8)
+    i = np.frombuffer(bytes(id_), np.uint8)
+    o = np.frombuffer(bytes(origin), np.uint8)
+    s = np.frombuffer(bytes(header_sig), np.uint8)
+    vp = np.ascontiguousarray(vote_pks, dtype=np.uint8)
+    vs = np.ascontiguousarray(vote_sigs, dtype=np.uint8)
+    nv = vp.size // 32
+    return _check(lib().coa_certificate_verify(_u8p(h), h.size, _u8p(i), _u8p(o), _u8p(s), round_, _u8p(vp),
+                                               _u8p(vs), nv, rng_seed))
+
+
+def certificate_verify_many_device(device, hdata, hoff, ids, origins, hsigs, rounds, vpks, vsigs, voff, status,
+                                   stream=None):
+    """Device-resident certificates (torch tensors); raw status words (uint32
+    tensor [n]) enqueued on `stream`."""
+    n = ids.shape[0]
+    nv = vpks.shape[0]
+    _check(lib().coa_certificate_verify_many_device(device, hdata.data_ptr(), hoff.data_ptr(), ids.data_ptr(),
+                                                    origins.data_ptr(), hsigs.data_ptr(), rounds.data_ptr(),
+                                                    vpks.data_ptr(), vsigs.data_ptr(), voff.data_ptr(), n, nv,
+                                                    status.data_ptr(), _handle(device, stream)))
 
 
 # --------------------------------------------------------- aggregation queue

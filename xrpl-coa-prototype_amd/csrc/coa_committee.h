@@ -1,0 +1,49 @@
+// Internal launch wrappers for the committee key cache (f2) and the fused
+// Certificate::verify kernel (f3) -- coa_committee.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// per-key comb of -A: 32 byte positions x 128 multiples x 24 dwords (384 KiB)
+#define COA_KEY_TAB_ENTRIES (32 * 128)
+#define COA_KEY_TAB_DWORDS (COA_KEY_TAB_ENTRIES * 24)
+
+// key flag bits (k_key_flags)
+#define COA_KEY_DECOMPRESSES 1u   // CompressedEdwardsY::decompress succeeds
+#define COA_KEY_SMALL_ORDER 2u    // [8]A == O  (verify_strict rejects)
+#define COA_KEY_TORSION_FREE 4u   // [l]A == O  (batch fast path is exact)
+
+// Internal status bits of k_cert_verify (low three are the public
+// COA_CERT_BAD_* bits of include/coa_verify.h).
+#define COA_CST_BAD_HEADER_ID 1u
+#define COA_CST_BAD_HEADER_SIG 2u
+#define COA_CST_BAD_VOTES 4u
+#define COA_CST_VOTES_INCONCLUSIVE 8u  // some vote failed its own equation, or a key has torsion
+#define COA_CST_UNCACHED 16u           // author or a voter is not in the registered committee
+
+struct CertArgs {
+  const uint8_t* hdr_data;      // Header::digest inputs, concatenated
+  const uint64_t* hdr_off;      // [nc + 1]
+  const uint32_t* ids;          // [nc][8]   header.id
+  const uint32_t* origins;      // [nc][8]   header.author (Certificate::origin)
+  const uint32_t* hsigs;        // [nc][16]  header.signature R || s
+  const uint64_t* rounds;       // [nc]
+  const uint32_t* vpks;         // [nv][8]   voter public keys
+  const uint32_t* vsigs;        // [nv][16]  vote signatures
+  const uint64_t* voff;         // [nc + 1]  certificate c owns votes [voff[c], voff[c+1])
+  uint32_t nc, nv;
+  uint32_t hdr_blocks;          // set by the launcher
+  const uint32_t* keys;         // [nk][8] registered keys, sorted as dword tuples
+  const uint32_t* kflags;       // [nk]
+  const uint32_t* ktabs;        // [nk][COA_KEY_TAB_DWORDS] comb of -A per key
+  uint32_t nk;
+  const uint32_t* comb;         // B comb (coa_halved.h)
+  uint32_t* status;             // [nc], zeroed by the caller
+};
+
+hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s);
+hipError_t coa_launch_key_tables(const uint32_t* keys, uint32_t nk, uint32_t* tabs, hipStream_t s);
+// lanes_per_sig: 64 (latency: one wave per signature, comb terms split over
+// the lanes and summed by a butterfly) or 1 (throughput: one lane per
+// signature).
+hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, hipStream_t s);

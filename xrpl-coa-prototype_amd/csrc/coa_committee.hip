@@ -1,0 +1,360 @@
+// Committee key cache and the fused Certificate::verify
+// kernel (f3) for gfx950.
+//
+// The reference re-decompresses every voter key on every call
+// (crypto/src/lib.rs:202,216) although keys are fixed per Committee
+// (config/src/lib.rs:140-143).  coa_committee_register() precomputes, once
+// per committee and per device:
+//   k_key_flags    decompression verdict, small order ([8]A == O) and
+//                  torsion freedom ([l]A == O) of every key
+//   k_key_tables   a comb of -A per key: entry (j, v) = (v+1)*256^j*(-A) as
+//                  affine Niels, built by exact double-and-add, so torsion
+//                  components are kept (the comb is an integer multiple, never
+//                  reduced mod l)
+// With those, a signature's equation P = [s]B + [k](-A) needs no doubling:
+// 32 comb additions for each scalar (signed radix-256 digits).
+//
+// k_cert_verify runs the whole crypto of Certificate::verify
+// (primary/src/messages.rs:189-215) in one launch, every check independent:
+//   * header digest role (leading blocks, one lane per certificate):
+//     SHA-512(Header::digest bytes)[..32] == header.id   (messages.rs:49-51)
+//   * signature role, one job per header signature and per vote:
+//     header: verify_strict(header.id, author)            (messages.rs:64-66)
+//             -- s < l, A and R decompress, neither small order, P == R
+//     vote:   the message is Certificate::digest =
+//             SHA-512(id || round || origin)[..32]         (messages.rs:226-234)
+//             computed in-kernel; per vote s < l, A and R decompress and
+//             P == R (cofactorless, projective).
+// verify_batch exactness (crypto/src/lib.rs:206-219 -> dalek verify_batch):
+// dalek accepts iff sum z_i (R_i + h_i A_i - s_i B) == O for its random z_i,
+// when every A_i is torsion free (then (z_i h_i mod l) A_i == z_i h_i A_i).
+// So if every vote satisfies its own equation and every key is torsion free
+// the batch verdict is Ok for EVERY z -- exactly dalek's.  Any other outcome
+// with well-formed inputs is flagged COA_CST_VOTES_INCONCLUSIVE and the host
+// re-runs that certificate through the exact RLC kernels (coa_batch.hip) with
+// real weights; malformed inputs (s >= l, R or A not decompressing) are a
+// definitive Err, as in dalek.
+//
+// Lanes per signature: 64 for latency (one wave per signature: the 64 comb
+// terms one per lane, then a 6-level xor butterfly of point additions) and
+// 1 for throughput (64 serial mixed additions per lane).
+#include "coa_committee.h"
+
+#include "coa_fe.h"
+#include "coa_ge.h"
+#include "coa_halved.h"
+#include "coa_sc.h"
+#include "coa_sha512.h"
+#include "coa_smul.h"
+
+namespace {
+
+COA_DEV uint32_t word_sel(const uint32_t* x, int i) {
+  uint32_t w = x[0];
+#pragma unroll
+  for (int k = 1; k < 8; k++) w = i == k ? x[k] : w;
+  return w;
+}
+
+COA_DEV uint32_t byte_of(const uint32_t* x, int j) { return (word_sel(x, j >> 2) >> (8 * (j & 3))) & 0xffu; }
+
+COA_DEV void load8(uint32_t* d, const uint32_t* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 a = q[0], b = q[1];
+  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+  d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+}
+
+COA_DEV void ge_neg(ge_p3& r, const ge_p3& p) {
+  r = p;
+  fe_neg(r.X, p.X);
+  fe_neg(r.T, p.T);
+}
+
+// [m]P by MSB-first double-and-add over bits top..0 of m: an exact integer
+// multiple (registration only; latency is irrelevant there).
+COA_DEV void ge_mul_bits(ge_p3& out, const ge_p3& P, const uint32_t* m, int top) {
+  ge_cached Pc;
+  ge_p3_to_cached(Pc, P);
+  ge_p3 acc;
+  ge_p3_identity(acc);
+  ge_p1p1 t;
+#pragma unroll 1
+  for (int b = top; b >= 0; b--) {
+    ge_p3_dbl(t, acc);
+    ge_p1p1_to_p3(acc, t);
+    if ((word_sel(m, b >> 5) >> (b & 31)) & 1u) {
+      ge_add(t, acc, Pc);
+      ge_p1p1_to_p3(acc, t);
+    }
+  }
+  out = acc;
+}
+
+COA_DEV void store_niels(uint32_t* e, const ge_p3& P) {
+  fe zi, x, y, xy, d2, n0, n1, n2;
+  fe_invert(zi, P.Z);
+  fe_mul(x, P.X, zi);
+  fe_mul(y, P.Y, zi);
+  fe_mul(xy, x, y);
+  fe_const_d2(d2);
+  fe_add(n0, y, x);
+  fe_sub(n1, y, x);
+  fe_mul(n2, xy, d2);
+  fe_canon(n0, n0);
+  fe_canon(n1, n1);
+  fe_canon(n2, n2);
+  uint4* o = reinterpret_cast<uint4*>(e);
+  o[0] = make_uint4(n0.v[0], n0.v[1], n0.v[2], n0.v[3]);
+  o[1] = make_uint4(n0.v[4], n0.v[5], n0.v[6], n0.v[7]);
+  o[2] = make_uint4(n1.v[0], n1.v[1], n1.v[2], n1.v[3]);
+  o[3] = make_uint4(n1.v[4], n1.v[5], n1.v[6], n1.v[7]);
+  o[4] = make_uint4(n2.v[0], n2.v[1], n2.v[2], n2.v[3]);
+  o[5] = make_uint4(n2.v[4], n2.v[5], n2.v[6], n2.v[7]);
+}
+
+// Lexicographic compare of two 8-dword tuples (the registration sort order).
+COA_DEV int cmp8(const uint32_t* a, const uint32_t* b) {
+  int r = 0;
+#pragma unroll
+  for (int i = 7; i >= 0; i--) r = a[i] != b[i] ? (a[i] < b[i] ? -1 : 1) : r;
+  return r;
+}
+
+COA_DEV int key_lookup(const uint32_t* __restrict__ keys, uint32_t nk, const uint32_t* pk) {
+  int lo = 0, hi = (int)nk - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    uint32_t k[8];
+    load8(k, keys + (uint64_t)mid * 8);
+    const int c = cmp8(k, pk);
+    if (c == 0) return mid;
+    if (c < 0) lo = mid + 1;
+    else hi = mid - 1;
+  }
+  return -1;
+}
+
+// certificate owning vote vi: the last c with voff[c] <= vi
+COA_DEV uint32_t vote_cert(const uint64_t* __restrict__ voff, uint32_t nc, uint32_t vi) {
+  uint32_t lo = 0, hi = nc;  // voff[lo] <= vi < voff[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (voff[mid] <= vi) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <int L>
+COA_DEV void shfl_fe(fe& r, const fe& a, int off) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = (uint32_t)__shfl_xor((int)a.v[i], off, 64);
+}
+
+// One signature job; g = lane within its group of L lanes.
+template <int L>
+COA_DEV void sig_job(const CertArgs& a, uint32_t job, uint32_t g) {
+  const bool hdr = job < a.nc;
+  const uint32_t vi = job - a.nc;
+  const uint32_t c = hdr ? job : vote_cert(a.voff, a.nc, vi);
+  const uint32_t* sig = hdr ? a.hsigs + (uint64_t)c * 16 : a.vsigs + (uint64_t)vi * 16;
+  uint32_t pk[8], rw[8], sw[8], msg[8];
+  load8(pk, hdr ? a.origins + (uint64_t)c * 8 : a.vpks + (uint64_t)vi * 8);
+  load8(rw, sig);
+  load8(sw, sig + 8);
+  load8(msg, a.ids + (uint64_t)c * 8);
+  const int slot = key_lookup(a.keys, a.nk, pk);
+  uint32_t bits = 0;
+  if (slot < 0) {
+    bits = COA_CST_UNCACHED;
+  } else {
+    uint64_t st[8];
+    uint32_t h[16];
+    if (!hdr) {  // Certificate::digest = SHA-512(id || round u64 LE || origin)[..32]
+      uint32_t in[18];
+      const uint64_t rd = a.rounds[c];
+#pragma unroll
+      for (int i = 0; i < 8; i++) in[i] = msg[i];
+      in[8] = (uint32_t)rd;
+      in[9] = (uint32_t)(rd >> 32);
+      load8(in + 10, a.origins + (uint64_t)c * 8);
+      coa_sha::hash_words<18>(st, in);
+      coa_sha::state_to_le_words(h, st);
+#pragma unroll
+      for (int i = 0; i < 8; i++) msg[i] = h[i];
+    }
+    {  // k = SHA-512(R || A || M) mod l
+      uint32_t in[24];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        in[i] = rw[i];
+        in[8 + i] = pk[i];
+        in[16 + i] = msg[i];
+      }
+      coa_sha::hash_words<24>(st, in);
+      coa_sha::state_to_le_words(h, st);
+    }
+    sc k;
+    sc_reduce512(k, h);
+    const uint32_t kf = a.kflags[slot];
+    const bool s_ok = sc_is_canonical(sw);
+    const bool a_ok = (kf & COA_KEY_DECOMPRESSES) != 0;
+    // P = [s]B + [k](-A): terms t < 32 are B-comb bytes of s, t >= 32 the
+    // key-comb bytes of k (signed radix-256 digits, bytes of x + 0x80..80)
+    uint32_t sd[8], kd[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      sd[i] = sw[i];
+      kd[i] = k.v[i];
+    }
+    add_const_word(sd, 0x80808080u);
+    add_const_word(kd, 0x80808080u);
+    const uint32_t* ktab = a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS;
+    ge_p3 P;
+    ge_p1p1 t;
+    ge_p3_identity(P);
+#pragma unroll 1
+    for (int term = (int)g; term < 64; term += L) {
+      const bool isb = term < 32;
+      const int j = term & 31;
+      const int e = (int)byte_of(isb ? sd : kd, j) - 128;
+      ge_niels q;
+      comb_select(q, isb ? a.comb : ktab, j, e);
+      ge_madd(t, P, q);
+      ge_p1p1_to_p3(P, t);
+    }
+    if constexpr (L > 1) {  // butterfly: every lane of the group ends with the sum
+#pragma unroll 1
+      for (int off = L / 2; off >= 1; off >>= 1) {
+        ge_p3 O;
+        shfl_fe<L>(O.X, P.X, off);
+        shfl_fe<L>(O.Y, P.Y, off);
+        shfl_fe<L>(O.Z, P.Z, off);
+        shfl_fe<L>(O.T, P.T, off);
+        ge_cached oc;
+        ge_p3_to_cached(oc, O);
+        ge_add(t, P, oc);
+        ge_p1p1_to_p3(P, t);
+      }
+    }
+    ge_p3 R;
+    const bool r_ok = ge_decompress(R, rw);
+    ge_p2 P2;
+    ge_p3_to_p2(P2, P);
+    const bool eq = ge_p2_eq_p3(P2, R);
+    if (hdr) {
+      const bool small = (kf & COA_KEY_SMALL_ORDER) != 0 || ge_is_small_order(R);
+      bits = (s_ok && a_ok && r_ok && !small && eq) ? 0u : COA_CST_BAD_HEADER_SIG;
+    } else if (!(s_ok && a_ok && r_ok)) {
+      bits = COA_CST_BAD_VOTES;
+    } else if (!eq || !(kf & COA_KEY_TORSION_FREE)) {
+      bits = COA_CST_VOTES_INCONCLUSIVE;
+    }
+  }
+  if (g == 0 && bits) atomicOr(a.status + c, bits);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_key_flags(const uint32_t* __restrict__ keys, uint32_t nk,
+                                                   uint32_t* __restrict__ flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nk) return;
+  uint32_t w[8];
+  load8(w, keys + (uint64_t)i * 8);
+  ge_p3 A;
+  uint32_t f = 0;
+  if (ge_decompress(A, w)) {
+    f |= COA_KEY_DECOMPRESSES;
+    if (ge_is_small_order(A)) f |= COA_KEY_SMALL_ORDER;
+    uint32_t l[8];
+    sc_const_l(l);
+    ge_p3 LA;
+    ge_mul_bits(LA, A, l, 252);
+    ge_p2 q;
+    ge_p3_to_p2(q, LA);
+    if (ge_p2_is_identity(q)) f |= COA_KEY_TORSION_FREE;
+  }
+  flags[i] = f;
+}
+
+// one lane per table entry: (key, j, v) -> (v+1)*256^j*(-A)
+__global__ void __launch_bounds__(256) k_key_tables(const uint32_t* __restrict__ keys, uint32_t nk,
+                                                    uint32_t* __restrict__ tabs) {
+  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t key = (uint32_t)(id / COA_KEY_TAB_ENTRIES);
+  if (key >= nk) return;
+  const uint32_t e = (uint32_t)(id % COA_KEY_TAB_ENTRIES), j = e >> 7, v = e & 127;
+  uint32_t w[8];
+  load8(w, keys + (uint64_t)key * 8);
+  uint32_t* out = tabs + (uint64_t)key * COA_KEY_TAB_DWORDS + (uint64_t)e * 24;
+  ge_p3 A;
+  if (!ge_decompress(A, w)) {  // never selected by an accepting path; keep it a valid point
+    ge_p3_identity(A);
+  }
+  ge_p3 nA, M;
+  ge_neg(nA, A);
+  uint32_t m[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) m[i] = 0;
+  // (v+1) << 8j with v+1 <= 128: at most two dwords are nonzero
+  const uint64_t sh = (uint64_t)(v + 1) << ((8 * j) & 31);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    if (i == (int)((8 * j) >> 5)) m[i] = (uint32_t)sh;
+    if (i == (int)((8 * j) >> 5) + 1) m[i] = (uint32_t)(sh >> 32);
+  }
+  ge_mul_bits(M, nA, m, 8 * j + 7);
+  store_niels(out, M);
+}
+
+template <int L>
+__global__ void __launch_bounds__(256) k_cert_verify(CertArgs a) {
+  if (blockIdx.x < a.hdr_blocks) {  // header digest role, one lane per certificate
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.nc) return;
+    const uint64_t o0 = a.hdr_off[c], o1 = a.hdr_off[c + 1];
+    uint64_t st[8];
+    coa_sha::hash_mem(st, a.hdr_data + o0, o1 - o0);
+    uint32_t h[16], id[8];
+    coa_sha::state_to_le_words(h, st);
+    load8(id, a.ids + (uint64_t)c * 8);
+    bool same = true;
+#pragma unroll
+    for (int i = 0; i < 8; i++) same = same && h[i] == id[i];
+    if (!same) atomicOr(a.status + c, COA_CST_BAD_HEADER_ID);
+    return;
+  }
+  const uint64_t tid = (uint64_t)(blockIdx.x - a.hdr_blocks) * blockDim.x + threadIdx.x;
+  const uint64_t job = tid / L;
+  if (job >= (uint64_t)a.nc + a.nv) return;  // whole groups of L lanes leave together
+  sig_job<L>(a, (uint32_t)job, (uint32_t)(tid % L));
+}
+
+// ---------------------------------------------------------------------------
+hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s) {
+  if (nk == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_key_flags, dim3((nk + 255) / 256), dim3(256), 0, s, keys, nk, flags);
+  return hipGetLastError();
+}
+
+hipError_t coa_launch_key_tables(const uint32_t* keys, uint32_t nk, uint32_t* tabs, hipStream_t s) {
+  if (nk == 0) return hipSuccess;
+  const uint64_t lanes = (uint64_t)nk * COA_KEY_TAB_ENTRIES;
+  hipLaunchKernelGGL(k_key_tables, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, keys, nk, tabs);
+  return hipGetLastError();
+}
+
+hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, hipStream_t s) {
+  if (a.nc == 0) return hipSuccess;
+  a.hdr_blocks = (a.nc + 255) / 256;
+  const uint64_t jobs = (uint64_t)a.nc + a.nv;
+  const int L = lanes_per_sig == 64 ? 64 : 1;
+  const uint64_t sig_blocks = (jobs * L + 255) / 256;
+  const uint32_t grid = (uint32_t)(a.hdr_blocks + sig_blocks);
+  if (L == 64) hipLaunchKernelGGL(k_cert_verify<64>, dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_cert_verify<1>, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}

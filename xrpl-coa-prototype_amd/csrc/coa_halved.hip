@@ -267,38 +267,6 @@ COA_DEV int wave_max(int v) {
   return v;
 }
 
-// Comb entry (j, |e|): signed radix-256 digit e of byte position j -> ±|e|*256^j*B.
-COA_DEV void comb_select(ge_niels& q, const uint32_t* __restrict__ comb, int j, int e) {
-  const int m = e < 0 ? -e : e;
-  const int idx = m == 0 ? 0 : m - 1;
-  const uint4* src = reinterpret_cast<const uint4*>(comb + ((uint64_t)j * 128 + idx) * 24);
-  uint32_t w[24];
-#pragma unroll
-  for (int i = 0; i < 6; i++) {
-    const uint4 v = src[i];
-    w[4 * i] = v.x;
-    w[4 * i + 1] = v.y;
-    w[4 * i + 2] = v.z;
-    w[4 * i + 3] = v.w;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    q.yplusx.v[i] = w[i];
-    q.yminusx.v[i] = w[8 + i];
-    q.xy2d.v[i] = w[16 + i];
-  }
-  if (m == 0) ge_niels_identity(q);
-  ge_niels_cneg(q, e < 0);
-}
-
-COA_DEV uint32_t take_low_byte(uint32_t* x) {
-  const uint32_t lo = x[0] & 0xffu;
-#pragma unroll
-  for (int i = 0; i < 7; i++) x[i] = __builtin_amdgcn_alignbit(x[i + 1], x[i], 8);
-  x[7] >>= 8;
-  return lo;
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------------------

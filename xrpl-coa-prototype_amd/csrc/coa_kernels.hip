@@ -264,65 +264,8 @@ __global__ void __launch_bounds__(256) k_sha512_many(const uint8_t* __restrict__
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint64_t o0 = off[i], o1 = off[i + 1];
-    const uint8_t* p = data + o0;
-    const uint64_t len = o1 - o0;
     uint64_t st[8];
-    coa_sha::init(st);
-    uint64_t pos = 0;
-    // full blocks straight from memory
-    if ((o0 & 3) == 0) {
-      for (; pos + 128 <= len; pos += 128) {
-        const uint32_t* w32 = reinterpret_cast<const uint32_t*>(p + pos);
-        uint64_t W[16];
-#pragma unroll
-        for (int w = 0; w < 16; w++) W[w] = coa_sha::be64(w32[2 * w], w32[2 * w + 1]);
-        coa_sha::compress(st, W);
-      }
-    } else {
-      for (; pos + 128 <= len; pos += 128) {
-        uint64_t W[16];
-#pragma unroll
-        for (int w = 0; w < 16; w++) {
-          uint32_t lo = 0, hi = 0;
-#pragma unroll
-          for (int b = 0; b < 4; b++) {
-            lo |= (uint32_t)p[pos + 8 * w + b] << (8 * b);
-            hi |= (uint32_t)p[pos + 8 * w + 4 + b] << (8 * b);
-          }
-          W[w] = coa_sha::be64(lo, hi);
-        }
-        coa_sha::compress(st, W);
-      }
-    }
-    // tail: remaining bytes + 0x80 + zero pad + 128-bit bit length
-    const uint32_t rem = (uint32_t)(len - pos);
-    const uint32_t tail_blocks = rem + 17 <= 128 ? 1 : 2;
-    for (uint32_t tb = 0; tb < tail_blocks; tb++) {
-      uint64_t W[16];
-#pragma unroll
-      for (int w = 0; w < 16; w++) {
-        uint32_t half[2];
-#pragma unroll
-        for (int hh = 0; hh < 2; hh++) {
-          uint32_t x = 0;
-#pragma unroll
-          for (int b = 0; b < 4; b++) {
-            const uint32_t q = tb * 128 + 8 * w + 4 * hh + b;
-            uint32_t byte = 0;
-            if (q < rem) byte = p[pos + q];
-            else if (q == rem) byte = 0x80;
-            x |= byte << (8 * b);
-          }
-          half[hh] = x;
-        }
-        W[w] = coa_sha::be64(half[0], half[1]);
-      }
-      if (tb == tail_blocks - 1) {
-        W[14] = len >> 61;
-        W[15] = len << 3;
-      }
-      coa_sha::compress(st, W);
-    }
+    coa_sha::hash_mem(st, data + o0, o1 - o0);
     uint32_t h[16];
     coa_sha::state_to_le_words(h, st);
     uint4* o = reinterpret_cast<uint4*>(out + (uint64_t)i * 16);

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -24,6 +25,7 @@
 #include <vector>
 
 #include "coa_batch.h"
+#include "coa_committee.h"
 #include "coa_halved.h"
 #include "coa_kernels.h"
 
@@ -66,16 +68,42 @@ struct DevBuf {
   }
 };
 
+// Page-locked host staging (hipHostMalloc), growable: one H2D copy per call
+// on the certificate path.
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
 struct Dev {
   int id = 0;
   hipStream_t stream = nullptr;
   uint32_t* btab = nullptr;  // 128 x (j+1)B, radix-256 fixed-base table (12 KiB)
   uint32_t* comb = nullptr;  // 32 x 128 x (v+1)256^j B comb for k_verify_halved (384 KiB)
   DevBuf msgs, pks, sigs, kbuf, rec, verdicts, scratch, aux, rbuf, seeds, offs, data, out, idx, zs, terms, flags;
+  // committee key cache (f2): sorted keys, flags, one comb of -A per key
+  DevBuf ckeys, kflags, ktabs, cert;
+  uint32_t nkeys = 0;
+  PinBuf pin;
   std::mutex mu;
   std::vector<DevBuf*> all() {
-    return {&msgs, &pks,  &sigs, &kbuf, &rec, &verdicts, &scratch, &aux,  &rbuf,
-            &seeds, &offs, &data, &out,  &idx, &zs,       &terms,   &flags};
+    return {&msgs,  &pks,  &sigs, &kbuf, &rec, &verdicts, &scratch, &aux,  &rbuf,   &seeds, &offs,
+            &data,  &out,  &idx,  &zs,   &terms, &flags,  &ckeys,   &kflags, &ktabs, &cert};
   }
 };
 
@@ -299,6 +327,194 @@ int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* si
   });
 }
 
+// ------------------------------------------------------------------------
+// Certificate::verify crypto (f2 + f3).  Inputs of a shard [lo, hi) are
+// packed into the device's pinned staging buffer and copied with ONE H2D; the
+// status words come back with one D2H.
+struct CertIn {
+  const uint8_t* hdr_data;
+  const uint64_t* hdr_off;
+  const uint8_t* ids;
+  const uint8_t* origins;
+  const uint8_t* hsigs;
+  const uint64_t* rounds;
+  const uint8_t* vpks;
+  const uint8_t* vsigs;
+  const uint64_t* voff;
+};
+
+// COA_CERT_LANES=1|64 forces the lanes-per-signature variant.
+int cert_lanes(size_t jobs) {
+  const char* e = getenv("COA_CERT_LANES");
+  if (e && std::string(e) == "1") return 1;
+  if (e && std::string(e) == "64") return 64;
+  return jobs <= 2048 ? 64 : 1;
+}
+
+struct CertPack {
+  size_t status, hoff, ids, origins, hsigs, rounds, voff, vpks, vsigs, hdata, total;
+};
+CertPack cert_layout(size_t nc, size_t nv, size_t hbytes) {
+  CertPack p;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = align_up(o + bytes, 256);
+    return at;
+  };
+  p.status = take(nc * 4);
+  p.hoff = take((nc + 1) * 8);
+  p.ids = take(nc * 32);
+  p.origins = take(nc * 32);
+  p.hsigs = take(nc * 64);
+  p.rounds = take(nc * 8);
+  p.voff = take((nc + 1) * 8);
+  p.vpks = take(nv * 32);
+  p.vsigs = take(nv * 64);
+  p.hdata = take(hbytes + 16);
+  p.total = o;
+  return p;
+}
+
+CertArgs cert_args(Dev& d, uint8_t* base, const CertPack& p, size_t nc, size_t nv) {
+  CertArgs a;
+  a.hdr_data = base + p.hdata;
+  a.hdr_off = reinterpret_cast<const uint64_t*>(base + p.hoff);
+  a.ids = reinterpret_cast<const uint32_t*>(base + p.ids);
+  a.origins = reinterpret_cast<const uint32_t*>(base + p.origins);
+  a.hsigs = reinterpret_cast<const uint32_t*>(base + p.hsigs);
+  a.rounds = reinterpret_cast<const uint64_t*>(base + p.rounds);
+  a.vpks = reinterpret_cast<const uint32_t*>(base + p.vpks);
+  a.vsigs = reinterpret_cast<const uint32_t*>(base + p.vsigs);
+  a.voff = reinterpret_cast<const uint64_t*>(base + p.voff);
+  a.nc = (uint32_t)nc;
+  a.nv = (uint32_t)nv;
+  a.hdr_blocks = 0;
+  a.keys = d.ckeys.as<uint32_t>();
+  a.kflags = d.kflags.as<uint32_t>();
+  a.ktabs = d.ktabs.as<uint32_t>();
+  a.nk = d.nkeys;
+  a.comb = d.comb;
+  a.status = reinterpret_cast<uint32_t*>(base + p.status);
+  return a;
+}
+
+// Fast path for certificates [lo, hi) on one device: raw status words out.
+int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_out) {
+  const size_t nc = hi - lo;
+  const uint64_t h0 = in.hdr_off[lo], hb = in.hdr_off[hi] - h0;
+  const uint64_t v0 = in.voff[lo], nv = in.voff[hi] - v0;
+  const CertPack p = cert_layout(nc, nv, hb);
+  HIP_TRY(d.pin.ensure(p.total));
+  HIP_TRY(d.cert.ensure(p.total));
+  uint8_t* h = static_cast<uint8_t*>(d.pin.p);
+  std::memset(h + p.status, 0, nc * 4);
+  uint64_t* ho = reinterpret_cast<uint64_t*>(h + p.hoff);
+  uint64_t* vo = reinterpret_cast<uint64_t*>(h + p.voff);
+  for (size_t i = 0; i <= nc; i++) {
+    ho[i] = in.hdr_off[lo + i] - h0;
+    vo[i] = in.voff[lo + i] - v0;
+  }
+  std::memcpy(h + p.ids, in.ids + lo * 32, nc * 32);
+  std::memcpy(h + p.origins, in.origins + lo * 32, nc * 32);
+  std::memcpy(h + p.hsigs, in.hsigs + lo * 64, nc * 64);
+  std::memcpy(h + p.rounds, in.rounds + lo, nc * 8);
+  if (nv) {
+    std::memcpy(h + p.vpks, in.vpks + v0 * 32, nv * 32);
+    std::memcpy(h + p.vsigs, in.vsigs + v0 * 64, nv * 64);
+  }
+  if (hb) std::memcpy(h + p.hdata, in.hdr_data + h0, hb);
+  hipStream_t s = d.stream;
+  HIP_TRY(hipMemcpyAsync(d.cert.p, h, p.total, hipMemcpyHostToDevice, s));
+  CertArgs a = cert_args(d, d.cert.as<uint8_t>(), p, nc, nv);
+  HIP_TRY(coa_launch_cert_verify(a, cert_lanes(nc + nv), s));
+  HIP_TRY(hipMemcpyAsync(h + p.status, d.cert.as<uint8_t>() + p.status, nc * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  std::memcpy(status_out + lo, h + p.status, nc * 4);
+  return COA_OK;
+}
+
+// Exact (non-cached) resolution of certificates `idx`: header signatures by
+// verify_strict (only when `hdr_too`), votes by the RLC kernels over
+// Certificate::digest.  ORs COA_CST_BAD_* into status.
+int cert_resolve(const CertIn& in, const std::vector<size_t>& idx, bool hdr_too, uint64_t seed, uint32_t* status) {
+  if (idx.empty()) return COA_OK;
+  const size_t m = idx.size();
+  // Certificate::digest inputs: id || round LE || origin (72 B)
+  std::vector<uint8_t> cin(m * 72), dig(m * 64);
+  std::vector<uint64_t> coff(m + 1);
+  for (size_t j = 0; j < m; j++) {
+    const size_t c = idx[j];
+    std::memcpy(&cin[j * 72], in.ids + c * 32, 32);
+    std::memcpy(&cin[j * 72 + 32], &in.rounds[c], 8);
+    std::memcpy(&cin[j * 72 + 40], in.origins + c * 32, 32);
+    coff[j] = j * 72;
+  }
+  coff[m] = m * 72;
+  int rc = coa_sha512_many(cin.data(), coff.data(), m, dig.data());
+  if (rc != COA_OK) return rc;
+  std::vector<uint8_t> gm(m * 32), gv(m), vp, vs;
+  std::vector<uint64_t> goff(m + 1, 0);
+  for (size_t j = 0; j < m; j++) {
+    const size_t c = idx[j];
+    std::memcpy(&gm[j * 32], &dig[j * 64], 32);
+    const uint64_t a = in.voff[c], b = in.voff[c + 1];
+    vp.insert(vp.end(), in.vpks + a * 32, in.vpks + b * 32);
+    vs.insert(vs.end(), in.vsigs + a * 64, in.vsigs + b * 64);
+    goff[j + 1] = goff[j] + (b - a);
+  }
+  rc = batch_groups_impl(gm.data(), vp.data(), vs.data(), goff.data(), m, nullptr, seed, gv.data());
+  if (rc != COA_OK) return rc;
+  std::vector<uint8_t> hv(m, 0);
+  if (hdr_too) {
+    std::vector<uint8_t> hm(m * 32), hp(m * 32), hs(m * 64);
+    for (size_t j = 0; j < m; j++) {
+      const size_t c = idx[j];
+      std::memcpy(&hm[j * 32], in.ids + c * 32, 32);
+      std::memcpy(&hp[j * 32], in.origins + c * 32, 32);
+      std::memcpy(&hs[j * 64], in.hsigs + c * 64, 64);
+    }
+    rc = coa_ed25519_verify_strict_many(hm.data(), 32, hp.data(), hs.data(), m, hv.data());
+    if (rc != COA_OK) return rc;
+  }
+  for (size_t j = 0; j < m; j++) {
+    status[idx[j]] |= (gv[j] ? COA_CST_BAD_VOTES : 0u) | (hv[j] ? COA_CST_BAD_HEADER_SIG : 0u);
+  }
+  return COA_OK;
+}
+
+int certificates_impl(const CertIn& in, size_t n, uint64_t rng_seed, uint8_t* status_out) {
+  if (n == 0) return COA_OK;
+  if (!in.hdr_off || !in.ids || !in.origins || !in.hsigs || !in.rounds || !in.voff || !status_out)
+    return fail(COA_EINVAL, "null argument");
+  for (size_t i = 0; i < n; i++)
+    if (in.hdr_off[i + 1] < in.hdr_off[i] || in.voff[i + 1] < in.voff[i])
+      return fail(COA_EINVAL, "offsets not monotone");
+  if (in.voff[0] != 0) return fail(COA_EINVAL, "vote_offsets[0] must be 0");
+  if (in.hdr_off[n] > in.hdr_off[0] && !in.hdr_data) return fail(COA_EINVAL, "null header data");
+  if (in.voff[n] && (!in.vpks || !in.vsigs)) return fail(COA_EINVAL, "null vote arrays");
+  if (check_n(n + in.voff[n]) != COA_OK) return COA_EINVAL;
+  std::vector<uint32_t> st(n, 0);
+  int rc = for_shards(n, [&](Dev& d, size_t lo, size_t hi) -> int { return cert_shard(d, in, lo, hi, st.data()); });
+  if (rc != COA_OK) return rc;
+  std::vector<size_t> uncached, rlc;
+  for (size_t i = 0; i < n; i++) {
+    if (st[i] & COA_CST_UNCACHED) {
+      st[i] &= COA_CST_BAD_HEADER_ID;  // the digest check does not use the cache
+      uncached.push_back(i);
+    } else if ((st[i] & COA_CST_VOTES_INCONCLUSIVE) && !(st[i] & COA_CST_BAD_VOTES)) {
+      rlc.push_back(i);
+    }
+  }
+  const uint64_t seed = rng_seed ? rng_seed : os_entropy_seed();
+  rc = cert_resolve(in, uncached, true, seed, st.data());
+  if (rc != COA_OK) return rc;
+  rc = cert_resolve(in, rlc, false, seed, st.data());
+  if (rc != COA_OK) return rc;
+  for (size_t i = 0; i < n; i++) status_out[i] = (uint8_t)(st[i] & 7u);
+  return COA_OK;
+}
+
 int sign_enqueue(Dev& d, const uint8_t* d_seeds, const uint8_t* d_msgs, size_t msg_len, size_t n, uint8_t* d_pks,
                  uint8_t* d_sigs, hipStream_t s) {
   HIP_TRY(d.aux.ensure(n * 64 + 64));
@@ -333,6 +549,8 @@ int coa_shutdown(void) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
     for (DevBuf* b : d->all()) b->release();
+    d->pin.release();
+    d->nkeys = 0;
     if (d->btab) (void)hipFree(d->btab);
     if (d->comb) (void)hipFree(d->comb);
     (void)hipStreamDestroy(d->stream);
@@ -582,6 +800,110 @@ int coa_ed25519_sign_many_device(int device, const uint8_t* d_seeds, const uint8
   rc = sign_enqueue(*d, d_seeds, d_msgs, msg_len, n, d_pks_out, d_sigs_out, s);
   if (rc != COA_OK) return rc;
   HIP_TRY(hipStreamSynchronize(s));
+  return COA_OK;
+}
+
+
+int coa_committee_register(const uint8_t* pks, size_t n) {
+  int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  if (n && !pks) return fail(COA_EINVAL, "null argument");
+  if (n > (1u << 20)) return fail(COA_EINVAL, "committee too large");
+  std::vector<std::array<uint32_t, 8>> keys(n);
+  for (size_t i = 0; i < n; i++) std::memcpy(keys[i].data(), pks + i * 32, 32);
+  std::sort(keys.begin(), keys.end());
+  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  const size_t nk = keys.size();
+  for (auto& dp : g_devs) {
+    Dev& d = *dp;
+    std::lock_guard<std::mutex> l(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    d.nkeys = 0;
+    if (nk == 0) continue;
+    HIP_TRY(d.ckeys.ensure(nk * 32));
+    HIP_TRY(d.kflags.ensure(nk * 4));
+    HIP_TRY(d.ktabs.ensure(nk * (size_t)COA_KEY_TAB_DWORDS * 4));
+    HIP_TRY(hipMemcpyAsync(d.ckeys.p, keys.data(), nk * 32, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(coa_launch_key_flags(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.kflags.as<uint32_t>(), d.stream));
+    HIP_TRY(coa_launch_key_tables(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.ktabs.as<uint32_t>(), d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    d.nkeys = (uint32_t)nk;
+  }
+  return (int)nk;
+}
+
+int coa_committee_key_flags(uint32_t* flags_out, size_t cap) {
+  int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  Dev& d = *g_devs[0];
+  std::lock_guard<std::mutex> l(d.mu);
+  const size_t nk = std::min<size_t>(d.nkeys, cap);
+  if (nk == 0) return (int)d.nkeys;
+  if (!flags_out) return fail(COA_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(d.id));
+  HIP_TRY(hipMemcpyAsync(flags_out, d.kflags.p, nk * 4, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  return (int)d.nkeys;
+}
+
+int coa_certificate_verify_many(const uint8_t* header_data, const uint64_t* header_offsets, const uint8_t* ids,
+                                const uint8_t* origins, const uint8_t* header_sigs, const uint64_t* rounds,
+                                const uint8_t* vote_pks, const uint8_t* vote_sigs, const uint64_t* vote_offsets,
+                                size_t n, uint64_t rng_seed, uint8_t* status_out) {
+  int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  const CertIn in{header_data, header_offsets, ids, origins, header_sigs, rounds, vote_pks, vote_sigs, vote_offsets};
+  return certificates_impl(in, n, rng_seed, status_out);
+}
+
+int coa_certificate_verify(const uint8_t* header_data, size_t header_len, const uint8_t id[32],
+                           const uint8_t origin[32], const uint8_t header_sig[64], uint64_t round,
+                           const uint8_t* vote_pks, const uint8_t* vote_sigs, size_t n_votes, uint64_t rng_seed) {
+  const uint64_t hoff[2] = {0, (uint64_t)header_len};
+  const uint64_t voff[2] = {0, (uint64_t)n_votes};
+  uint8_t st = 0;
+  const int rc = coa_certificate_verify_many(header_data, hoff, id, origin, header_sig, &round, vote_pks, vote_sigs,
+                                             voff, 1, rng_seed, &st);
+  return rc != COA_OK ? rc : (int)st;
+}
+
+int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data, const uint64_t* d_header_offsets,
+                                       const uint8_t* d_ids, const uint8_t* d_origins, const uint8_t* d_header_sigs,
+                                       const uint64_t* d_rounds, const uint8_t* d_vote_pks,
+                                       const uint8_t* d_vote_sigs, const uint64_t* d_vote_offsets, size_t n,
+                                       size_t n_votes, uint32_t* d_status, void* stream) {
+  int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  if (n == 0) return COA_OK;
+  if (!d_header_offsets || !d_ids || !d_origins || !d_header_sigs || !d_rounds || !d_vote_offsets || !d_status ||
+      (n_votes && (!d_vote_pks || !d_vote_sigs)))
+    return fail(COA_EINVAL, "null argument");
+  if (check_n(n + n_votes) != COA_OK) return COA_EINVAL;
+  Dev* d = dev_by_id(device);
+  if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  CertArgs a;
+  a.hdr_data = d_header_data;
+  a.hdr_off = d_header_offsets;
+  a.ids = reinterpret_cast<const uint32_t*>(d_ids);
+  a.origins = reinterpret_cast<const uint32_t*>(d_origins);
+  a.hsigs = reinterpret_cast<const uint32_t*>(d_header_sigs);
+  a.rounds = d_rounds;
+  a.vpks = reinterpret_cast<const uint32_t*>(d_vote_pks);
+  a.vsigs = reinterpret_cast<const uint32_t*>(d_vote_sigs);
+  a.voff = d_vote_offsets;
+  a.nc = (uint32_t)n;
+  a.nv = (uint32_t)n_votes;
+  a.hdr_blocks = 0;
+  a.keys = d->ckeys.as<uint32_t>();
+  a.kflags = d->kflags.as<uint32_t>();
+  a.ktabs = d->ktabs.as<uint32_t>();
+  a.nk = d->nkeys;
+  a.comb = d->comb;
+  a.status = d_status;
+  HIP_TRY(hipMemsetAsync(d_status, 0, n * 4, s));
+  HIP_TRY(coa_launch_cert_verify(a, cert_lanes(n + n_votes), s));
   return COA_OK;
 }
 

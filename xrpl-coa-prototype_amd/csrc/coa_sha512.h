@@ -5,8 +5,6 @@
 // 228-232) and inside ed25519 verification (k = H(R || A || M),
 // ed25519-dalek 1.0.1 verify_strict / verify_batch).
 //
-// 64-bit words are kept as uint64_t; hipcc lowers the rotations to
-// v_alignbit_b32 pairs and Ch/Maj to v_bitop3_b32 on gfx950.
 #pragma once
 #include "coa_fe.h"
 
@@ -34,7 +32,38 @@ __device__ __constant__ static const uint64_t K512[80] = {
     0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
     0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
 
-COA_DEV uint64_t rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit words live in VGPR pairs.  gfx950 has no 64-bit rotate, and hipcc
+// lowers `(x >> n) | (x << (64 - n))` to two 64-bit shifts plus two ORs; a
+// rotate is instead two v_alignbit_b32 (one per half), three-way XORs and
+// Ch/Maj are one v_bitop3_b32 per half, and 64-bit adds are v_lshl_add_u64.
+// That takes a round from ~75 to ~40 VALU instructions.
+COA_DEV uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+COA_DEV uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+COA_DEV uint64_t mk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+template <int N>
+COA_DEV uint64_t rotr(uint64_t x) {
+  static_assert(N > 0 && N < 64 && N != 32, "rotate amount");
+  const uint32_t l = lo32(x), h = hi32(x);
+  if constexpr (N < 32)
+    return mk64(__builtin_amdgcn_alignbit(h, l, N), __builtin_amdgcn_alignbit(l, h, N));
+  else
+    return mk64(__builtin_amdgcn_alignbit(l, h, N - 32), __builtin_amdgcn_alignbit(h, l, N - 32));
+}
+template <int N>
+COA_DEV uint64_t shr(uint64_t x) {
+  static_assert(N > 0 && N < 32, "shift amount");
+  return mk64(__builtin_amdgcn_alignbit(hi32(x), lo32(x), N), hi32(x) >> N);
+}
+// bitop3 truth tables over (S0, S1, S2) = (0xF0, 0xCC, 0xAA)
+template <unsigned TT>
+COA_DEV uint64_t bitop3(uint64_t a, uint64_t b, uint64_t c) {
+  return mk64(__builtin_amdgcn_bitop3_b32(lo32(a), lo32(b), lo32(c), TT),
+              __builtin_amdgcn_bitop3_b32(hi32(a), hi32(b), hi32(c), TT));
+}
+COA_DEV uint64_t xor3(uint64_t a, uint64_t b, uint64_t c) { return bitop3<0x96>(a, b, c); }
+COA_DEV uint64_t ch(uint64_t e, uint64_t f, uint64_t g) { return bitop3<0xCA>(e, f, g); }
+COA_DEV uint64_t maj(uint64_t a, uint64_t b, uint64_t c) { return bitop3<0xE8>(a, b, c); }
 
 COA_DEV void init(uint64_t st[8]) {
   st[0] = 0x6a09e667f3bcc908ull;
@@ -47,36 +76,52 @@ COA_DEV void init(uint64_t st[8]) {
   st[7] = 0x5be0cd19137e2179ull;
 }
 
+// One round with the working variables passed by name (the usual renaming:
+// only d and h are written).
+COA_DEV void round_(uint64_t a, uint64_t b, uint64_t c, uint64_t& d, uint64_t e, uint64_t f, uint64_t g,
+                    uint64_t& h, uint64_t kw) {
+  const uint64_t t1 = h + xor3(rotr<14>(e), rotr<18>(e), rotr<41>(e)) + ch(e, f, g) + kw;
+  const uint64_t t2 = xor3(rotr<28>(a), rotr<34>(a), rotr<39>(a)) + maj(a, b, c);
+  d += t1;
+  h = t1 + t2;
+}
+
 // One 128-byte block; W holds the 16 big-endian message words (clobbered).
+// Five passes of 16 rounds: every W index is static (no dynamic VGPR
+// indexing), K512 comes in through scalar loads.  Passes 2-5 first extend
+// the schedule in place, W[i] = W[i] + s0(W[i+1]) + W[i+9] + s1(W[i+14])
+// (indices mod 16), which is exactly W[t] from W[t-16], W[t-15], W[t-7] and
+// W[t-2] when evaluated in increasing i.
 COA_DEV void compress(uint64_t st[8], uint64_t W[16]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3];
   uint64_t e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll 1
+  for (int r = 0; r < 80; r += 16) {
+    if (r) {
 #pragma unroll
-  for (int t = 0; t < 80; t++) {
-    uint64_t w;
-    if (t < 16) {
-      w = W[t];
-    } else {
-      const uint64_t w15 = W[(t - 15) & 15], w2 = W[(t - 2) & 15];
-      const uint64_t s0 = rotr(w15, 1) ^ rotr(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = rotr(w2, 19) ^ rotr(w2, 61) ^ (w2 >> 6);
-      w = W[t & 15] + s0 + W[(t - 7) & 15] + s1;
-      W[t & 15] = w;
+      for (int i = 0; i < 16; i++) {
+        const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
+        W[i] += xor3(rotr<1>(w15), rotr<8>(w15), shr<7>(w15)) + W[(i + 9) & 15] +
+                xor3(rotr<19>(w2), rotr<61>(w2), shr<6>(w2));
+      }
     }
-    const uint64_t S1 = rotr(e, 14) ^ rotr(e, 18) ^ rotr(e, 41);
-    const uint64_t ch = (e & f) ^ (~e & g);
-    const uint64_t t1 = h + S1 + ch + K512[t] + w;
-    const uint64_t S0 = rotr(a, 28) ^ rotr(a, 34) ^ rotr(a, 39);
-    const uint64_t maj = (a & b) ^ (a & c) ^ (b & c);
-    const uint64_t t2 = S0 + maj;
-    h = g;
-    g = f;
-    f = e;
-    e = d + t1;
-    d = c;
-    c = b;
-    b = a;
-    a = t1 + t2;
+    const uint64_t* K = K512 + r;
+    round_(a, b, c, d, e, f, g, h, K[0] + W[0]);
+    round_(h, a, b, c, d, e, f, g, K[1] + W[1]);
+    round_(g, h, a, b, c, d, e, f, K[2] + W[2]);
+    round_(f, g, h, a, b, c, d, e, K[3] + W[3]);
+    round_(e, f, g, h, a, b, c, d, K[4] + W[4]);
+    round_(d, e, f, g, h, a, b, c, K[5] + W[5]);
+    round_(c, d, e, f, g, h, a, b, K[6] + W[6]);
+    round_(b, c, d, e, f, g, h, a, K[7] + W[7]);
+    round_(a, b, c, d, e, f, g, h, K[8] + W[8]);
+    round_(h, a, b, c, d, e, f, g, K[9] + W[9]);
+    round_(g, h, a, b, c, d, e, f, K[10] + W[10]);
+    round_(f, g, h, a, b, c, d, e, K[11] + W[11]);
+    round_(e, f, g, h, a, b, c, d, K[12] + W[12]);
+    round_(d, e, f, g, h, a, b, c, K[13] + W[13]);
+    round_(c, d, e, f, g, h, a, b, K[14] + W[14]);
+    round_(b, c, d, e, f, g, h, a, K[15] + W[15]);
   }
   st[0] += a;
   st[1] += b;
@@ -167,6 +212,99 @@ COA_DEV void hash_segs(uint64_t st[8], const Segs& s, bool aligned) {
     }
     compress(st, W);
   }
+}
+
+// ------------------------------------------------------------------------
+// SHA-512 of p[0 .. len) in global memory, one lane (the worker batch and
+// header digests).  Full blocks are read as dwords when p is 4-byte aligned
+// (byte gathers otherwise); the tail block(s) carry the 0x80 terminator and
+// the 128-bit bit length.
+COA_DEV void hash_mem(uint64_t st[8], const uint8_t* p, uint64_t len) {
+  init(st);
+  uint64_t pos = 0;
+  if ((reinterpret_cast<uintptr_t>(p) & 3) == 0) {
+    // one block of prefetch: block i+1's loads are in flight while block i
+    // is compressed (a lone lane hashing a long header is latency-bound)
+    uint4 nxt[8];
+    if (len >= 128) {
+#pragma unroll
+      for (int q = 0; q < 8; q++) nxt[q] = reinterpret_cast<const uint4*>(p)[q];
+    }
+    for (; pos + 128 <= len; pos += 128) {
+      uint64_t W[16];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        W[2 * q] = be64(nxt[q].x, nxt[q].y);
+        W[2 * q + 1] = be64(nxt[q].z, nxt[q].w);
+      }
+      if (pos + 256 <= len) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) nxt[q] = reinterpret_cast<const uint4*>(p + pos + 128)[q];
+      }
+      compress(st, W);
+    }
+  } else {
+    for (; pos + 128 <= len; pos += 128) {
+      uint64_t W[16];
+#pragma unroll
+      for (int w = 0; w < 16; w++) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          lo |= (uint32_t)p[pos + 8 * w + b] << (8 * b);
+          hi |= (uint32_t)p[pos + 8 * w + 4 + b] << (8 * b);
+        }
+        W[w] = be64(lo, hi);
+      }
+      compress(st, W);
+    }
+  }
+  const uint32_t rem = (uint32_t)(len - pos);
+  const uint32_t tail_blocks = rem + 17 <= 128 ? 1 : 2;
+  for (uint32_t tb = 0; tb < tail_blocks; tb++) {
+    uint64_t W[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+      uint32_t half[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; hh++) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint32_t q = tb * 128 + 8 * w + 4 * hh + b;
+          uint32_t byte = 0;
+          if (q < rem) byte = p[pos + q];
+          else if (q == rem) byte = 0x80;
+          x |= byte << (8 * b);
+        }
+        half[hh] = x;
+      }
+      W[w] = be64(half[0], half[1]);
+    }
+    if (tb == tail_blocks - 1) {
+      W[14] = len >> 61;
+      W[15] = len << 3;
+    }
+    compress(st, W);
+  }
+}
+
+// SHA-512 of a short message held in registers: NW little-endian dwords in
+// memory order (4*NW <= 108 bytes, so one block).  Used for the certificate
+// digest (72 B) and k = H(R || A || M) (96 B) inside the fused kernels.
+template <int NW>
+COA_DEV void hash_words(uint64_t st[8], const uint32_t* w) {
+  static_assert(NW % 2 == 0 && 4 * NW + 17 <= 128, "one-block message");
+  uint64_t W[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    if (2 * i + 1 < NW) W[i] = be64(w[2 * i], w[2 * i + 1]);
+    else if (2 * i == NW) W[i] = 0x8000000000000000ull;
+    else W[i] = 0;
+  }
+  W[15] = (uint64_t)NW * 32;
+  init(st);
+  compress(st, W);
 }
 
 }  // namespace coa_sha
