@@ -35,9 +35,17 @@
 // real weights; malformed inputs (s >= l, R or A not decompressing) are a
 // definitive Err, as in dalek.
 //
-// Lanes per signature: 64 for latency (one wave per signature: the 64 comb
-// terms one per lane, then a 6-level xor butterfly of point additions) and
-// 1 for throughput (64 serial mixed additions per lane).
+// Two variants:
+//   k_cert_verify<1>   throughput: one lane per signature (64 serial mixed
+//                      additions), one lane per header digest
+//   k_cert_verify_lat  latency: one 128-thread workgroup per signature --
+//                      wave 0 hashes Certificate::digest and k, takes one
+//                      comb term per lane, sums the 64 terms by a 6-level
+//                      xor butterfly and tests P for small order, while
+//                      wave 1 decompresses R; the two meet in LDS.  One
+//                      workgroup per header digest: its lanes expand every
+//                      block's message schedule into LDS, then one wave
+//                      runs the rounds (coa_sha512.h, compress_kw).
 #include "coa_committee.h"
 
 #include "coa_fe.h"
@@ -63,6 +71,16 @@ COA_DEV void load8(uint32_t* d, const uint32_t* p) {
   const uint4 a = q[0], b = q[1];
   d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
   d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+}
+
+// wave-uniform copies (SGPRs) of values every lane loaded alike
+COA_DEV void load8u(uint32_t* d, const uint32_t* p) {
+  load8(d, p);
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = coa_sha::uni(d[i]);
+}
+COA_DEV uint64_t uni64(uint64_t v) {
+  return ((uint64_t)coa_sha::uni((uint32_t)(v >> 32)) << 32) | coa_sha::uni((uint32_t)v);
 }
 
 COA_DEV void ge_neg(ge_p3& r, const ge_p3& p) {
@@ -135,12 +153,36 @@ COA_DEV int key_lookup(const uint32_t* __restrict__ keys, uint32_t nk, const uin
   return -1;
 }
 
+COA_DEV int key_lookup_u(const uint32_t* __restrict__ keys, uint32_t nk, const uint32_t* pk) {
+  int lo = 0, hi = (int)nk - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    uint32_t k[8];
+    load8u(k, keys + (uint64_t)mid * 8);
+    const int c = cmp8(k, pk);
+    if (c == 0) return mid;
+    if (c < 0) lo = mid + 1;
+    else hi = mid - 1;
+  }
+  return -1;
+}
+
 // certificate owning vote vi: the last c with voff[c] <= vi
 COA_DEV uint32_t vote_cert(const uint64_t* __restrict__ voff, uint32_t nc, uint32_t vi) {
   uint32_t lo = 0, hi = nc;  // voff[lo] <= vi < voff[hi]
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
     if (voff[mid] <= vi) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+COA_DEV uint32_t vote_cert_u(const uint64_t* __restrict__ voff, uint32_t nc, uint32_t vi) {
+  uint32_t lo = 0, hi = nc;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (uni64(voff[mid]) <= vi) lo = mid;
     else hi = mid;
   }
   return lo;
@@ -333,6 +375,167 @@ __global__ void __launch_bounds__(256) k_cert_verify(CertArgs a) {
   sig_job<L>(a, (uint32_t)job, (uint32_t)(tid % L));
 }
 
+
+// ---------------------------------------------------------------------------
+// Latency variant (one certificate at a time): see the file comment.
+// Blocks [0, nc): header digests (wave 0 of each).  Blocks [nc, 2nc + nv):
+// one signature job each.
+#define KW_CHUNK 64  // blocks of schedule per LDS pass (40 KiB)
+__global__ void __launch_bounds__(128) k_cert_verify_lat(CertArgs a) {
+  const uint32_t wave = coa_sha::uni(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (blockIdx.x < a.nc) {  // header digest: schedule in parallel, rounds on wave 0
+    __shared__ uint64_t kw_lds[KW_CHUNK * 80];
+    const uint32_t c = blockIdx.x;
+    const uint64_t o0 = uni64(a.hdr_off[c]), len = uni64(a.hdr_off[c + 1]) - o0;
+    const uint8_t* p = a.hdr_data + o0;
+    const uint64_t nblk = (len + 17 + 127) / 128;
+    uint64_t st[8];
+    coa_sha::init(st);
+#pragma unroll 1
+    for (uint64_t b0 = 0; b0 < nblk; b0 += KW_CHUNK) {
+      const uint32_t nb = (uint32_t)min<uint64_t>(KW_CHUNK, nblk - b0);
+      if (threadIdx.x < nb) {
+        uint64_t W[16];
+        coa_sha::padded_block(W, p, len, b0 + threadIdx.x, nblk);
+        coa_sha::expand_kw(kw_lds + threadIdx.x * 80, W);
+      }
+      __syncthreads();
+      if (wave == 0) {
+#pragma unroll 1
+        for (uint32_t b = 0; b < nb; b++) coa_sha::compress_kw(st, kw_lds + b * 80);
+      }
+      __syncthreads();
+    }
+    if (wave) return;
+    uint32_t h[16], id[8];
+    coa_sha::state_to_le_words(h, st);
+    load8u(id, a.ids + (uint64_t)c * 8);
+    bool same = true;
+#pragma unroll
+    for (int i = 0; i < 8; i++) same = same && h[i] == id[i];
+    if (lane == 0 && !same) atomicOr(a.status + c, COA_CST_BAD_HEADER_ID);
+    return;
+  }
+  __shared__ uint32_t r_lds[17];  // R.X, R.Y, decompress ok
+  const uint32_t job = blockIdx.x - a.nc;
+  const bool hdr = job < a.nc;
+  const uint32_t vi = job - a.nc;
+  const uint32_t c = hdr ? job : vote_cert_u(a.voff, a.nc, vi);
+  const uint32_t* sig = hdr ? a.hsigs + (uint64_t)c * 16 : a.vsigs + (uint64_t)vi * 16;
+  uint32_t rw[8];
+  load8u(rw, sig);
+  uint32_t bits = 0;
+  ge_p3 P;
+  if (wave == 1) {  // R's decompression
+    ge_p3 R;
+    const bool ok = ge_decompress(R, rw);
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        r_lds[i] = R.X.v[i];
+        r_lds[8 + i] = R.Y.v[i];
+      }
+      r_lds[16] = ok;
+    }
+  } else {
+    uint32_t pk[8], sw[8], msg[8];
+    load8u(pk, hdr ? a.origins + (uint64_t)c * 8 : a.vpks + (uint64_t)vi * 8);
+    load8u(sw, sig + 8);
+    load8u(msg, a.ids + (uint64_t)c * 8);
+    const int slot = key_lookup_u(a.keys, a.nk, pk);
+    if (slot < 0) {
+      bits = COA_CST_UNCACHED;
+    } else {
+      uint64_t st[8];
+      uint32_t h[16];
+      if (!hdr) {  // Certificate::digest on the scalar unit
+        uint32_t in[18];
+        const uint64_t rd = uni64(a.rounds[c]);
+#pragma unroll
+        for (int i = 0; i < 8; i++) in[i] = msg[i];
+        in[8] = (uint32_t)rd;
+        in[9] = (uint32_t)(rd >> 32);
+        load8u(in + 10, a.origins + (uint64_t)c * 8);
+        coa_sha::hash_words<18>(st, in);
+        coa_sha::state_to_le_words(h, st);
+#pragma unroll
+        for (int i = 0; i < 8; i++) msg[i] = h[i];
+      }
+      uint32_t in[24];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        in[i] = rw[i];
+        in[8 + i] = pk[i];
+        in[16 + i] = msg[i];
+      }
+      coa_sha::hash_words<24>(st, in);
+      coa_sha::state_to_le_words(h, st);
+      sc k;
+      sc_reduce512(k, h);
+      const uint32_t kf = coa_sha::uni(a.kflags[slot]);
+      const bool s_ok = sc_is_canonical(sw);
+      const bool a_ok = (kf & COA_KEY_DECOMPRESSES) != 0;
+      uint32_t dg[8];  // this lane's scalar: s for lanes < 32, k above
+#pragma unroll
+      for (int i = 0; i < 8; i++) dg[i] = lane < 32 ? sw[i] : k.v[i];
+      add_const_word(dg, 0x80808080u);
+      const int j = lane & 31;
+      const int e = (int)byte_of(dg, j) - 128;
+      ge_niels q;
+      comb_select(q, lane < 32 ? a.comb : a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS, j, e);
+      ge_p1p1 t;
+      ge_p3_identity(P);
+      ge_madd(t, P, q);
+      ge_p1p1_to_p3(P, t);
+#pragma unroll 1
+      for (int off = 32; off >= 1; off >>= 1) {
+        ge_p3 O;
+        shfl_fe<64>(O.X, P.X, off);
+        shfl_fe<64>(O.Y, P.Y, off);
+        shfl_fe<64>(O.Z, P.Z, off);
+        shfl_fe<64>(O.T, P.T, off);
+        ge_cached oc;
+        ge_p3_to_cached(oc, O);
+        ge_add(t, P, oc);
+        ge_p1p1_to_p3(P, t);
+      }
+      // verify_strict's small-order test of R, taken on P: an accepting
+      // verdict needs R == P, and every other verdict is Err already
+      const bool small_p = hdr && ge_is_small_order(P);
+      bits = (s_ok ? 0u : 1u) | (a_ok ? 0u : 2u) | ((kf & COA_KEY_SMALL_ORDER) ? 4u : 0u) |
+             ((kf & COA_KEY_TORSION_FREE) ? 0u : 8u) | (small_p ? 16u : 0u);
+      bits <<= 8;  // pre-verdict flags, resolved after the hand-off
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    if (!(bits & COA_CST_UNCACHED)) {
+      const uint32_t pre = bits >> 8;
+      ge_p3 R;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        R.X.v[i] = r_lds[i];
+        R.Y.v[i] = r_lds[8 + i];
+      }
+      fe_set(R.Z, 1);
+      const bool r_ok = r_lds[16] != 0, small_r = (pre & 16) != 0;
+      ge_p2 P2;
+      ge_p3_to_p2(P2, P);
+      const bool eq = ge_p2_eq_p3(P2, R);
+      const bool s_ok = !(pre & 1), a_ok = !(pre & 2), small_a = (pre & 4) != 0, tfree = !(pre & 8);
+      if (hdr) {
+        bits = (s_ok && a_ok && r_ok && !small_a && !small_r && eq) ? 0u : COA_CST_BAD_HEADER_SIG;
+      } else if (!(s_ok && a_ok && r_ok)) {
+        bits = COA_CST_BAD_VOTES;
+      } else {
+        bits = (eq && tfree) ? 0u : COA_CST_VOTES_INCONCLUSIVE;
+      }
+    }
+    if (lane == 0 && bits) atomicOr(a.status + c, bits);
+  }
+}
+
 // ---------------------------------------------------------------------------
 hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s) {
   if (nk == 0) return hipSuccess;
@@ -351,10 +554,11 @@ hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, hipStream_t s) 
   if (a.nc == 0) return hipSuccess;
   a.hdr_blocks = (a.nc + 255) / 256;
   const uint64_t jobs = (uint64_t)a.nc + a.nv;
-  const int L = lanes_per_sig == 64 ? 64 : 1;
-  const uint64_t sig_blocks = (jobs * L + 255) / 256;
-  const uint32_t grid = (uint32_t)(a.hdr_blocks + sig_blocks);
-  if (L == 64) hipLaunchKernelGGL(k_cert_verify<64>, dim3(grid), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(k_cert_verify<1>, dim3(grid), dim3(256), 0, s, a);
+  if (lanes_per_sig == 64) {  // one workgroup per header digest and per signature
+    hipLaunchKernelGGL(k_cert_verify_lat, dim3((uint32_t)(a.nc + jobs)), dim3(128), 0, s, a);
+    return hipGetLastError();
+  }
+  const uint64_t sig_blocks = (jobs + 255) / 256;
+  hipLaunchKernelGGL(k_cert_verify<1>, dim3((uint32_t)(a.hdr_blocks + sig_blocks)), dim3(256), 0, s, a);
   return hipGetLastError();
 }

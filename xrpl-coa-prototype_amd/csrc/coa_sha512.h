@@ -307,4 +307,103 @@ COA_DEV void hash_words(uint64_t st[8], const uint32_t* w) {
   compress(st, W);
 }
 
+// ------------------------------------------------------------------------
+// Latency path for ONE long message (a certificate's header digest): the
+// message schedule does not depend on the chaining state, so lanes expand
+// every block's W[0..79] + K[t] in parallel into LDS, and the hashing wave
+// runs only the rounds (one LDS broadcast read per round instead of ~17
+// schedule instructions).  A lone wave issues at most one instruction per
+// ~4 cycles whatever the unit (the scalar unit measured slower: 9.5 us per
+// block vs 8 us), so the instruction count of the serial stream is the
+// latency.
+COA_DEV uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Block `blk` of the padded message p[0 .. len) (FIPS 180-4 padding; nblk
+// blocks in total) as 16 big-endian words.
+COA_DEV void padded_block(uint64_t W[16], const uint8_t* p, uint64_t len, uint64_t blk, uint64_t nblk) {
+  const uint64_t base = blk * 128;
+  if (base + 128 <= len && (reinterpret_cast<uintptr_t>(p) & 3) == 0) {
+    const uint4* q = reinterpret_cast<const uint4*>(p + base);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint4 v = q[i];
+      W[2 * i] = be64(v.x, v.y);
+      W[2 * i + 1] = be64(v.z, v.w);
+    }
+  } else {
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+      uint32_t half[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; hh++) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint64_t q = base + 8 * w + 4 * hh + b;
+          uint32_t byte = 0;
+          if (q < len) byte = p[q];
+          else if (q == len) byte = 0x80;
+          x |= byte << (8 * b);
+        }
+        half[hh] = x;
+      }
+      W[w] = be64(half[0], half[1]);
+    }
+  }
+  if (blk == nblk - 1) {
+    W[14] = len >> 61;
+    W[15] = len << 3;
+  }
+}
+
+// kw[t] = K[t] + W[t], t = 0..79, for one block.
+COA_DEV void expand_kw(uint64_t* kw, uint64_t W[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) kw[i] = K512[i] + W[i];
+#pragma unroll 1
+  for (int r = 16; r < 80; r += 16) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
+      W[i] += xor3(rotr<1>(w15), rotr<8>(w15), shr<7>(w15)) + W[(i + 9) & 15] +
+              xor3(rotr<19>(w2), rotr<61>(w2), shr<6>(w2));
+      kw[r + i] = K512[r + i] + W[i];
+    }
+  }
+}
+
+// One block's 80 rounds from a precomputed kw (LDS, broadcast to the wave).
+COA_DEV void compress_kw(uint64_t st[8], const uint64_t* kw) {
+  uint64_t a = st[0], b = st[1], c = st[2], d = st[3];
+  uint64_t e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll 1
+  for (int r = 0; r < 80; r += 16) {
+    const uint64_t* k = kw + r;
+    round_(a, b, c, d, e, f, g, h, k[0]);
+    round_(h, a, b, c, d, e, f, g, k[1]);
+    round_(g, h, a, b, c, d, e, f, k[2]);
+    round_(f, g, h, a, b, c, d, e, k[3]);
+    round_(e, f, g, h, a, b, c, d, k[4]);
+    round_(d, e, f, g, h, a, b, c, k[5]);
+    round_(c, d, e, f, g, h, a, b, k[6]);
+    round_(b, c, d, e, f, g, h, a, k[7]);
+    round_(a, b, c, d, e, f, g, h, k[8]);
+    round_(h, a, b, c, d, e, f, g, k[9]);
+    round_(g, h, a, b, c, d, e, f, k[10]);
+    round_(f, g, h, a, b, c, d, e, k[11]);
+    round_(e, f, g, h, a, b, c, d, k[12]);
+    round_(d, e, f, g, h, a, b, c, k[13]);
+    round_(c, d, e, f, g, h, a, b, k[14]);
+    round_(b, c, d, e, f, g, h, a, k[15]);
+  }
+  st[0] += a;
+  st[1] += b;
+  st[2] += c;
+  st[3] += d;
+  st[4] += e;
+  st[5] += f;
+  st[6] += g;
+  st[7] += h;
+}
+
 }  // namespace coa_sha
