@@ -275,7 +275,7 @@ def main():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    coa_crypto.init(0)
+    coa_crypto.init_devices([local])  # this rank's GPU only
 
     n = args.n
     base, _ = sharding.rank_slice(rank, world, n)  # this rank's contiguous index range

@@ -44,6 +44,10 @@ extern "C" {
  * (0 = all visible), builds the fixed-base tables on each.  Idempotent; the
  * other calls initialise lazily with n_gpus = 0 when it was not called. */
 int coa_init(int n_gpus);
+/* Opens exactly the listed HIP devices (one process per GPU: each rank opens
+ * its own).  Idempotent like coa_init; host-pointer calls shard over the
+ * opened devices in list order. */
+int coa_init_devices(const int* device_ids, int n);
 int coa_shutdown(void);
 int coa_device_count(void);
 /* Human-readable description of the last error on this thread. */
@@ -220,8 +224,19 @@ int coa_queue_submit_verify(coa_queue* q, const uint8_t msg[32], const uint8_t p
                             coa_verdict_cb cb, void* user);
 int coa_queue_submit_batch(coa_queue* q, const uint8_t msg[32], const uint8_t* pks, const uint8_t* sigs, size_t n,
                            coa_verdict_cb cb, void* user);
+/* Whole certificates (the fused Certificate::verify crypto, f3): the
+ * callback receives one status byte of COA_CERT_* bits (0 = all Ok). */
+int coa_queue_submit_certificate(coa_queue* q, const uint8_t* header_data, size_t header_len, const uint8_t id[32],
+                                 const uint8_t origin[32], const uint8_t header_sig[64], uint64_t round,
+                                 const uint8_t* vote_pks, const uint8_t* vote_sigs, size_t n_votes, coa_verdict_cb cb,
+                                 void* user);
+/* Worker batch digests (worker/src/processor.rs:38, Processor::spawn): the
+ * callback receives the 32-byte Digest (n = 32). */
+int coa_queue_submit_digest(coa_queue* q, const uint8_t* data, size_t len, coa_verdict_cb cb, void* user);
 int coa_queue_flush(coa_queue* q);
+/* items = verify requests; groups = vote batches + certificates. */
 int coa_queue_stats(coa_queue* q, uint64_t* launches, uint64_t* items, uint64_t* groups);
+int coa_queue_digest_count(coa_queue* q, uint64_t* digests);
 int coa_queue_destroy(coa_queue* q);
 
 #ifdef __cplusplus

@@ -40,13 +40,16 @@ def test_queue_coalesces_and_reports_engine_errors_without_gpu():
         for t in th:
             t.join()
         futs.append(q.submit_batch(bytes(32), [(cc.PublicKey(), cc.Signature())] * 3))
+        futs.append(q.submit_certificate(b"hdr", bytes(32), bytes(32), bytes(64), 1,
+                                         [(cc.PublicKey(), cc.Signature())] * 2))
+        futs.append(q.submit_digest(b"batch"))
         q.flush()
         assert all(f.done() for f in futs)
         for f in futs:
             with pytest.raises(cc.EngineError):
                 f.result()
         st = q.stats()
-        assert st["signatures"] == 200 and st["batches"] == 1
+        assert st["signatures"] == 200 and st["batches"] == 2 and st["digests"] == 1
         assert st["launches"] < 20  # coalesced, not one launch per request
 
 
@@ -79,3 +82,37 @@ def test_queue_verdicts_gpu(engine):
         for f, exp in futs + gf:
             assert f.result(timeout=60) == exp
         assert q.stats()["launches"] < len(futs)
+
+
+@pytest.mark.gpu
+def test_queue_certificates_and_digests_gpu(engine):
+    """Whole certificates (fused Certificate::verify crypto) and worker batch
+    digests through the queue: one coalesced launch each, results equal the
+    per-call entry points and hashlib."""
+    import hashlib
+
+    import certificates as C
+    import workloads
+
+    committee, batch = C.synth_certificates(12, committee_size=10, n_payload=4, seed=21)
+    committee.register()
+    batch.vote_sigs[3 * 7 + 2, 40] ^= 1          # certificate 3: bad vote
+    batch.header_sigs[5, 33] ^= 1                 # certificate 5: bad header signature
+    want = C.verify_certificate_batch(batch, committee, rng_seed=1)
+    with engine.AggregationQueue(max_batch=100_000, max_delay_us=200_000) as q:
+        cf = []
+        for i in range(len(batch)):
+            lo, hi = int(batch.offsets[i]), int(batch.offsets[i + 1])
+            votes = [(engine.PublicKey(bytes(batch.vote_pks[j])), engine.Signature.from_bytes(bytes(batch.vote_sigs[j])))
+                     for j in range(lo, hi)]
+            cf.append(q.submit_certificate(batch.header_inputs[i], bytes(batch.ids[i]), bytes(batch.authors[i]),
+                                           bytes(batch.header_sigs[i]), batch.round, votes))
+        blobs = [workloads.worker_batch(b, ntx=20) for b in range(6)] + [b"", b"x" * 111, b"y" * 112]
+        df = [q.submit_digest(b) for b in blobs]
+        q.flush()
+        got = [f.result(timeout=60) for f in cf]
+        assert [int(g != 0) for g in got] == list(want)
+        assert got[3] == engine.CERT_BAD_VOTES and got[5] == engine.CERT_BAD_HEADER_SIG
+        assert [bytes(f.result(timeout=60)) for f in df] == [hashlib.sha512(b).digest()[:32] for b in blobs]
+        st = q.stats()
+        assert st["batches"] == len(batch) and st["digests"] == len(blobs) and st["launches"] <= 2

@@ -63,6 +63,7 @@ def lib():
     sz, vp = ctypes.c_size_t, ctypes.c_void_p
     sig = {
         "coa_init": ([ctypes.c_int], ctypes.c_int),
+        "coa_init_devices": ([ctypes.POINTER(ctypes.c_int), ctypes.c_int], ctypes.c_int),
         "coa_shutdown": ([], ctypes.c_int),
         "coa_device_count": ([], ctypes.c_int),
         "coa_last_error": ([], ctypes.c_char_p),
@@ -92,6 +93,10 @@ def lib():
         "coa_queue_create": ([sz, ctypes.c_uint32], vp),
         "coa_queue_submit_verify": ([vp, P8, P8, P8, VERDICT_CB, vp], ctypes.c_int),
         "coa_queue_submit_batch": ([vp, P8, P8, P8, sz, VERDICT_CB, vp], ctypes.c_int),
+        "coa_queue_submit_certificate": ([vp, P8, sz, P8, P8, P8, ctypes.c_uint64, P8, P8, sz, VERDICT_CB, vp],
+                                         ctypes.c_int),
+        "coa_queue_submit_digest": ([vp, P8, sz, VERDICT_CB, vp], ctypes.c_int),
+        "coa_queue_digest_count": ([vp, P64], ctypes.c_int),
         "coa_queue_flush": ([vp], ctypes.c_int),
         "coa_queue_stats": ([vp, P64, P64, P64], ctypes.c_int),
         "coa_queue_destroy": ([vp], ctypes.c_int),
@@ -243,6 +248,12 @@ class Signature:
 # ----------------------------------------------------------- engine level
 def init(n_gpus=0):
     return _check(lib().coa_init(n_gpus))
+
+
+def init_devices(ids):
+    """Open exactly these HIP devices (bench.py: each rank its own GPU)."""
+    arr = (ctypes.c_int * len(ids))(*ids)
+    return _check(lib().coa_init_devices(arr, len(ids)))
 
 
 def device_count():
@@ -462,9 +473,11 @@ def certificate_verify_many_device(device, hdata, hoff, ids, origins, hsigs, rou
 # --------------------------------------------------------- aggregation queue
 class AggregationQueue:
     """Python face of the native coalescing stage (coa_queue_*): submit
-    header/vote signatures and certificate vote batches from any thread, get
-    a concurrent.futures.Future per request resolving to True (Ok) / False
-    (Err); the engine error status raises EngineError in the future."""
+    header/vote signatures, certificate vote batches, whole certificates and
+    worker batch digests from any thread, get a concurrent.futures.Future per
+    request -- True (Ok) / False (Err) for signatures and vote batches, the
+    CERT_BAD_* bits for certificates, the 32-byte Digest for digests; the
+    engine error status raises EngineError in the future."""
 
     def __init__(self, max_batch=65536, max_delay_us=500):
         import concurrent.futures as cf
@@ -479,19 +492,53 @@ class AggregationQueue:
 
     def _on_verdict(self, user, status, verdicts, n):
         with self._lock:
-            fut = self._pending.pop(user)
+            fut, kind = self._pending.pop(user)
         if status < 0:
             fut.set_exception(EngineError(f"{_ERRORS.get(status, status)}"))
+        elif kind == "digest":
+            fut.set_result(Digest(bytes(verdicts[:32])))
+        elif kind == "certificate":
+            fut.set_result(int(verdicts[0]))
         else:
             fut.set_result(verdicts[0] == 0)
 
-    def _register(self):
+    def _register(self, kind="verdict"):
         fut = self._cf.Future()
         with self._lock:
             key = self._next
             self._next += 1
-            self._pending[key] = fut
+            self._pending[key] = (fut, kind)
         return key, fut
+
+    def _submitted(self, key, rc):
+        if rc < 0:
+            with self._lock:
+                self._pending.pop(key, None)
+            _check(rc)
+
+    def submit_certificate(self, header_input, id_, origin, header_sig, round_, votes):
+        """Future of the certificate's CERT_BAD_* bits (0 = all crypto Ok)."""
+        key, fut = self._register("certificate")
+        votes = list(votes)
+        h = np.frombuffer(bytes(header_input), np.uint8).copy() if len(header_input) else np.zeros(1, np.uint8)
+        i = np.frombuffer(bytes(id_), np.uint8).copy()
+        o = np.frombuffer(bytes(origin), np.uint8).copy()
+        sg = np.frombuffer(header_sig.flatten() if isinstance(header_sig, Signature) else bytes(header_sig),
+                           np.uint8).copy()
+        pks = _bytes_array([bytes(pk) for pk, _ in votes], 32) if votes else np.zeros(32, np.uint8)
+        sgs = _bytes_array([s.flatten() for _, s in votes], 64) if votes else np.zeros(64, np.uint8)
+        rc = lib().coa_queue_submit_certificate(self._q, _u8p(h), len(header_input), _u8p(i), _u8p(o), _u8p(sg),
+                                                round_, _u8p(pks), _u8p(sgs), len(votes), self._cb, key)
+        self._submitted(key, rc)
+        return fut
+
+    def submit_digest(self, data):
+        """Future of Digest(Sha512(data)[..32]) (worker/src/processor.rs:38)."""
+        key, fut = self._register("digest")
+        buf = np.frombuffer(bytes(data), np.uint8).copy() if len(data) else np.zeros(1, np.uint8)
+        rc = lib().coa_queue_submit_digest(self._q, _u8p(buf), len(data), self._cb, key)
+        self._submitted(key, rc)
+        return fut
 
     def submit_verify(self, digest, public_key, signature):
         key, fut = self._register()
@@ -523,9 +570,10 @@ class AggregationQueue:
         _check(lib().coa_queue_flush(self._q))
 
     def stats(self):
-        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        a, b, c, d = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         _check(lib().coa_queue_stats(self._q, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
-        return {"launches": a.value, "signatures": b.value, "batches": c.value}
+        _check(lib().coa_queue_digest_count(self._q, ctypes.byref(d)))
+        return {"launches": a.value, "signatures": b.value, "batches": c.value, "digests": d.value}
 
     def close(self):
         if self._q:

@@ -123,28 +123,49 @@ std::mutex g_init_mu;
 std::vector<std::unique_ptr<Dev>> g_devs;
 bool g_inited = false;
 
-int init_locked(int n_gpus) {
+int open_device(int d) {
+  auto dev = std::make_unique<Dev>();
+  dev->id = d;
+  HIP_TRY(hipSetDevice(d));
+  HIP_TRY(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
+  HIP_TRY(hipMalloc(&dev->btab, COA_BTAB_DWORDS * sizeof(uint32_t)));
+  HIP_TRY(coa_launch_build_btable(dev->btab, dev->stream));
+  HIP_TRY(hipMalloc(&dev->comb, COA_COMB_DWORDS * sizeof(uint32_t)));
+  HIP_TRY(coa_launch_build_comb(dev->comb, dev->btab, dev->stream));
+  HIP_TRY(hipStreamSynchronize(dev->stream));
+  g_devs.push_back(std::move(dev));
+  return COA_OK;
+}
+
+// Opens the listed devices (ids == nullptr: the first n, n <= 0: all).
+int init_locked(const int* ids, int n) {
   if (g_inited) return COA_OK;
   int count = 0;
   hipError_t e = hipGetDeviceCount(&count);
   if (e != hipSuccess || count <= 0)
     return fail(COA_ENODEVICE, "no HIP device available (this engine has no CPU fallback)");
-  if (n_gpus <= 0 || n_gpus > count) n_gpus = count;
-  for (int d = 0; d < n_gpus; d++) {
-    auto dev = std::make_unique<Dev>();
-    dev->id = d;
-    HIP_TRY(hipSetDevice(d));
-    HIP_TRY(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
-    HIP_TRY(hipMalloc(&dev->btab, COA_BTAB_DWORDS * sizeof(uint32_t)));
-    HIP_TRY(coa_launch_build_btable(dev->btab, dev->stream));
-    HIP_TRY(hipMalloc(&dev->comb, COA_COMB_DWORDS * sizeof(uint32_t)));
-    HIP_TRY(coa_launch_build_comb(dev->comb, dev->btab, dev->stream));
-    HIP_TRY(hipStreamSynchronize(dev->stream));
-    g_devs.push_back(std::move(dev));
+  std::vector<int> want;
+  if (ids) {
+    for (int i = 0; i < n; i++) {
+      if (ids[i] < 0 || ids[i] >= count) return fail(COA_EINVAL, "device id out of range");
+      if (std::find(want.begin(), want.end(), ids[i]) == want.end()) want.push_back(ids[i]);
+    }
+    if (want.empty()) return fail(COA_EINVAL, "empty device list");
+  } else {
+    if (n <= 0 || n > count) n = count;
+    for (int d = 0; d < n; d++) want.push_back(d);
+  }
+  for (int d : want) {
+    const int rc = open_device(d);
+    if (rc != COA_OK) {
+      g_devs.clear();
+      return rc;
+    }
   }
   g_inited = true;
   return COA_OK;
 }
+int init_locked(int n_gpus) { return init_locked(nullptr, n_gpus); }
 
 int ensure_init() {
   std::lock_guard<std::mutex> g(g_init_mu);
@@ -540,6 +561,12 @@ const char* coa_version(void) { return "coa_verify 0.1.0 gfx950"; }
 int coa_init(int n_gpus) {
   std::lock_guard<std::mutex> g(g_init_mu);
   return init_locked(n_gpus);
+}
+
+int coa_init_devices(const int* device_ids, int n) {
+  if (!device_ids || n <= 0) return fail(COA_EINVAL, "empty device list");
+  std::lock_guard<std::mutex> g(g_init_mu);
+  return init_locked(device_ids, n);
 }
 
 int coa_shutdown(void) {
