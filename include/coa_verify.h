@@ -196,6 +196,44 @@ int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data,
                                        const uint8_t* d_vote_sigs, const uint64_t* d_vote_offsets, size_t n,
                                        size_t n_votes, uint32_t* d_status, void* stream);
 
+/* ------------------------------------------------------- wire decode (f4)
+ * bincode 1.3 decode of PrimaryMessage frames, as
+ * PrimaryReceiverHandler::dispatch does (primary/src/primary.rs:223-244),
+ * straight into the arrays of the batched entry points above.  Host-only
+ * parsing (no device work).  frames[frame_offsets[i] .. frame_offsets[i+1])
+ * is frame i.
+ *   coa_wire_scan: kind_out[i] = COA_MSG_* or a negative COA_WIRE_E* (the
+ *     reference drops such frames); header_bytes_out[i] = length of the
+ *     Header::digest input (Header and Certificate frames), votes_out[i] =
+ *     number of votes (Certificate frames); both optional.
+ *   coa_wire_decode_certificates: every frame must be a Certificate; fills
+ *     the coa_certificate_verify_many arguments (header_data sized by the
+ *     scan's header bytes, vote arrays by its vote counts); payload_counts
+ *     (optional) = entries of header.payload, whose worker ids sit at
+ *     header_data + 40 + 36 k + 32 (the MalformedHeader check).
+ *   coa_wire_decode_votes / _headers: Vote / Header frames (Vote::digest
+ *     input = id || round LE || origin; Header::digest input as above).
+ * Header::digest input = author | round LE | (digest | worker id LE)* in key
+ * order | parents* in order (primary/src/messages.rs:70-84). */
+#define COA_MSG_HEADER 0
+#define COA_MSG_VOTE 1
+#define COA_MSG_CERTIFICATE 2
+#define COA_MSG_CERT_REQUEST 3
+#define COA_WIRE_ETRUNC (-10)  /* frame ends inside a field / length prefix too large */
+#define COA_WIRE_EFORMAT (-11) /* unknown variant or non-UTF-8 string */
+#define COA_WIRE_EKEY (-12)    /* PublicKey string is not base64 of >= 32 bytes */
+int coa_wire_scan(const uint8_t* frames, const uint64_t* frame_offsets, size_t n, int32_t* kind_out,
+                  uint64_t* header_bytes_out, uint64_t* votes_out);
+int coa_wire_decode_certificates(const uint8_t* frames, const uint64_t* frame_offsets, size_t n, uint8_t* header_data,
+                                 uint64_t* header_offsets, uint8_t* ids, uint8_t* origins, uint8_t* header_sigs,
+                                 uint64_t* rounds, uint8_t* vote_pks, uint8_t* vote_sigs, uint64_t* vote_offsets,
+                                 uint32_t* payload_counts);
+int coa_wire_decode_votes(const uint8_t* frames, const uint64_t* frame_offsets, size_t n, uint8_t* ids,
+                          uint64_t* rounds, uint8_t* origins, uint8_t* authors, uint8_t* sigs);
+int coa_wire_decode_headers(const uint8_t* frames, const uint64_t* frame_offsets, size_t n, uint8_t* header_data,
+                            uint64_t* header_offsets, uint8_t* ids, uint8_t* authors, uint8_t* sigs,
+                            uint64_t* rounds, uint32_t* payload_counts);
+
 /* --------------------------------------------------------------- signing
  * RFC 8032 signing == crypto::Signature::new (crypto/src/lib.rs:185-191) /
  * generate_keypair (:167-175) from 32-byte seeds.  Not on the verification

@@ -90,6 +90,12 @@ def lib():
         "coa_certificate_verify": ([P8, sz, P8, P8, P8, ctypes.c_uint64, P8, P8, sz, ctypes.c_uint64], ctypes.c_int),
         "coa_certificate_verify_many_device": ([ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, sz, vp, vp],
                                                ctypes.c_int),
+        "coa_wire_scan": ([P8, P64, sz, ctypes.POINTER(ctypes.c_int32), P64, P64], ctypes.c_int),
+        "coa_wire_decode_certificates": ([P8, P64, sz, P8, P64, P8, P8, P8, P64, P8, P8, P64,
+                                          ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+        "coa_wire_decode_votes": ([P8, P64, sz, P8, P64, P8, P8, P8], ctypes.c_int),
+        "coa_wire_decode_headers": ([P8, P64, sz, P8, P64, P8, P8, P8, P64, ctypes.POINTER(ctypes.c_uint32)],
+                                    ctypes.c_int),
         "coa_queue_create": ([sz, ctypes.c_uint32], vp),
         "coa_queue_submit_verify": ([vp, P8, P8, P8, VERDICT_CB, vp], ctypes.c_int),
         "coa_queue_submit_batch": ([vp, P8, P8, P8, sz, VERDICT_CB, vp], ctypes.c_int),
@@ -468,6 +474,81 @@ def certificate_verify_many_device(device, hdata, hoff, ids, origins, hsigs, rou
                                                     origins.data_ptr(), hsigs.data_ptr(), rounds.data_ptr(),
                                                     vpks.data_ptr(), vsigs.data_ptr(), voff.data_ptr(), n, nv,
                                                     status.data_ptr(), _handle(device, stream)))
+
+
+# ------------------------------------------------------------- wire (f4)
+MSG_HEADER, MSG_VOTE, MSG_CERTIFICATE, MSG_CERT_REQUEST = 0, 1, 2, 3
+WIRE_ETRUNC, WIRE_EFORMAT, WIRE_EKEY = -10, -11, -12
+
+
+def _frames(frames):
+    data = np.frombuffer(b"".join(bytes(f) for f in frames), np.uint8) if frames else np.zeros(0, np.uint8)
+    offs = np.zeros(len(frames) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(f) for f in frames])
+    return (data if data.size else np.zeros(1, np.uint8)), offs
+
+
+def wire_scan(frames):
+    """bincode PrimaryMessage frames -> (kinds int32 [n], header digest input
+    bytes [n], vote counts [n]); kinds are MSG_* or negative WIRE_E*."""
+    n = len(frames)
+    data, offs = _frames(frames)
+    kinds = np.zeros(max(n, 1), np.int32)
+    hb = np.zeros(max(n, 1), np.uint64)
+    nv = np.zeros(max(n, 1), np.uint64)
+    _check(lib().coa_wire_scan(_u8p(data), _u64p(offs), n, kinds.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                               _u64p(hb), _u64p(nv)))
+    return kinds[:n], hb[:n], nv[:n]
+
+
+def wire_decode_certificates(frames):
+    """Certificate frames -> the arguments of certificate_verify_many:
+    dict(header_inputs, ids, origins, header_sigs, rounds, vote_pks, vote_sigs, vote_offsets)."""
+    n = len(frames)
+    kinds, hb, nv = wire_scan(frames)
+    if n and (kinds != MSG_CERTIFICATE).any():
+        raise ValueError("not all frames are well-formed Certificate messages")
+    data, offs = _frames(frames)
+    hd = np.zeros(max(int(hb.sum()), 1), np.uint8)
+    hoff = np.zeros(n + 1, np.uint64)
+    ids, origins = np.zeros((n, 32), np.uint8), np.zeros((n, 32), np.uint8)
+    hsigs, rounds = np.zeros((n, 64), np.uint8), np.zeros(n, np.uint64)
+    tv = int(nv.sum())
+    vp, vs = np.zeros((max(tv, 1), 32), np.uint8), np.zeros((max(tv, 1), 64), np.uint8)
+    voff = np.zeros(n + 1, np.uint64)
+    pc = np.zeros(max(n, 1), np.uint32)
+    _check(lib().coa_wire_decode_certificates(_u8p(data), _u64p(offs), n, _u8p(hd), _u64p(hoff), _u8p(ids),
+                                              _u8p(origins), _u8p(hsigs), _u64p(rounds), _u8p(vp), _u8p(vs),
+                                              _u64p(voff), pc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
+    hdr = [bytes(hd[int(hoff[i]):int(hoff[i + 1])]) for i in range(n)]
+    return {"header_inputs": hdr, "ids": ids, "origins": origins, "header_sigs": hsigs, "rounds": rounds,
+            "vote_pks": vp[:tv], "vote_sigs": vs[:tv], "vote_offsets": voff, "payload_counts": pc[:n]}
+
+
+def wire_decode_votes(frames):
+    n = len(frames)
+    data, offs = _frames(frames)
+    ids, origins, authors = (np.zeros((n, 32), np.uint8) for _ in range(3))
+    rounds, sigs = np.zeros(n, np.uint64), np.zeros((n, 64), np.uint8)
+    _check(lib().coa_wire_decode_votes(_u8p(data), _u64p(offs), n, _u8p(ids), _u64p(rounds), _u8p(origins),
+                                       _u8p(authors), _u8p(sigs)))
+    return {"ids": ids, "rounds": rounds, "origins": origins, "authors": authors, "sigs": sigs}
+
+
+def wire_decode_headers(frames):
+    n = len(frames)
+    _, hb, _ = wire_scan(frames)
+    data, offs = _frames(frames)
+    hd = np.zeros(max(int(hb.sum()), 1), np.uint8)
+    hoff = np.zeros(n + 1, np.uint64)
+    ids, authors = np.zeros((n, 32), np.uint8), np.zeros((n, 32), np.uint8)
+    sigs, rounds = np.zeros((n, 64), np.uint8), np.zeros(n, np.uint64)
+    pc = np.zeros(max(n, 1), np.uint32)
+    _check(lib().coa_wire_decode_headers(_u8p(data), _u64p(offs), n, _u8p(hd), _u64p(hoff), _u8p(ids),
+                                         _u8p(authors), _u8p(sigs), _u64p(rounds),
+                                         pc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
+    return {"header_inputs": [bytes(hd[int(hoff[i]):int(hoff[i + 1])]) for i in range(n)], "ids": ids,
+            "authors": authors, "sigs": sigs, "rounds": rounds, "payload_counts": pc[:n]}
 
 
 # --------------------------------------------------------- aggregation queue
