@@ -353,7 +353,7 @@ __global__ void __launch_bounds__(256) k_key_tables(const uint32_t* __restrict__
 }
 
 template <int L>
-__global__ void __launch_bounds__(256) k_cert_verify(CertArgs a) {
+__global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a) {
   if (blockIdx.x < a.hdr_blocks) {  // header digest role, one lane per certificate
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.nc) return;
