@@ -12,14 +12,18 @@ verifies its own 65,536 triples (weak scaling, contiguous index ranges, no
 data-path collective); value = all ranks' verifications / max-over-ranks time.
 
 Also reported:
-  roofline      the dominant kernel (k_verify_strict) against the INT32 VALU
-                issue peak; algorithmic work = the dalek algorithm's field
-                operation count (2,967 mul+sq per verify, frozen by the
-                instrumented C restatement: oracle/coa_oracle.c) x 200 INT32
-                ops per field op (SURVEY.md 8(d) cost model); its time is
-                measured here with HIP events on the stream it runs on.
+  roofline      the dominant kernel pair (k_halve + k_verify_halved) against
+                the INT32 VALU issue peak; algorithmic work = the dalek
+                algorithm's field operation count (2,967 mul+sq per verify,
+                frozen by the instrumented C restatement: oracle/coa_oracle.c)
+                x 200 INT32 ops per field op (SURVEY.md 8(d) cost model); its
+                time is measured here with HIP events on the stream it runs on.
   cpu_baseline  the C restatement of dalek's algorithms (oracle/, "port")
                 on this host's cores, rank 0 at N=1 only, on a bounded sample.
+  secondary     (rank 0, N=1) C4 worker-batch SHA-512 GB/s; C3 and C1
+                Certificate::verify -- certificates/s for a round resident in
+                HBM and p50/p99 latency of one certificate through the
+                host-pointer C ABI, beside the single-core CPU restatement.
 """
 import argparse
 import json
@@ -160,9 +164,11 @@ def c4_sha512(local, dev, stream, counts, steps, cpu_threads):
     return out
 
 
-def c3_certificates(n_certs, latency_samples, cpu_threads, dev, stream):
-    """C3: committee of 100, 67 votes per certificate, Certificate::verify
-    through the fused path (committee key cache f2 + one-launch crypto f3):
+def certificate_config(n_certs, latency_samples, cpu_threads, dev, stream, committee_size=100, n_payload=32):
+    """C3 (committee of 100, 67 votes per certificate, 32 payload digests and
+    67 parents per header) or C1 (committee of 4, 3 votes, 1 payload digest,
+    3 parents): Certificate::verify through the fused path (committee key
+    cache f2 + one-launch crypto f3):
       certs_per_s       a round of n_certs certificates resident in HBM,
                         coa_certificate_verify_many_device, HIP events
       host_certs_per_s  the same round through the host-pointer C ABI
@@ -178,12 +184,12 @@ def c3_certificates(n_certs, latency_samples, cpu_threads, dev, stream):
     import certificates as C
     import coa_crypto
 
-    committee, batch = C.synth_certificates(n_certs, committee_size=100, n_payload=32, seed=3)
+    committee, batch = C.synth_certificates(n_certs, committee_size=committee_size, n_payload=n_payload, seed=3)
     t0 = time.perf_counter()
     committee.register()
     reg_ms = (time.perf_counter() - t0) * 1e3
     v = C.verify_certificate_batch(batch, committee)  # warm-up + correctness (host path)
-    assert int(v.sum()) == 0, "C3 certificates rejected"
+    assert int(v.sum()) == 0, "certificates rejected"
     rounds = np.full(n_certs, batch.round, np.uint64)
     t0 = time.perf_counter()
     st = coa_crypto.certificate_verify_many(batch.header_inputs, batch.ids, batch.authors, batch.header_sigs, rounds,
@@ -191,7 +197,7 @@ def c3_certificates(n_certs, latency_samples, cpu_threads, dev, stream):
     host_el = time.perf_counter() - t0
     assert int(st.sum()) == 0
     # device-resident round
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).to(dev)  # noqa: E731
     hoff = np.zeros(n_certs + 1, np.uint64)
     hoff[1:] = np.cumsum([len(h) for h in batch.header_inputs])
     d = [T(np.frombuffer(b"".join(batch.header_inputs), np.uint8)), T(hoff.view(np.int64)), T(batch.ids),
@@ -200,7 +206,7 @@ def c3_certificates(n_certs, latency_samples, cpu_threads, dev, stream):
     status = torch.ones(n_certs, dtype=torch.int32, device=dev)
     coa_crypto.certificate_verify_many_device(0 if dev.index is None else dev.index, *d, status, stream)
     torch.cuda.synchronize()
-    assert int(status.abs().sum().item()) == 0, "fused device path rejected C3 certificates"
+    assert int(status.abs().sum().item()) == 0, "fused device path rejected certificates"
     reps = 5
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -223,7 +229,10 @@ def c3_certificates(n_certs, latency_samples, cpu_threads, dev, stream):
         assert r == 0
     lat = np.array(lat[20:]) * 1e3
     nv = int(batch.offsets[-1])
-    res = {"workload": "C3: committee 100, 67 votes/certificate, header 32 payload + 67 parents (3,336 B)",
+    q = committee.quorum_threshold()
+    name = "C3" if committee_size == 100 else "C1" if committee_size == 4 else f"committee {committee_size}"
+    res = {"workload": f"{name}: committee {committee_size}, {q} votes/certificate, header {n_payload} payload + "
+                       f"{q} parents ({len(batch.header_inputs[0]):,} B)",
            "path": "fused: committee key cache + coa_certificate_verify[_many] (one launch)",
            "certificates": n_certs, "votes": nv, "register_ms": round(reg_ms, 2),
            "certs_per_s": round(n_certs / (dev_ms * 1e-3), 1), "round_ms": round(dev_ms, 3),
@@ -269,12 +278,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    # bind this rank to its GPU before RCCL sees it (one process per GPU)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=dev)
     coa_crypto.init_devices([local])  # this rank's GPU only
 
     n = args.n
@@ -355,7 +365,9 @@ def main():
         secondary = {
             "c4_sha512": c4_sha512(local, dev, stream, [int(x) for x in args.c4_batches.split(",") if x], 2,
                                    threads),
-            "c3_certificate_verify": c3_certificates(args.c3_certs, 1000, threads, dev, stream),
+            "c3_certificate_verify": certificate_config(args.c3_certs, 1000, threads, dev, stream),
+            "c1_certificate_verify": certificate_config(2000, 1000, threads, dev, stream, committee_size=4,
+                                                        n_payload=1),
         }
 
     if rank == 0:
