@@ -219,18 +219,20 @@ COA_DEV bool ge_p2_is_identity(const ge_p2& p) {
   return fe_iszero(p.X) && fe_eq(p.Y, p.Z);
 }
 
-// EdwardsPoint::is_small_order: [8]P == identity.
+// EdwardsPoint::is_small_order ([8]P == identity), as a coordinate test.
+// The eight points of E[8] are exactly those with X = 0 (orders 1 and 2),
+// Y = 0 (order 4: x^2 = -1) or X^2 + Y^2 = 0 (order 8: y^2 = -x^2 on
+// -x^2 + y^2 = 1 + d x^2 y^2 gives d x^4 - 2 x^2 - 1 = 0, whose four points
+// are the order-8 ones).  Homogeneous, so valid for any Z != 0.  Two
+// squarings instead of three doublings (~21 field operations); checked
+// against [8]P == O on every torsion point and on random and mixed-order
+// points with the oracle, and by the small-order golden classes.
 COA_DEV bool ge_is_small_order(const ge_p3& p) {
-  ge_p1p1 t;
-  ge_p2 q;
-  ge_p3_to_p2(q, p);
-  ge_p2_dbl(t, q);
-  ge_p1p1_to_p2(q, t);
-  ge_p2_dbl(t, q);
-  ge_p1p1_to_p2(q, t);
-  ge_p2_dbl(t, q);
-  ge_p1p1_to_p2(q, t);
-  return ge_p2_is_identity(q);
+  fe xx, yy, s;
+  fe_sq(xx, p.X);
+  fe_sq(yy, p.Y);
+  fe_add(s, xx, yy);
+  return fe_iszero(p.X) || fe_iszero(p.Y) || fe_iszero(s);
 }
 
 // EdwardsPoint::ct_eq between a projective P and an extended Q.

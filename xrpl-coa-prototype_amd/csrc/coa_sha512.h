@@ -39,7 +39,18 @@ __device__ __constant__ static const uint64_t K512[80] = {
 // That takes a round from ~75 to ~40 VALU instructions.
 COA_DEV uint32_t lo32(uint64_t x) { return (uint32_t)x; }
 COA_DEV uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
-COA_DEV uint64_t mk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+// A register pair from two halves.  Built as a <2 x i32> bitcast, not as
+// (hi << 32) | lo: LLVM splits an add of the shift/or form into a
+// zero-extended low add, a separate high add and v_mov's of zero halves
+// (~10 extra instructions per round); the bitcast keeps every 64-bit add a
+// single v_lshl_add_u64 on a pair.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+COA_DEV uint64_t mk64(uint32_t lo, uint32_t hi) {
+  u32x2 v;
+  v.x = lo;
+  v.y = hi;
+  return __builtin_bit_cast(uint64_t, v);
+}
 
 template <int N>
 COA_DEV uint64_t rotr(uint64_t x) {
