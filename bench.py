@@ -204,18 +204,20 @@ def certificate_config(n_certs, latency_samples, cpu_threads, dev, stream, commi
          T(batch.authors), T(batch.header_sigs), T(rounds.view(np.int64)), T(batch.vote_pks), T(batch.vote_sigs),
          T(batch.offsets.view(np.int64))]
     status = torch.ones(n_certs, dtype=torch.int32, device=dev)
-    coa_crypto.certificate_verify_many_device(0 if dev.index is None else dev.index, *d, status, stream)
+    cws = torch.empty(coa_crypto.certificate_workspace_bytes(n_certs, int(batch.offsets[-1])), dtype=torch.uint8,
+                      device=dev)
+    coa_crypto.certificate_verify_many_device(0 if dev.index is None else dev.index, *d, status, stream, cws)
     torch.cuda.synchronize()
     assert int(status.abs().sum().item()) == 0, "fused device path rejected certificates"
     reps = 5
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(reps):
-        coa_crypto.certificate_verify_many_device(0 if dev.index is None else dev.index, *d, status, stream)
+        coa_crypto.certificate_verify_many_device(0 if dev.index is None else dev.index, *d, status, stream, cws)
     e1.record(stream)
     torch.cuda.synchronize()
     dev_ms = e0.elapsed_time(e1) / reps
-    del d, status
+    del d, status, cws
     # latency: one certificate per call
     lat = []
     for i in range(latency_samples + 20):

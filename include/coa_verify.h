@@ -189,12 +189,15 @@ int coa_certificate_verify(const uint8_t* header_data, size_t header_len, const 
 /* Device-resident form (asynchronous on `stream`): d_status[c] receives the
  * raw status word -- COA_CERT_* bits plus 8 = votes need the exact RLC check
  * (coa_ed25519_verify_batch_groups) and 16 = a key is not registered (use the
- * uncached entry points).  The host-pointer calls above resolve both. */
+ * uncached entry points).  The host-pointer calls above resolve both.
+ * `workspace`: NULL (engine-owned; the call then waits for its stream) or
+ * coa_certificate_workspace_bytes(n, n_votes) bytes of device memory. */
+size_t coa_certificate_workspace_bytes(size_t n, size_t n_votes);
 int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data, const uint64_t* d_header_offsets,
                                        const uint8_t* d_ids, const uint8_t* d_origins, const uint8_t* d_header_sigs,
                                        const uint64_t* d_rounds, const uint8_t* d_vote_pks,
                                        const uint8_t* d_vote_sigs, const uint64_t* d_vote_offsets, size_t n,
-                                       size_t n_votes, uint32_t* d_status, void* stream);
+                                       size_t n_votes, uint32_t* d_status, void* workspace, void* stream);
 
 /* ------------------------------------------------------- wire decode (f4)
  * bincode 1.3 decode of PrimaryMessage frames, as

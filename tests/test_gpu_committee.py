@@ -299,11 +299,18 @@ def world(engine):
     return World(engine)
 
 
-@pytest.fixture(params=["64", "1"])
+@pytest.fixture(params=["64", "1/T0", "1/T256", "1/T512"])
 def lanes(request):
-    os.environ["COA_CERT_LANES"] = request.param
-    yield int(request.param)
+    """Latency kernel (64) and throughput kernel with one signature per lane
+    (T0 = default grid) or a grid of 256 / 512 lanes, so each lane shares one
+    inversion among several signatures (P compared with R's encoding)."""
+    lanes_, _, t = request.param.partition("/T")
+    os.environ["COA_CERT_LANES"] = lanes_
+    if t and t != "0":
+        os.environ["COA_CERT_LANES_TOTAL"] = t
+    yield int(lanes_)
     del os.environ["COA_CERT_LANES"]
+    os.environ.pop("COA_CERT_LANES_TOTAL", None)
 
 
 def test_fused_certificates_adversarial(engine, world, lanes):
@@ -351,7 +358,7 @@ def test_fused_weight_dependent_classes(engine, world, lanes):
     assert seen == {True, False}  # both verdicts occur
 
 
-def test_c3_fused_matches_stepwise(engine):
+def test_c3_fused_matches_stepwise(engine, lanes):
     import certificates as C
 
     committee, batch = C.synth_certificates(24, committee_size=100, n_payload=32, seed=11)

@@ -88,7 +88,8 @@ def lib():
         "coa_certificate_verify_many": ([P8, P64, P8, P8, P8, P64, P8, P8, P64, sz, ctypes.c_uint64, P8],
                                         ctypes.c_int),
         "coa_certificate_verify": ([P8, sz, P8, P8, P8, ctypes.c_uint64, P8, P8, sz, ctypes.c_uint64], ctypes.c_int),
-        "coa_certificate_verify_many_device": ([ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, sz, vp, vp],
+        "coa_certificate_workspace_bytes": ([sz, sz], sz),
+        "coa_certificate_verify_many_device": ([ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, sz, vp, vp, vp],
                                                ctypes.c_int),
         "coa_wire_scan": ([P8, P64, sz, ctypes.POINTER(ctypes.c_int32), P64, P64], ctypes.c_int),
         "coa_wire_decode_certificates": ([P8, P64, sz, P8, P64, P8, P8, P8, P64, P8, P8, P64,
@@ -464,16 +465,22 @@ def certificate_verify(header_input, id_, origin, header_sig, round_, vote_pks, 
                                                _u8p(vs), nv, rng_seed))
 
 
+def certificate_workspace_bytes(n, n_votes):
+    return lib().coa_certificate_workspace_bytes(n, n_votes)
+
+
 def certificate_verify_many_device(device, hdata, hoff, ids, origins, hsigs, rounds, vpks, vsigs, voff, status,
-                                   stream=None):
+                                   stream=None, workspace=None):
     """Device-resident certificates (torch tensors); raw status words (uint32
-    tensor [n]) enqueued on `stream`."""
+    tensor [n]) enqueued on `stream`.  workspace: None (engine-owned; the call
+    waits for the stream) or a device tensor of certificate_workspace_bytes."""
     n = ids.shape[0]
     nv = vpks.shape[0]
+    ws = workspace.data_ptr() if workspace is not None else None
     _check(lib().coa_certificate_verify_many_device(device, hdata.data_ptr(), hoff.data_ptr(), ids.data_ptr(),
                                                     origins.data_ptr(), hsigs.data_ptr(), rounds.data_ptr(),
                                                     vpks.data_ptr(), vsigs.data_ptr(), voff.data_ptr(), n, nv,
-                                                    status.data_ptr(), _handle(device, stream)))
+                                                    status.data_ptr(), ws, _handle(device, stream)))
 
 
 # ------------------------------------------------------------- wire (f4)

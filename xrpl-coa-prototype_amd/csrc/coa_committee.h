@@ -43,7 +43,10 @@ struct CertArgs {
 
 hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s);
 hipError_t coa_launch_key_tables(const uint32_t* keys, uint32_t nk, uint32_t* tabs, hipStream_t s);
-// lanes_per_sig: 64 (latency: one wave per signature, comb terms split over
-// the lanes and summed by a butterfly) or 1 (throughput: one lane per
-// signature).
-hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, hipStream_t s);
+// lanes_per_sig: 64 (latency: two waves per signature, comb terms split over
+// a wave's lanes and summed by a butterfly) or 1 (throughput: K signatures
+// per lane, K from the job count).
+// pscr: device scratch of coa_cert_scratch_bytes(nc + nv) bytes (throughput
+// variant only; may be null for lanes_per_sig == 64).
+size_t coa_cert_scratch_bytes(uint64_t jobs);
+hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr, hipStream_t s);

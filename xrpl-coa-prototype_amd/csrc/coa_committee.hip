@@ -36,8 +36,10 @@
 // definitive Err, as in dalek.
 //
 // Two variants:
-//   k_cert_verify<1>   throughput: one lane per signature (64 serial mixed
-//                      additions), one lane per header digest
+//   k_cert_verify      throughput: two waves per SIMD, each lane a strided
+//                      set of signatures (64 serial mixed additions each), P
+//                      compared with R's encoding after one inversion shared
+//                      by the lane's signatures; one lane per header digest
 //   k_cert_verify_lat  latency: one 128-thread workgroup per signature --
 //                      wave 0 hashes Certificate::digest and k, takes one
 //                      comb term per lane, sums the 64 terms by a 6-level
@@ -47,6 +49,8 @@
 //                      block's message schedule into LDS, then one wave
 //                      runs the rounds (coa_sha512.h, compress_kw).
 #include "coa_committee.h"
+
+#include <cstdlib>
 
 #include "coa_fe.h"
 #include "coa_ge.h"
@@ -194,107 +198,151 @@ COA_DEV void shfl_fe(fe& r, const fe& a, int off) {
   for (int i = 0; i < 8; i++) r.v[i] = (uint32_t)__shfl_xor((int)a.v[i], off, 64);
 }
 
-// One signature job; g = lane within its group of L lanes.
-template <int L>
-COA_DEV void sig_job(const CertArgs& a, uint32_t job, uint32_t g) {
+// Throughput path, phase A of one signature job: flags and
+// P = [s]B + [k](-A) from the combs (no doubling).  pre: bit0 s >= l, bit1 A
+// does not decompress, bit2 A small order, bit3 A has torsion, bit4 header
+// signature, bit5 key not registered, bit6 no job.
+#define PRE_S 1u
+#define PRE_A 2u
+#define PRE_SMALL_A 4u
+#define PRE_TORSION 8u
+#define PRE_HDR 16u
+#define PRE_UNCACHED 32u
+#define PRE_NONE 64u
+
+COA_DEV void job_comb(const CertArgs& a, uint32_t job, ge_p3& P, uint32_t& pre, uint32_t& cert) {
   const bool hdr = job < a.nc;
   const uint32_t vi = job - a.nc;
   const uint32_t c = hdr ? job : vote_cert(a.voff, a.nc, vi);
+  cert = c;
   const uint32_t* sig = hdr ? a.hsigs + (uint64_t)c * 16 : a.vsigs + (uint64_t)vi * 16;
   uint32_t pk[8], rw[8], sw[8], msg[8];
   load8(pk, hdr ? a.origins + (uint64_t)c * 8 : a.vpks + (uint64_t)vi * 8);
   load8(rw, sig);
   load8(sw, sig + 8);
   load8(msg, a.ids + (uint64_t)c * 8);
+  ge_p3_identity(P);
   const int slot = key_lookup(a.keys, a.nk, pk);
-  uint32_t bits = 0;
   if (slot < 0) {
-    bits = COA_CST_UNCACHED;
-  } else {
-    uint64_t st[8];
-    uint32_t h[16];
-    if (!hdr) {  // Certificate::digest = SHA-512(id || round u64 LE || origin)[..32]
-      uint32_t in[18];
-      const uint64_t rd = a.rounds[c];
+    pre = PRE_UNCACHED;
+    return;
+  }
+  uint64_t st[8];
+  uint32_t h[16];
+  if (!hdr) {  // Certificate::digest = SHA-512(id || round u64 LE || origin)[..32]
+    uint32_t in[18];
+    const uint64_t rd = a.rounds[c];
 #pragma unroll
-      for (int i = 0; i < 8; i++) in[i] = msg[i];
-      in[8] = (uint32_t)rd;
-      in[9] = (uint32_t)(rd >> 32);
-      load8(in + 10, a.origins + (uint64_t)c * 8);
-      coa_sha::hash_words<18>(st, in);
-      coa_sha::state_to_le_words(h, st);
+    for (int i = 0; i < 8; i++) in[i] = msg[i];
+    in[8] = (uint32_t)rd;
+    in[9] = (uint32_t)(rd >> 32);
+    load8(in + 10, a.origins + (uint64_t)c * 8);
+    coa_sha::hash_words<18>(st, in);
+    coa_sha::state_to_le_words(h, st);
 #pragma unroll
-      for (int i = 0; i < 8; i++) msg[i] = h[i];
-    }
-    {  // k = SHA-512(R || A || M) mod l
-      uint32_t in[24];
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        in[i] = rw[i];
-        in[8 + i] = pk[i];
-        in[16 + i] = msg[i];
-      }
-      coa_sha::hash_words<24>(st, in);
-      coa_sha::state_to_le_words(h, st);
-    }
-    sc k;
-    sc_reduce512(k, h);
-    const uint32_t kf = a.kflags[slot];
-    const bool s_ok = sc_is_canonical(sw);
-    const bool a_ok = (kf & COA_KEY_DECOMPRESSES) != 0;
-    // P = [s]B + [k](-A): terms t < 32 are B-comb bytes of s, t >= 32 the
-    // key-comb bytes of k (signed radix-256 digits, bytes of x + 0x80..80)
-    uint32_t sd[8], kd[8];
+    for (int i = 0; i < 8; i++) msg[i] = h[i];
+  }
+  {  // k = SHA-512(R || A || M) mod l
+    uint32_t in[24];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-      sd[i] = sw[i];
-      kd[i] = k.v[i];
+      in[i] = rw[i];
+      in[8 + i] = pk[i];
+      in[16 + i] = msg[i];
     }
-    add_const_word(sd, 0x80808080u);
-    add_const_word(kd, 0x80808080u);
-    const uint32_t* ktab = a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS;
-    ge_p3 P;
-    ge_p1p1 t;
-    ge_p3_identity(P);
-#pragma unroll 1
-    for (int term = (int)g; term < 64; term += L) {
-      const bool isb = term < 32;
-      const int j = term & 31;
-      const int e = (int)byte_of(isb ? sd : kd, j) - 128;
-      ge_niels q;
-      comb_select(q, isb ? a.comb : ktab, j, e);
-      ge_madd(t, P, q);
-      ge_p1p1_to_p3(P, t);
-    }
-    if constexpr (L > 1) {  // butterfly: every lane of the group ends with the sum
-#pragma unroll 1
-      for (int off = L / 2; off >= 1; off >>= 1) {
-        ge_p3 O;
-        shfl_fe<L>(O.X, P.X, off);
-        shfl_fe<L>(O.Y, P.Y, off);
-        shfl_fe<L>(O.Z, P.Z, off);
-        shfl_fe<L>(O.T, P.T, off);
-        ge_cached oc;
-        ge_p3_to_cached(oc, O);
-        ge_add(t, P, oc);
-        ge_p1p1_to_p3(P, t);
-      }
-    }
-    ge_p3 R;
-    const bool r_ok = ge_decompress(R, rw);
-    ge_p2 P2;
-    ge_p3_to_p2(P2, P);
-    const bool eq = ge_p2_eq_p3(P2, R);
-    if (hdr) {
-      const bool small = (kf & COA_KEY_SMALL_ORDER) != 0 || ge_is_small_order(R);
-      bits = (s_ok && a_ok && r_ok && !small && eq) ? 0u : COA_CST_BAD_HEADER_SIG;
-    } else if (!(s_ok && a_ok && r_ok)) {
-      bits = COA_CST_BAD_VOTES;
-    } else if (!eq || !(kf & COA_KEY_TORSION_FREE)) {
-      bits = COA_CST_VOTES_INCONCLUSIVE;
-    }
+    coa_sha::hash_words<24>(st, in);
+    coa_sha::state_to_le_words(h, st);
   }
-  if (g == 0 && bits) atomicOr(a.status + c, bits);
+  sc k;
+  sc_reduce512(k, h);
+  const uint32_t kf = a.kflags[slot];
+  pre = (sc_is_canonical(sw) ? 0u : PRE_S) | ((kf & COA_KEY_DECOMPRESSES) ? 0u : PRE_A) |
+        ((kf & COA_KEY_SMALL_ORDER) ? PRE_SMALL_A : 0u) | ((kf & COA_KEY_TORSION_FREE) ? 0u : PRE_TORSION) |
+        (hdr ? PRE_HDR : 0u);
+  // terms t < 32: B-comb bytes of s; t >= 32: key-comb bytes of k (signed
+  // radix-256 digits = bytes of x + 0x80..80)
+  uint32_t sd[8], kd[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    sd[i] = sw[i];
+    kd[i] = k.v[i];
+  }
+  add_const_word(sd, 0x80808080u);
+  add_const_word(kd, 0x80808080u);
+  const uint32_t* ktab = a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS;
+  ge_p1p1 t;
+#pragma unroll 1
+  for (int term = 0; term < 64; term++) {
+    const bool isb = term < 32;
+    const int j = term & 31;
+    const int e = (int)byte_of(isb ? sd : kd, j) - 128;
+    ge_niels q;
+    comb_select(q, isb ? a.comb : ktab, j, e);
+    ge_madd(t, P, q);
+    ge_p1p1_to_p3(P, t);
+  }
+}
+
+// Phase C: the verdict bits of a job from P's affine coordinates.  dalek's
+// `P == decompress(R)` holds iff y_P == y_R (mod p; R's y is read as 255 bits,
+// y >= p meaning y - p) and, unless x_P == 0, x_P's sign equals R's sign bit:
+// when y_P == y_R the point P itself proves that R decompresses (to +-x_P).
+COA_DEV uint32_t job_verdict(const CertArgs& a, uint32_t job, uint32_t pre, const fe& x, const fe& y) {
+  if (pre & (PRE_NONE | PRE_UNCACHED)) return (pre & PRE_UNCACHED) ? COA_CST_UNCACHED : 0u;
+  const bool hdr = (pre & PRE_HDR) != 0;
+  const uint32_t* sig = hdr ? a.hsigs + (uint64_t)job * 16 : a.vsigs + (uint64_t)(job - a.nc) * 16;
+  uint32_t rw[8];
+  load8(rw, sig);
+  fe yr, xc, yc;
+  fe_from_words(yr, rw);
+  fe_canon(yr, yr);
+  fe_canon(xc, x);
+  fe_canon(yc, y);
+  bool same_y = true, x_zero = true;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    same_y = same_y && yc.v[i] == yr.v[i];
+    x_zero = x_zero && xc.v[i] == 0;
+  }
+  const bool eq = same_y && (x_zero || (xc.v[0] & 1u) == (rw[7] >> 31));
+  const bool s_ok = !(pre & PRE_S), a_ok = !(pre & PRE_A);
+  if (hdr) {
+    // verify_strict: R == P, neither A nor R (== P) small order
+    fe xx, yy, ss;
+    fe_sq(xx, xc);
+    fe_sq(yy, yc);
+    fe_add(ss, xx, yy);
+    bool y_zero = true;
+#pragma unroll
+    for (int i = 0; i < 8; i++) y_zero = y_zero && yc.v[i] == 0;
+    const bool small_p = x_zero || y_zero || fe_iszero(ss);
+    return (s_ok && a_ok && !(pre & PRE_SMALL_A) && eq && !small_p) ? 0u : COA_CST_BAD_HEADER_SIG;
+  }
+  if (!(s_ok && a_ok)) return COA_CST_BAD_VOTES;
+  // P != R: R may not decompress (Err) or differ by a torsion point (a
+  // weight-dependent verdict) -- the host's exact RLC path decides both
+  return (eq && !(pre & PRE_TORSION)) ? 0u : COA_CST_VOTES_INCONCLUSIVE;
+}
+
+// Scratch slab of the throughput kernel: per job slot 9 uint4 rows, each row
+// lane-major (row r of slot q at uint4 index (q * 9 + r) * lanes + lane):
+// X, Y, Z, prefix product of the Z's (2 rows each), then (pre, cert, -, -).
+#define PSCR_ROWS 9
+COA_DEV void pscr_put(uint32_t* pscr, uint64_t lanes, uint64_t lane, int j, int row, const fe& f) {
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+    reinterpret_cast<uint4*>(pscr)[((uint64_t)j * PSCR_ROWS + row + h) * lanes + lane] =
+        make_uint4(f.v[4 * h], f.v[4 * h + 1], f.v[4 * h + 2], f.v[4 * h + 3]);
+}
+COA_DEV void pscr_get(fe& f, const uint32_t* pscr, uint64_t lanes, uint64_t lane, int j, int row) {
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint4 v = reinterpret_cast<const uint4*>(pscr)[((uint64_t)j * PSCR_ROWS + row + h) * lanes + lane];
+    f.v[4 * h] = v.x;
+    f.v[4 * h + 1] = v.y;
+    f.v[4 * h + 2] = v.z;
+    f.v[4 * h + 3] = v.w;
+  }
 }
 
 }  // namespace
@@ -352,8 +400,14 @@ __global__ void __launch_bounds__(256) k_key_tables(const uint32_t* __restrict__
   store_niels(out, M);
 }
 
-template <int L>
-__global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a) {
+// Throughput variant: a grid of two waves per SIMD; lane L takes the jobs
+// L, L + lanes, L + 2 lanes, ... (at most jpl of them).  Phase A computes
+// every job's P and parks it with the running product of the Z's in a
+// lane-major scratch slab; ONE field inversion serves all of a lane's jobs
+// (Montgomery's trick), then phase C compares each affine P with its R
+// encoding.  Per vote: ~265/jpl field operations of inversion instead of R's
+// ~277-operation decompression, and no wave-count tail.
+__global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a, uint32_t* __restrict__ pscr, uint32_t jpl) {
   if (blockIdx.x < a.hdr_blocks) {  // header digest role, one lane per certificate
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.nc) return;
@@ -369,12 +423,50 @@ __global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a) {
     if (!same) atomicOr(a.status + c, COA_CST_BAD_HEADER_ID);
     return;
   }
-  const uint64_t tid = (uint64_t)(blockIdx.x - a.hdr_blocks) * blockDim.x + threadIdx.x;
-  const uint64_t job = tid / L;
-  if (job >= (uint64_t)a.nc + a.nv) return;  // whole groups of L lanes leave together
-  sig_job<L>(a, (uint32_t)job, (uint32_t)(tid % L));
+  const uint64_t lanes = (uint64_t)(gridDim.x - a.hdr_blocks) * blockDim.x;
+  const uint64_t lane = (uint64_t)(blockIdx.x - a.hdr_blocks) * blockDim.x + threadIdx.x;
+  const uint64_t jobs = (uint64_t)a.nc + a.nv;
+  if (lane >= jobs) return;
+  const int nj = (int)min<uint64_t>(jpl, (jobs - lane + lanes - 1) / lanes);  // this lane's jobs
+  fe zp;  // running prefix product of the Z's
+#pragma unroll 1
+  for (int j = 0; j < nj; j++) {
+    const uint64_t job = lane + (uint64_t)j * lanes;
+    ge_p3 P;
+    uint32_t pre = PRE_NONE, cert = 0;
+    job_comb(a, (uint32_t)job, P, pre, cert);
+    if (j == 0) zp = P.Z;
+    else fe_mul(zp, zp, P.Z);
+    pscr_put(pscr, lanes, lane, j, 0, P.X);
+    pscr_put(pscr, lanes, lane, j, 2, P.Y);
+    pscr_put(pscr, lanes, lane, j, 4, P.Z);
+    pscr_put(pscr, lanes, lane, j, 6, zp);
+    reinterpret_cast<uint4*>(pscr)[((uint64_t)j * PSCR_ROWS + 8) * lanes + lane] = make_uint4(pre, cert, 0, 0);
+  }
+  fe inv;
+  fe_invert(inv, zp);
+#pragma unroll 1
+  for (int j = nj - 1; j >= 0; j--) {
+    fe zinv, x, y, X, Y;
+    if (j > 0) {
+      fe Z, zprev;
+      pscr_get(zprev, pscr, lanes, lane, j - 1, 6);
+      pscr_get(Z, pscr, lanes, lane, j, 4);
+      fe_mul(zinv, inv, zprev);
+      fe_mul(inv, inv, Z);
+    } else {
+      zinv = inv;
+    }
+    pscr_get(X, pscr, lanes, lane, j, 0);
+    pscr_get(Y, pscr, lanes, lane, j, 2);
+    const uint4 m = reinterpret_cast<const uint4*>(pscr)[((uint64_t)j * PSCR_ROWS + 8) * lanes + lane];
+    fe_mul(x, X, zinv);
+    fe_mul(y, Y, zinv);
+    const uint64_t job = lane + (uint64_t)j * lanes;
+    const uint32_t bits = job_verdict(a, (uint32_t)job, m.x, x, y);
+    if (bits) atomicOr(a.status + m.y, bits);
+  }
 }
-
 
 // ---------------------------------------------------------------------------
 // Latency variant (one certificate at a time): see the file comment.
@@ -537,6 +629,17 @@ __global__ void __launch_bounds__(128) k_cert_verify_lat(CertArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Grid of the throughput kernel: two waves per SIMD (256 CUs x 4 SIMDs x 2
+// x 64 lanes), or one lane per job when there are fewer jobs.
+// COA_CERT_LANES_TOTAL overrides (A/B runs).
+uint64_t cert_tp_lanes(uint64_t jobs) {
+  uint64_t target = 256ull * 4 * 2 * 64;
+  if (const char* e = getenv("COA_CERT_LANES_TOTAL")) target = strtoull(e, nullptr, 10);
+  if (target < 256) target = 256;
+  const uint64_t lanes = jobs < target ? jobs : target;
+  return (lanes + 255) / 256 * 256;
+}
+
 hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s) {
   if (nk == 0) return hipSuccess;
   hipLaunchKernelGGL(k_key_flags, dim3((nk + 255) / 256), dim3(256), 0, s, keys, nk, flags);
@@ -550,7 +653,13 @@ hipError_t coa_launch_key_tables(const uint32_t* keys, uint32_t nk, uint32_t* ta
   return hipGetLastError();
 }
 
-hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, hipStream_t s) {
+size_t coa_cert_scratch_bytes(uint64_t jobs) {
+  const uint64_t lanes = cert_tp_lanes(jobs ? jobs : 1);
+  const uint64_t jpl = (jobs + lanes - 1) / lanes;
+  return (size_t)(lanes * (jpl ? jpl : 1) * 9 * 16 + 256);
+}
+
+hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr, hipStream_t s) {
   if (a.nc == 0) return hipSuccess;
   a.hdr_blocks = (a.nc + 255) / 256;
   const uint64_t jobs = (uint64_t)a.nc + a.nv;
@@ -558,7 +667,8 @@ hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, hipStream_t s) 
     hipLaunchKernelGGL(k_cert_verify_lat, dim3((uint32_t)(a.nc + jobs)), dim3(128), 0, s, a);
     return hipGetLastError();
   }
-  const uint64_t sig_blocks = (jobs + 255) / 256;
-  hipLaunchKernelGGL(k_cert_verify<1>, dim3((uint32_t)(a.hdr_blocks + sig_blocks)), dim3(256), 0, s, a);
+  const uint64_t lanes = cert_tp_lanes(jobs);
+  const uint32_t jpl = (uint32_t)((jobs + lanes - 1) / lanes);
+  hipLaunchKernelGGL(k_cert_verify, dim3((uint32_t)(a.hdr_blocks + lanes / 256)), dim3(256), 0, s, a, pscr, jpl);
   return hipGetLastError();
 }

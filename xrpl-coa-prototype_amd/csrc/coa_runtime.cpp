@@ -97,13 +97,13 @@ struct Dev {
   uint32_t* comb = nullptr;  // 32 x 128 x (v+1)256^j B comb for k_verify_halved (384 KiB)
   DevBuf msgs, pks, sigs, kbuf, rec, verdicts, scratch, aux, rbuf, seeds, offs, data, out, idx, zs, terms, flags;
   // committee key cache (f2): sorted keys, flags, one comb of -A per key
-  DevBuf ckeys, kflags, ktabs, cert;
+  DevBuf ckeys, kflags, ktabs, cert, cscr;
   uint32_t nkeys = 0;
   PinBuf pin;
   std::mutex mu;
   std::vector<DevBuf*> all() {
     return {&msgs,  &pks,  &sigs, &kbuf, &rec, &verdicts, &scratch, &aux,  &rbuf,   &seeds, &offs,
-            &data,  &out,  &idx,  &zs,   &terms, &flags,  &ckeys,   &kflags, &ktabs, &cert};
+            &data,  &out,  &idx,  &zs,   &terms, &flags,  &ckeys,   &kflags, &ktabs, &cert, &cscr};
   }
 };
 
@@ -448,7 +448,9 @@ int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_
   hipStream_t s = d.stream;
   HIP_TRY(hipMemcpyAsync(d.cert.p, h, p.total, hipMemcpyHostToDevice, s));
   CertArgs a = cert_args(d, d.cert.as<uint8_t>(), p, nc, nv);
-  HIP_TRY(coa_launch_cert_verify(a, cert_lanes(nc + nv), s));
+  const int lanes = cert_lanes(nc + nv);
+  if (lanes == 1) HIP_TRY(d.cscr.ensure(coa_cert_scratch_bytes(nc + nv)));
+  HIP_TRY(coa_launch_cert_verify(a, lanes, d.cscr.as<uint32_t>(), s));
   HIP_TRY(hipMemcpyAsync(h + p.status, d.cert.as<uint8_t>() + p.status, nc * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   std::memcpy(status_out + lo, h + p.status, nc * 4);
@@ -894,11 +896,13 @@ int coa_certificate_verify(const uint8_t* header_data, size_t header_len, const 
   return rc != COA_OK ? rc : (int)st;
 }
 
+size_t coa_certificate_workspace_bytes(size_t n, size_t n_votes) { return coa_cert_scratch_bytes(n + n_votes); }
+
 int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data, const uint64_t* d_header_offsets,
                                        const uint8_t* d_ids, const uint8_t* d_origins, const uint8_t* d_header_sigs,
                                        const uint64_t* d_rounds, const uint8_t* d_vote_pks,
                                        const uint8_t* d_vote_sigs, const uint64_t* d_vote_offsets, size_t n,
-                                       size_t n_votes, uint32_t* d_status, void* stream) {
+                                       size_t n_votes, uint32_t* d_status, void* workspace, void* stream) {
   int rc = ensure_init();
   if (rc != COA_OK) return rc;
   if (n == 0) return COA_OK;
@@ -929,8 +933,16 @@ int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data,
   a.nk = d->nkeys;
   a.comb = d->comb;
   a.status = d_status;
+  const int lanes = cert_lanes(n + n_votes);
   HIP_TRY(hipMemsetAsync(d_status, 0, n * 4, s));
-  HIP_TRY(coa_launch_cert_verify(a, cert_lanes(n + n_votes), s));
+  if (workspace || lanes == 64) {
+    HIP_TRY(coa_launch_cert_verify(a, lanes, static_cast<uint32_t*>(workspace), s));
+    return COA_OK;
+  }
+  std::lock_guard<std::mutex> l(d->mu);
+  HIP_TRY(d->cscr.ensure(coa_cert_scratch_bytes(n + n_votes)));
+  HIP_TRY(coa_launch_cert_verify(a, lanes, d->cscr.as<uint32_t>(), s));
+  HIP_TRY(hipStreamSynchronize(s));  // engine-owned workspace: drain before release
   return COA_OK;
 }
 
