@@ -64,16 +64,36 @@ COA_DEV void shr1_8(uint32_t* x) {
   for (int i = 0; i < 8; i++) x[i] = __builtin_amdgcn_alignbit(i < 7 ? x[i + 1] : 0u, x[i], 1);
 }
 
+// 8-limb add / subtract with carry / borrow out, as one unpadded VCC chain
+// (hipcc pads every VCC hand-off of __builtin_addc/subc with s_nop on gfx950;
+// see coa_fe.h).  The last instruction turns VCC into the 0/1 result word.
+#define COA_CHAIN8(OP0, OPC)                                                       \
+  OP0 " %0, vcc, %9, %17\n\t" OPC " %1, vcc, %10, %18, vcc\n\t"                 \
+  OPC " %2, vcc, %11, %19, vcc\n\t" OPC " %3, vcc, %12, %20, vcc\n\t"           \
+  OPC " %4, vcc, %13, %21, vcc\n\t" OPC " %5, vcc, %14, %22, vcc\n\t"           \
+  OPC " %6, vcc, %15, %23, vcc\n\t" OPC " %7, vcc, %16, %24, vcc\n\t"           \
+  "v_addc_co_u32_e32 %8, vcc, 0, %25, vcc"
+#define COA_CHAIN8_OPS(r, a, b, c, z)                                                                        \
+  : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]), \
+    "=&v"(c)                                                                                                 \
+  : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(b[0]),      \
+    "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]), "v"(z)                      \
+  : "vcc"
+
 COA_DEV uint32_t sub8(uint32_t* r, const uint32_t* a, const uint32_t* b) {
-  uint32_t bw = 0;
+  uint32_t o[8], bw;
+  const uint32_t z = 0;
+  asm(COA_CHAIN8("v_sub_co_u32_e32", "v_subb_co_u32_e32") COA_CHAIN8_OPS(o, a, b, bw, z));
 #pragma unroll
-  for (int i = 0; i < 8; i++) r[i] = subb32(a[i], b[i], bw, bw);
+  for (int i = 0; i < 8; i++) r[i] = o[i];
   return bw;
 }
 COA_DEV uint32_t add8(uint32_t* r, const uint32_t* a, const uint32_t* b) {
-  uint32_t c = 0;
+  uint32_t o[8], c;
+  const uint32_t z = 0;
+  asm(COA_CHAIN8("v_add_co_u32_e32", "v_addc_co_u32_e32") COA_CHAIN8_OPS(o, a, b, c, z));
 #pragma unroll
-  for (int i = 0; i < 8; i++) r[i] = addc32(a[i], b[i], c, c);
+  for (int i = 0; i < 8; i++) r[i] = o[i];
   return c;
 }
 
@@ -84,7 +104,8 @@ COA_DEV double to_f64(const uint32_t* x) {
   return d;
 }
 
-// r = a - q*b (mod 2^288); returns the borrow (1 if a < q*b).
+// r = a - q*b (mod 2^256); returns 1 if a < q*b (the borrow out of the
+// 288-bit subtraction, top word included).
 COA_DEV uint32_t submul8(uint32_t* r, const uint32_t* a, const uint32_t* b, uint32_t q) {
   uint32_t pr[9];
   uint64_t acc = 0;
@@ -94,11 +115,25 @@ COA_DEV uint32_t submul8(uint32_t* r, const uint32_t* a, const uint32_t* b, uint
     pr[i] = (uint32_t)acc;
   }
   pr[8] = (uint32_t)(acc >> 32);
-  uint32_t bw = 0;
+  uint32_t o[8], bw;
+  const uint32_t z = 0;
+  asm("v_sub_co_u32_e32 %0, vcc, %9, %17\n\t"
+      "v_subb_co_u32_e32 %1, vcc, %10, %18, vcc\n\t"
+      "v_subb_co_u32_e32 %2, vcc, %11, %19, vcc\n\t"
+      "v_subb_co_u32_e32 %3, vcc, %12, %20, vcc\n\t"
+      "v_subb_co_u32_e32 %4, vcc, %13, %21, vcc\n\t"
+      "v_subb_co_u32_e32 %5, vcc, %14, %22, vcc\n\t"
+      "v_subb_co_u32_e32 %6, vcc, %15, %23, vcc\n\t"
+      "v_subb_co_u32_e32 %7, vcc, %16, %24, vcc\n\t"
+      "v_subb_co_u32_e32 %8, vcc, %26, %25, vcc\n\t"
+      "v_addc_co_u32_e32 %8, vcc, 0, %26, vcc"
+      : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7]),
+        "=&v"(bw)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(pr[0]),
+        "v"(pr[1]), "v"(pr[2]), "v"(pr[3]), "v"(pr[4]), "v"(pr[5]), "v"(pr[6]), "v"(pr[7]), "v"(pr[8]), "v"(z)
+      : "vcc");
 #pragma unroll
-  for (int i = 0; i < 8; i++) r[i] = subb32(a[i], pr[i], bw, bw);
-  uint32_t top = subb32(0u, pr[8], bw, bw);
-  (void)top;
+  for (int i = 0; i < 8; i++) r[i] = o[i];
   return bw;
 }
 
@@ -149,10 +184,16 @@ COA_DEV void halve(uint32_t* c_out, uint32_t* d_out, int& cost_out, bool& neg_ou
   bool tb_neg = false;  // sign of t_b; t_a has the opposite sign
   int best = max(bitlen(k, 8), 1);
   bool best_neg = false;
+  int lb = bitlen(b, 8);
+  double af = to_f64(a), bf = to_f64(b);  // f64 images, carried across steps
   for (int guard = 0; guard < 400; guard++) {
-    const int lb = bitlen(b, 8);
     if (lb <= 118) break;
-    const double qd = floor(to_f64(a) / to_f64(b));
+    // quotient estimate: a correctly rounded f64 division of the f64 images
+    // (relative error ~2^-50), so for q < 2^31 floor() is off by at most one
+    // and the fix-ups below correct it.  NOT v_rcp_f64: its approximation
+    // error let a rare large quotient overshoot the fix-ups (one valid
+    // signature in 4M rejected, tests/test_gpu_halve.py pins such k).
+    const double qd = floor(af / bf);
     uint32_t r[8], mr[8];
     if (qd < 2147483648.0) {
       uint32_t q = (uint32_t)qd;
@@ -189,6 +230,7 @@ COA_DEV void halve(uint32_t* c_out, uint32_t* d_out, int& cost_out, bool& neg_ou
           a[i] = r[i];
           ma[i] = mr[i];
         }
+        af = to_f64(a);
         continue;
       }
     }
@@ -201,7 +243,10 @@ COA_DEV void halve(uint32_t* c_out, uint32_t* d_out, int& cost_out, bool& neg_ou
       mb[i] = mr[i];
     }
     tb_neg = !tb_neg;
-    if (bitlen(b, 8) <= 136) {
+    lb = bitlen(b, 8);
+    af = bf;
+    bf = to_f64(b);
+    if (lb <= 136) {
       consider(c_out, d_out, best, best_neg, b, mb, tb_neg);
       consider(c_out, d_out, best, best_neg, a, ma, !tb_neg);
       if ((ma[0] ^ mb[0]) & 1) {
