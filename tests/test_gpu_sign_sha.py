@@ -66,3 +66,22 @@ def test_worker_batch_500kb(engine):
     out = engine.sha512_many(batches)
     for b, d in zip(batches, out):
         assert bytes(d) == hashlib.sha512(b).digest()
+
+
+@pytest.mark.parametrize("lanes", ["1", "2", "4", "16", "64", "auto"])
+def test_sha512_lanes_per_message_ragged(engine, lanes, monkeypatch):
+    """SHA-512 with L lanes per message (shared message schedule in LDS):
+    ragged lengths around the padding boundaries, multi-block, empty and
+    mixed lengths inside one wave, vs hashlib."""
+    import hashlib
+    import random
+
+    if lanes != "auto":
+        monkeypatch.setenv("COA_SHA_LANES", lanes)
+    rng = random.Random(int(lanes) if lanes != "auto" else 99)
+    lens = [0, 1, 111, 112, 113, 127, 128, 129, 239, 240, 255, 256, 1000, 3336, 9001]
+    lens += [rng.randrange(0, 5000) for _ in range(70)]
+    msgs = [bytes(rng.getrandbits(8) for _ in range(n)) for n in lens]
+    got = engine.sha512_many(msgs)
+    for m, g in zip(msgs, got):
+        assert bytes(g) == hashlib.sha512(m).digest(), len(m)

@@ -15,6 +15,8 @@
 //                     (crypto/src/lib.rs:185-191); used to synthesise inputs.
 #include "coa_kernels.h"
 
+#include <cstdlib>
+
 #include "coa_fe.h"
 #include "coa_ge.h"
 #include "coa_sc.h"
@@ -275,6 +277,58 @@ __global__ void __launch_bounds__(256) k_sha512_many(const uint8_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// SHA-512 of few long messages (worker batches): L lanes per message.  A lone
+// lane hashing a 500 KB batch is bound by its own instruction stream (~42
+// VALU instructions per round with the message schedule inline), and with
+// fewer messages than 64 x SIMDs most of the chip idles.  Here the L lanes of
+// a message expand the schedules of L consecutive blocks at once into LDS
+// (kw[t][slot], slot = j * G + group, conflict-free), then all L run the
+// rounds of those L blocks from LDS (28 instructions per round).  One
+// 64-thread workgroup per wave; G = 64 / L messages per wave.
+// ---------------------------------------------------------------------------
+template <int L>
+__global__ void __launch_bounds__(64) k_sha512_ml(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                                                  uint32_t n, uint32_t* __restrict__ out) {
+  constexpr int G = 64 / L;
+  __shared__ uint64_t kw[80 * 64];  // 40 KiB
+  const uint32_t lane = threadIdx.x, grp = lane / L, q = lane % L;
+  const uint32_t msg = blockIdx.x * G + grp;
+  const bool live = msg < n;
+  const uint64_t o0 = live ? off[msg] : 0, len = live ? off[msg + 1] - o0 : 0;
+  const uint8_t* p = data + o0;
+  const uint64_t nblk = live ? (len + 17 + 127) / 128 : 0;
+  uint64_t maxblk = nblk;  // wave-uniform trip count
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t other = ((uint64_t)__shfl_xor((int)(maxblk >> 32), o, 64) << 32) |
+                           (uint32_t)__shfl_xor((int)(uint32_t)maxblk, o, 64);
+    maxblk = other > maxblk ? other : maxblk;
+  }
+  uint64_t st[8];
+  coa_sha::init(st);
+#pragma unroll 1
+  for (uint64_t b0 = 0; b0 < maxblk; b0 += L) {
+    if (b0 + q < nblk) {
+      uint64_t W[16];
+      coa_sha::padded_block(W, p, len, b0 + q, nblk);
+      coa_sha::expand_kws<64>(kw + q * G + grp, W);
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int j = 0; j < L; j++)
+      if (b0 + j < nblk) coa_sha::compress_kws<64>(st, kw + j * G + grp);
+    __syncthreads();
+  }
+  if (live && q == 0) {
+    uint32_t h[16];
+    coa_sha::state_to_le_words(h, st);
+    uint4* o = reinterpret_cast<uint4*>(out + (uint64_t)msg * 16);
+#pragma unroll
+    for (int i = 0; i < 4; i++) o[i] = make_uint4(h[4 * i], h[4 * i + 1], h[4 * i + 2], h[4 * i + 3]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // RFC 8032 signing (crypto::Signature::new / dalek Keypair::sign), used to
 // synthesise benchmark inputs on the device.
 // ---------------------------------------------------------------------------
@@ -418,7 +472,21 @@ hipError_t coa_launch_verify_strict(const uint8_t* pks, const uint8_t* sigs, con
 hipError_t coa_launch_sha512_many(const uint8_t* data, const uint64_t* off, uint32_t n, uint32_t* out,
                                   hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_sha512_many, dim3(grid_for(n, 64, 65536)), dim3(64), 0, s, data, off, n, out);
+  // lanes per message: enough messages fill 1024 waves (one per SIMD) with
+  // one lane each; fewer share the schedule work (COA_SHA_LANES overrides)
+  uint32_t L = 1;
+  while (L < 64 && (uint64_t)n * L * 2 <= 65536) L *= 2;
+  if (const char* e = getenv("COA_SHA_LANES")) L = (uint32_t)atoi(e);
+  const uint32_t waves = (uint32_t)(((uint64_t)n * L + 63) / 64);
+  switch (L) {
+    case 2: hipLaunchKernelGGL(k_sha512_ml<2>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
+    case 4: hipLaunchKernelGGL(k_sha512_ml<4>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
+    case 8: hipLaunchKernelGGL(k_sha512_ml<8>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
+    case 16: hipLaunchKernelGGL(k_sha512_ml<16>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
+    case 32: hipLaunchKernelGGL(k_sha512_ml<32>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
+    case 64: hipLaunchKernelGGL(k_sha512_ml<64>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
+    default: hipLaunchKernelGGL(k_sha512_many, dim3(grid_for(n, 64, 65536)), dim3(64), 0, s, data, off, n, out);
+  }
   return hipGetLastError();
 }
 

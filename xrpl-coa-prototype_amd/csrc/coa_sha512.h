@@ -417,4 +417,57 @@ COA_DEV void compress_kw(uint64_t st[8], const uint64_t* kw) {
   st[7] += h;
 }
 
+// compress_kw with kw[t] at kw[t * STRIDE] (the shared-schedule kernel's
+// lane-interleaved LDS layout).
+template <int STRIDE>
+COA_DEV void compress_kws(uint64_t st[8], const uint64_t* kw) {
+  uint64_t a = st[0], b = st[1], c = st[2], d = st[3];
+  uint64_t e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll 1
+  for (int r = 0; r < 80; r += 16) {
+    const uint64_t* k = kw + r * STRIDE;
+    round_(a, b, c, d, e, f, g, h, k[0 * STRIDE]);
+    round_(h, a, b, c, d, e, f, g, k[1 * STRIDE]);
+    round_(g, h, a, b, c, d, e, f, k[2 * STRIDE]);
+    round_(f, g, h, a, b, c, d, e, k[3 * STRIDE]);
+    round_(e, f, g, h, a, b, c, d, k[4 * STRIDE]);
+    round_(d, e, f, g, h, a, b, c, k[5 * STRIDE]);
+    round_(c, d, e, f, g, h, a, b, k[6 * STRIDE]);
+    round_(b, c, d, e, f, g, h, a, k[7 * STRIDE]);
+    round_(a, b, c, d, e, f, g, h, k[8 * STRIDE]);
+    round_(h, a, b, c, d, e, f, g, k[9 * STRIDE]);
+    round_(g, h, a, b, c, d, e, f, k[10 * STRIDE]);
+    round_(f, g, h, a, b, c, d, e, k[11 * STRIDE]);
+    round_(e, f, g, h, a, b, c, d, k[12 * STRIDE]);
+    round_(d, e, f, g, h, a, b, c, k[13 * STRIDE]);
+    round_(c, d, e, f, g, h, a, b, k[14 * STRIDE]);
+    round_(b, c, d, e, f, g, h, a, k[15 * STRIDE]);
+  }
+  st[0] += a;
+  st[1] += b;
+  st[2] += c;
+  st[3] += d;
+  st[4] += e;
+  st[5] += f;
+  st[6] += g;
+  st[7] += h;
+}
+
+// expand_kw writing kw[t] to kw[t * STRIDE].
+template <int STRIDE>
+COA_DEV void expand_kws(uint64_t* kw, uint64_t W[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) kw[i * STRIDE] = K512[i] + W[i];
+#pragma unroll 1
+  for (int r = 16; r < 80; r += 16) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
+      W[i] += xor3(rotr<1>(w15), rotr<8>(w15), shr<7>(w15)) + W[(i + 9) & 15] +
+              xor3(rotr<19>(w2), rotr<61>(w2), shr<6>(w2));
+      kw[(r + i) * STRIDE] = K512[r + i] + W[i];
+    }
+  }
+}
+
 }  // namespace coa_sha
