@@ -85,7 +85,7 @@ def cpu_baseline(msgs, pks, sigs, seconds):
     one = coa_oracle.verify_strict_many(m[:2048], p[:2048], s[:2048], 1)
     st = time.perf_counter() - t1
     assert int(one.sum()) == 0
-    return {
+    out = {
         "value": done / el,
         "unit": "verifications/s",
         "cores": threads,
@@ -94,6 +94,38 @@ def cpu_baseline(msgs, pks, sigs, seconds):
                   f"{threads} threads, {el:.1f} s wall ({el * threads:.1f} thread-s)",
         "single_thread_value": 2048 / st,
     }
+    sodium = libsodium_baseline(m, p, s, threads, min(seconds, 1.0))
+    if sodium:
+        out["second_reference"] = sodium
+    return out
+
+
+def libsodium_baseline(m, p, s, threads, seconds):
+    """Second CPU reference: libsodium's
+    crypto_sign_verify_detached on the same triples and thread split, driven
+    from C threads (oracle/sodium_drive.c), when the box has the library.  Its
+    acceptance rules differ from dalek's only on non-canonical and small-order
+    encodings, which these valid triples do not contain."""
+    import coa_oracle
+
+    first = coa_oracle.sodium_verify_many(m[:64], p[:64], s[:64], 1)
+    if first is None:
+        return None
+    done, t0 = 0, time.perf_counter()
+    while True:
+        out, ver = coa_oracle.sodium_verify_many(m, p, s, threads)
+        assert int(out.sum()) == 0, "libsodium rejected a valid benchmark signature"
+        done += len(p)
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    t1 = time.perf_counter()
+    one, _ = coa_oracle.sodium_verify_many(m[:2048], p[:2048], s[:2048], 1)
+    st = time.perf_counter() - t1
+    assert int(one.sum()) == 0
+    return {"value": done / el, "unit": "verifications/s", "cores": threads, "single_thread_value": 2048 / st,
+            "kind": f"libsodium {ver} crypto_sign_verify_detached",
+            "sample": f"{done} C2 triples ({done // len(p)} passes over the first {len(p)}), {threads} threads"}
 
 
 def worker_batches_on_device(nb, dev):

@@ -12,9 +12,11 @@ _libs = {}
 
 
 def build():
-    src = os.path.join(HERE, "coa_oracle.c")
-    outs = [os.path.join(BUILD, n) for n in ("libcoa_oracle.so", "libcoa_oracle_count.so")]
-    if all(os.path.exists(o) and os.path.getmtime(o) >= os.path.getmtime(src) for o in outs):
+    pairs = [("coa_oracle.c", "libcoa_oracle.so"), ("coa_oracle.c", "libcoa_oracle_count.so"),
+             ("sodium_drive.c", "libcoa_sodium_drive.so")]
+    if all(os.path.exists(os.path.join(BUILD, o))
+           and os.path.getmtime(os.path.join(BUILD, o)) >= os.path.getmtime(os.path.join(HERE, s))
+           for s, o in pairs):
         return
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
@@ -41,6 +43,31 @@ def lib(count=False):
             L.coa_oracle_reset_counts.argtypes = []
         _libs[key] = L
     return _libs[key]
+
+
+SODIUM = "/opt/conda/lib/libsodium.so"
+
+
+def sodium_verify_many(msgs, pks, sigs, nthreads=1, path=SODIUM):
+    """libsodium crypto_sign_verify_detached over rows (second CPU reference,
+    bench.py only).  Returns (out, version) or None when libsodium is absent."""
+    if "sodium" not in _libs:
+        build()
+        L = ctypes.CDLL(os.path.join(BUILD, "libcoa_sodium_drive.so"))
+        P8 = ctypes.POINTER(ctypes.c_uint8)
+        L.coa_sodium_verify_many.argtypes = [ctypes.c_char_p, P8, ctypes.c_size_t, P8, P8, ctypes.c_size_t, P8,
+                                             ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]
+        L.coa_sodium_verify_many.restype = ctypes.c_int
+        _libs["sodium"] = L
+    msgs, pks, sigs = (np.ascontiguousarray(a, dtype=np.uint8) for a in (msgs, pks, sigs))
+    n = pks.shape[0]
+    out = np.zeros(n, np.uint8)
+    ver = ctypes.c_char_p()
+    rc = _libs["sodium"].coa_sodium_verify_many(path.encode(), _p(msgs), msgs.shape[1], _p(pks), _p(sigs), n,
+                                                _p(out), nthreads, ctypes.byref(ver))
+    if rc != 0:
+        return None
+    return out, ver.value.decode()
 
 
 def _p(a):

@@ -63,3 +63,25 @@ def test_c_oracle_batch_random_z_torsion_free():
     for _ in range(3):
         zs = [rng.getrandbits(128) for _ in seeds]
         assert co.verify_batch(m, pks, sigs, zs) and o.verify_batch(m, pks, sigs, zs)
+
+
+def test_libsodium_second_reference_agrees_on_canonical_triples():
+    """bench.py's second CPU reference (oracle/sodium_drive.c) gives dalek's
+    verdicts on canonical valid / tampered triples (the only inputs it is
+    timed on); skipped where the image has no libsodium."""
+    import pytest
+
+    n = 48
+    seeds = [o.sha512(b"sod" + struct.pack("<Q", i))[:32] for i in range(n)]
+    ms = [o.sha512(struct.pack("<Q", 7 * i))[:32] for i in range(n)]
+    sigs = [bytearray(o.sign(s, m)) for s, m in zip(seeds, ms)]
+    ms = [bytearray(m) for m in ms]
+    for i in range(0, n, 3):
+        (sigs[i] if i % 2 else ms[i])[i % 32] ^= 1 << (i % 8)   # tamper R/s or the message
+    A = lambda rows, w: np.frombuffer(b"".join(bytes(r) for r in rows), np.uint8).reshape(n, w).copy()  # noqa
+    msgs, pks, sg = A(ms, 32), A([o.public_key(s) for s in seeds], 32), A(sigs, 64)
+    got = co.sodium_verify_many(msgs, pks, sg, 2)
+    if got is None:
+        pytest.skip("libsodium not present")
+    assert (got[0] == co.verify_strict_many(msgs, pks, sg, 2)).all()
+    assert int(got[0].sum()) == len(range(0, n, 3))
