@@ -50,6 +50,12 @@ int coa_init(int n_gpus);
 int coa_init_devices(const int* device_ids, int n);
 int coa_shutdown(void);
 int coa_device_count(void);
+/* Self-test of device `device`'s fixed-base tables (no reference
+ * counterpart): checks every entry of the wide HBM comb of B against its
+ * neighbours (m*2^(Wj)*B = (m-1)*2^(Wj)*B + 2^(Wj)*B, 2^(W(j+1))*B =
+ * [2^W] 2^(Wj)*B, entry (0,1) = B, canonical encodings).  *bad_entries gets
+ * the number of failing entries (0 when the table is absent: COA_WCOMB=0). */
+int coa_self_test(int device, uint64_t* bad_entries);
 /* Human-readable description of the last error on this thread. */
 const char* coa_last_error(void);
 /* Library / ABI version string. */

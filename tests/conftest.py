@@ -32,7 +32,14 @@ def load_golden(name):
 
 @pytest.fixture(scope="session")
 def engine():
-    """The built engine library, initialised on the GPU (gpu tests only)."""
+    """The built engine library, initialised on the GPU (gpu tests only).
+
+    torch is imported first: the engine links libamdhip64 by soname, so the
+    process then holds one HIP runtime (torch's).  Loaded the other way round,
+    torch's bundled runtime is a second copy that sees no GPU
+    (tools/probe_torch_after_init.py)."""
+    import torch  # noqa: F401
+
     import build  # xrpl-coa-prototype_amd/build.py
 
     build.build()

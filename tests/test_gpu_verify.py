@@ -108,3 +108,21 @@ def test_grid_stride_large_n_all_valid(engine):
     v = engine.verify_strict_many(msgs, pks, sigs2)
     assert (v[~bad] == 0).all()
     assert (v[bad] == 1).all()
+
+
+def test_wide_comb_table_consistent(engine):
+    """Every entry of the 654 MB HBM comb of B is m * 2^(20 j) * B: checked on
+    the device against its neighbours, independently of how it was built."""
+    assert engine.self_test(0) == 0
+
+
+def test_wide_comb_matches_radix256_comb(engine, monkeypatch):
+    """[e]B through the wide comb (default) and through the radix-256 comb
+    (COA_WCOMB=0, read per call) give the same verdicts on valid, tampered
+    and adversarial triples."""
+    msgs, pks, sigs, exp = _mixed_inputs(400, 11)
+    wide = engine.verify_strict_many(msgs, pks, sigs)
+    monkeypatch.setenv("COA_WCOMB", "0")
+    narrow = engine.verify_strict_many(msgs, pks, sigs)
+    assert (wide == narrow).all()
+    assert ((wide == 0) == exp).all()

@@ -19,6 +19,11 @@ calls raise EngineError -- there is no CPU fallback.
 Bulk (engine-level) entry points, used by the primary/worker callers'
 batching paths and by the benchmark, take numpy arrays (host) or torch
 tensors (device) -- see verify_strict_many, verify_batch_groups, sha512_many.
+
+A process that also uses torch's GPU API must import torch before the first
+call here: the library links libamdhip64 by soname and then shares torch's
+HIP runtime; loaded first, it brings ROCm's own runtime and torch's bundled
+copy finds no GPU (tools/probe_torch_after_init.py).
 """
 import base64
 import ctypes
@@ -66,6 +71,7 @@ def lib():
         "coa_init_devices": ([ctypes.POINTER(ctypes.c_int), ctypes.c_int], ctypes.c_int),
         "coa_shutdown": ([], ctypes.c_int),
         "coa_device_count": ([], ctypes.c_int),
+        "coa_self_test": ([ctypes.c_int, P64], ctypes.c_int),
         "coa_last_error": ([], ctypes.c_char_p),
         "coa_version": ([], ctypes.c_char_p),
         "coa_ed25519_verify_strict": ([P8, P8, P8], ctypes.c_int),
@@ -265,6 +271,14 @@ def init_devices(ids):
 
 def device_count():
     return _check(lib().coa_device_count())
+
+
+def self_test(device=0):
+    """Number of inconsistent entries in the device's wide B comb (0 = every
+    entry is m * 2^(20 j) * B; also 0 when the table is disabled)."""
+    bad = ctypes.c_uint64(0)
+    _check(lib().coa_self_test(device, ctypes.byref(bad)))
+    return bad.value
 
 
 def verify_strict_many(msgs, pks, sigs):

@@ -4,6 +4,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// wide HBM comb of B (coa_smul.h): positions x magnitudes, 24 dwords each
+#define COA_WCOMB_W 20
+#define COA_WCOMB_POS 13
+#define COA_WCOMB_MAG (1u << (COA_WCOMB_W - 1))
+#define COA_WCOMB_ENTRIES ((uint64_t)COA_WCOMB_POS * COA_WCOMB_MAG)
+#define COA_WCOMB_DWORDS (COA_WCOMB_ENTRIES * 24)
 #define COA_COMB_ENTRIES (32 * 128)
 #define COA_COMB_DWORDS (COA_COMB_ENTRIES * 24)
 // k_halve record per signature: c[8] | |d|[8] | e[8] | meta | pad[7]
@@ -15,4 +21,9 @@ hipError_t coa_launch_build_comb(uint32_t* comb, const uint32_t* btab, hipStream
 hipError_t coa_launch_halve(const uint32_t* kbuf, const uint8_t* sigs, uint32_t n, uint32_t* rec, hipStream_t s);
 hipError_t coa_launch_verify_halved(const uint8_t* pks, const uint8_t* sigs, const uint32_t* rec, uint32_t n,
                                     uint8_t* verdicts, uint32_t* scratch, uint32_t scratch_lanes,
-                                    const uint32_t* comb, int waves, hipStream_t s);
+                                    const uint32_t* comb, const uint32_t* wcomb, int waves, hipStream_t s);
+// wide HBM comb of B (coa_smul.h, COA_WCOMB_*): build from the radix-256
+// comb, and the whole-table consistency check (count of bad entries in *bad,
+// zeroed by the caller)
+hipError_t coa_launch_build_wcomb(uint32_t* wcomb, const uint32_t* comb, hipStream_t s);
+hipError_t coa_launch_check_wcomb(const uint32_t* wcomb, uint32_t* bad, hipStream_t s);

@@ -355,6 +355,146 @@ __global__ void __launch_bounds__(256) k_build_comb(uint32_t* __restrict__ comb,
   }
 }
 
+// Wide comb entry id = j * 2^(W-1) + (m - 1): m * 2^(W j) * B by the
+// doubling-free radix-256 comb (32 mixed additions), made affine.
+__global__ void __launch_bounds__(256) k_build_wcomb(uint32_t* __restrict__ wcomb, const uint32_t* __restrict__ comb) {
+  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= COA_WCOMB_ENTRIES) return;
+  const int j = (int)(id / COA_WCOMB_MAG);
+  const uint32_t m = (uint32_t)(id % COA_WCOMB_MAG) + 1;
+  uint32_t wide[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) wide[i] = 0;
+  const int bitpos = COA_WCOMB_W * j;
+  const uint64_t mm = (uint64_t)m << (bitpos & 31);
+  for (int i = 0; i < 16; i++) {
+    if (i == (bitpos >> 5)) wide[i] = (uint32_t)mm;
+    if (i == (bitpos >> 5) + 1) wide[i] = (uint32_t)(mm >> 32);
+  }
+  sc x;
+  sc_reduce512(x, wide);
+  uint32_t e[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) e[i] = x.v[i];
+  add_const_word(e, 0x80808080u);
+  ge_p3 acc3;
+  ge_p1p1 t;
+  ge_p3_identity(acc3);
+#pragma unroll 1
+  for (int k = 0; k < 32; k++) {
+    const int ek = (int)take_low_byte(e) - 128;
+    ge_niels qb;
+    comb_select(qb, comb, k, ek);
+    ge_madd(t, acc3, qb);
+    ge_p1p1_to_p3(acc3, t);
+  }
+  fe zi, xx, yy, xy, d2, n0, n1, n2;
+  fe_invert(zi, acc3.Z);
+  fe_mul(xx, acc3.X, zi);
+  fe_mul(yy, acc3.Y, zi);
+  fe_mul(xy, xx, yy);
+  fe_const_d2(d2);
+  fe_add(n0, yy, xx);
+  fe_sub(n1, yy, xx);
+  fe_mul(n2, xy, d2);
+  fe_canon(n0, n0);
+  fe_canon(n1, n1);
+  fe_canon(n2, n2);
+  uint4* o = reinterpret_cast<uint4*>(wcomb + id * 24);
+  o[0] = make_uint4(n0.v[0], n0.v[1], n0.v[2], n0.v[3]);
+  o[1] = make_uint4(n0.v[4], n0.v[5], n0.v[6], n0.v[7]);
+  o[2] = make_uint4(n1.v[0], n1.v[1], n1.v[2], n1.v[3]);
+  o[3] = make_uint4(n1.v[4], n1.v[5], n1.v[6], n1.v[7]);
+  o[4] = make_uint4(n2.v[0], n2.v[1], n2.v[2], n2.v[3]);
+  o[5] = make_uint4(n2.v[4], n2.v[5], n2.v[6], n2.v[7]);
+}
+
+namespace {
+COA_DEV void niels_to_p3(ge_p3& r, const ge_niels& q) {  // affine Niels -> extended (Z = 1)
+  fe two_y, two_x, half;
+  fe_add(two_y, q.yplusx, q.yminusx);
+  fe_sub(two_x, q.yplusx, q.yminusx);
+  // 1/2 mod p = (p + 1) / 2
+  fe_set(half, 0);
+  half.v[0] = 0xfffffff7u;
+  for (int i = 1; i < 7; i++) half.v[i] = 0xffffffffu;
+  half.v[7] = 0x3fffffffu;
+  fe_mul(r.X, two_x, half);
+  fe_mul(r.Y, two_y, half);
+  fe_set(r.Z, 1);
+  fe_mul(r.T, r.X, r.Y);
+}
+COA_DEV bool niels_eq_p3(const ge_niels& q, const ge_p3& p) {  // same point (p projective)?
+  ge_p3 a;
+  niels_to_p3(a, q);
+  ge_p2 a2;
+  ge_p3_to_p2(a2, a);
+  return ge_p2_eq_p3(a2, p);
+}
+}  // namespace
+
+// Whole-table consistency of the wide comb, independent of how it was built:
+// entry(j, m) == entry(j, m-1) + entry(j, 1) for m >= 2, entry(j, 1) ==
+// [2^W] entry(j-1, 1) for j >= 1, entry(0, 1) == B, and every entry's
+// xy2d == 2d x y.  By induction every entry is m * 2^(W j) * B.  Each
+// thread checks one entry and counts failures into *bad.
+__global__ void __launch_bounds__(256) k_check_wcomb(const uint32_t* __restrict__ wcomb, uint32_t* __restrict__ bad) {
+  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= COA_WCOMB_ENTRIES) return;
+  const int j = (int)(id / COA_WCOMB_MAG);
+  const uint32_t m = (uint32_t)(id % COA_WCOMB_MAG) + 1;
+  uint32_t w[24];
+  ge_niels q;
+  wcomb_load(w, wcomb, j, (int)m);
+  wcomb_apply(q, w, 1);
+  bool ok = true;
+  {  // internal consistency: xy2d == 2d x y, coordinates canonical
+    ge_p3 a;
+    niels_to_p3(a, q);
+    fe d2, want, c;
+    fe_const_d2(d2);
+    fe_mul(want, a.T, d2);
+    fe_canon(want, want);
+    ok = ok && fe_eq(want, q.xy2d);
+    // stored encodings are canonical (< p), word for word
+    const fe* co[3] = {&q.yplusx, &q.yminusx, &q.xy2d};
+    for (int k = 0; k < 3; k++) {
+      fe_canon(c, *co[k]);
+      for (int i = 0; i < 8; i++) ok = ok && c.v[i] == co[k]->v[i];
+    }
+  }
+  ge_p3 expect;
+  ge_p1p1 t;
+  if (m >= 2) {
+    ge_niels prev, one;
+    wcomb_load(w, wcomb, j, (int)m - 1);
+    wcomb_apply(prev, w, 1);
+    wcomb_load(w, wcomb, j, 1);
+    wcomb_apply(one, w, 1);
+    ge_p3 pp;
+    niels_to_p3(pp, prev);
+    ge_madd(t, pp, one);
+    ge_p1p1_to_p3(expect, t);
+  } else if (j >= 1) {
+    ge_niels base;
+    wcomb_load(w, wcomb, j - 1, 1);
+    wcomb_apply(base, w, 1);
+    ge_p3 pp;
+    niels_to_p3(pp, base);
+    ge_p2 a2;
+    ge_p3_to_p2(a2, pp);
+    for (int k = 0; k < COA_WCOMB_W; k++) {
+      ge_p2_dbl(t, a2);
+      ge_p1p1_to_p2(a2, t);
+    }
+    ge_p1p1_to_p3(expect, t);
+  } else {
+    ge_basepoint(expect);
+  }
+  ok = ok && niels_eq_p3(q, expect);
+  if (!ok) atomicAdd(bad, 1u);
+}
+
 // (k, s) -> record {c'[8], d'[8], e[8], meta, pad[7]}: c' = c + 0x88..8,
 // d' = |d| + 0x88..8 (signed radix-16 recodings), meta = H | (d < 0) << 31.
 __global__ void __launch_bounds__(256) k_halve(const uint32_t* __restrict__ kbuf, const uint8_t* __restrict__ sigs,
@@ -403,7 +543,8 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_halved(const uint8_t* __r
                                                           const uint8_t* __restrict__ sigs,
                                                           const uint32_t* __restrict__ rec, uint32_t n,
                                                           uint8_t* __restrict__ verdicts, uint32_t* __restrict__ scr,
-                                                          const uint32_t* __restrict__ comb) {
+                                                          const uint32_t* __restrict__ comb,
+                                                          const uint32_t* __restrict__ wcomb) {
   const uint32_t lanes = gridDim.x * blockDim.x;
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   // grid-stride with a wave-uniform trip count (wave_max below needs all lanes)
@@ -489,18 +630,40 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_halved(const uint8_t* __r
         if (pos != 0) ge_p1p1_to_p2(acc2, t);
       }
       ge_p1p1_to_p3(acc3, t);
-      // [e]B by the doubling-free comb
       uint32_t e[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) e[j] = myrec[16 + j];
-      add_const_word(e, 0x80808080u);
+      if (wcomb) {
+        // [e]B from the wide HBM comb: 13 mixed additions; entry j+1 is
+        // loaded while addition j runs (one wave per SIMD hides nothing else)
+        uint32_t r[9], cur[24], nxt[24];
+        wcomb_recode(r, e);
+        int d = wcomb_take_digit(r);
+        wcomb_load(cur, wcomb, 0, d);
 #pragma unroll 1
-      for (int j = 0; j < 32; j++) {
-        const int ej = (int)take_low_byte(e) - 128;
-        ge_niels qb;
-        comb_select(qb, comb, j, ej);
-        ge_madd(t, acc3, qb);
-        ge_p1p1_to_p3(acc3, t);
+        for (int j = 0; j < COA_WCOMB_POS; j++) {
+          const int jn = j + 1 < COA_WCOMB_POS ? j + 1 : j;
+          const int dn = wcomb_take_digit(r);
+          wcomb_load(nxt, wcomb, jn, dn);
+          ge_niels qb;
+          wcomb_apply(qb, cur, d);
+          ge_madd(t, acc3, qb);
+          ge_p1p1_to_p3(acc3, t);
+          d = dn;
+#pragma unroll
+          for (int i = 0; i < 24; i++) cur[i] = nxt[i];
+        }
+      } else {
+        // [e]B by the doubling-free radix-256 comb
+        add_const_word(e, 0x80808080u);
+#pragma unroll 1
+        for (int j = 0; j < 32; j++) {
+          const int ej = (int)take_low_byte(e) - 128;
+          ge_niels qb;
+          comb_select(qb, comb, j, ej);
+          ge_madd(t, acc3, qb);
+          ge_p1p1_to_p3(acc3, t);
+        }
       }
       ge_p2 q2;
       ge_p3_to_p2(q2, acc3);
@@ -524,19 +687,28 @@ hipError_t coa_launch_halve(const uint32_t* kbuf, const uint8_t* sigs, uint32_t 
   return hipGetLastError();
 }
 
+hipError_t coa_launch_build_wcomb(uint32_t* wcomb, const uint32_t* comb, hipStream_t s) {
+  hipLaunchKernelGGL(k_build_wcomb, dim3((uint32_t)((COA_WCOMB_ENTRIES + 255) / 256)), dim3(256), 0, s, wcomb, comb);
+  return hipGetLastError();
+}
+hipError_t coa_launch_check_wcomb(const uint32_t* wcomb, uint32_t* bad, hipStream_t s) {
+  hipLaunchKernelGGL(k_check_wcomb, dim3((uint32_t)((COA_WCOMB_ENTRIES + 255) / 256)), dim3(256), 0, s, wcomb, bad);
+  return hipGetLastError();
+}
+
 // waves: register bound of the instance (2 = 256 VGPRs, 3 = 168 with spills)
 hipError_t coa_launch_verify_halved(const uint8_t* pks, const uint8_t* sigs, const uint32_t* rec, uint32_t n,
                                     uint8_t* verdicts, uint32_t* scratch, uint32_t scratch_lanes,
-                                    const uint32_t* comb, int waves, hipStream_t s) {
+                                    const uint32_t* comb, const uint32_t* wcomb, int waves, hipStream_t s) {
   if (n == 0) return hipSuccess;
   uint64_t blocks = ((uint64_t)n + COA_VERIFY_BLOCK - 1) / COA_VERIFY_BLOCK;
   const uint64_t maxb = scratch_lanes / COA_VERIFY_BLOCK;
   if (blocks > maxb) blocks = maxb;
   if (waves == 3)
     hipLaunchKernelGGL(k_verify_halved<3>, dim3((uint32_t)blocks), dim3(COA_VERIFY_BLOCK), 0, s, pks, sigs, rec, n,
-                       verdicts, scratch, comb);
+                       verdicts, scratch, comb, wcomb);
   else
     hipLaunchKernelGGL(k_verify_halved<2>, dim3((uint32_t)blocks), dim3(COA_VERIFY_BLOCK), 0, s, pks, sigs, rec, n,
-                       verdicts, scratch, comb);
+                       verdicts, scratch, comb, wcomb);
   return hipGetLastError();
 }

@@ -95,6 +95,7 @@ struct Dev {
   hipStream_t stream = nullptr;
   uint32_t* btab = nullptr;  // 128 x (j+1)B, radix-256 fixed-base table (12 KiB)
   uint32_t* comb = nullptr;  // 32 x 128 x (v+1)256^j B comb for k_verify_halved (384 KiB)
+  uint32_t* wcomb = nullptr;  // wide B comb, COA_WCOMB_POS x 2^(W-1) entries (654 MB at W = 20)
   DevBuf msgs, pks, sigs, kbuf, rec, verdicts, scratch, aux, rbuf, seeds, offs, data, out, idx, zs, terms, flags;
   // committee key cache (f2): sorted keys, flags, one comb of -A per key
   DevBuf ckeys, kflags, ktabs, cert, cscr;
@@ -113,6 +114,13 @@ bool full_impl() {
   const char* impl = getenv("COA_VERIFY_IMPL");
   return impl && std::string(impl) == "full";
 }
+bool env_is(const char* name, const char* value) {
+  const char* v = getenv(name);
+  return v && std::string(v) == value;
+}
+// The wide comb is built at device open unless COA_WCOMB=0 then; COA_WCOMB=0
+// at call time selects the radix-256 comb (A/B runs; read per call).
+const uint32_t* wcomb_of(const Dev& d) { return env_is("COA_WCOMB", "0") ? nullptr : d.wcomb; }
 // COA_VERIFY_WAVES=3 selects the 168-VGPR instance of k_verify_halved.
 int verify_waves() {
   const char* w = getenv("COA_VERIFY_WAVES");
@@ -132,6 +140,10 @@ int open_device(int d) {
   HIP_TRY(coa_launch_build_btable(dev->btab, dev->stream));
   HIP_TRY(hipMalloc(&dev->comb, COA_COMB_DWORDS * sizeof(uint32_t)));
   HIP_TRY(coa_launch_build_comb(dev->comb, dev->btab, dev->stream));
+  if (!env_is("COA_WCOMB", "0")) {
+    HIP_TRY(hipMalloc(&dev->wcomb, COA_WCOMB_DWORDS * sizeof(uint32_t)));
+    HIP_TRY(coa_launch_build_wcomb(dev->wcomb, dev->comb, dev->stream));
+  }
   HIP_TRY(hipStreamSynchronize(dev->stream));
   g_devs.push_back(std::move(dev));
   return COA_OK;
@@ -235,7 +247,7 @@ int enqueue_verify_prehashed(Dev& d, const uint8_t* d_pks, const uint8_t* d_sigs
   }
   HIP_TRY(coa_launch_halve(d_k, d_sigs, (uint32_t)n, w.rec, s));
   HIP_TRY(coa_launch_verify_halved(d_pks, d_sigs, w.rec, (uint32_t)n, d_verdicts, w.scratch, lanes, d.comb,
-                                   verify_waves(), s));
+                                   wcomb_of(d), verify_waves(), s));
   return COA_OK;
 }
 
@@ -582,6 +594,7 @@ int coa_shutdown(void) {
     d->nkeys = 0;
     if (d->btab) (void)hipFree(d->btab);
     if (d->comb) (void)hipFree(d->comb);
+    if (d->wcomb) (void)hipFree(d->wcomb);
     (void)hipStreamDestroy(d->stream);
   }
   g_devs.clear();
@@ -593,6 +606,29 @@ int coa_device_count(void) {
   const int r = ensure_init();
   if (r != COA_OK) return r;
   return (int)g_devs.size();
+}
+
+int coa_self_test(int device, uint64_t* bad_entries) {
+  if (!bad_entries) return fail(COA_EINVAL, "null output");
+  *bad_entries = 0;
+  const int r = ensure_init();
+  if (r != COA_OK) return r;
+  Dev* d = dev_by_id(device);
+  if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
+  std::lock_guard<std::mutex> l(d->mu);
+  if (!d->wcomb) return COA_OK;
+  HIP_TRY(hipSetDevice(d->id));
+  uint32_t* dbad = nullptr;
+  HIP_TRY(hipMalloc(&dbad, sizeof(uint32_t)));
+  uint32_t hbad = 0;
+  hipError_t e = hipMemsetAsync(dbad, 0, sizeof(uint32_t), d->stream);
+  if (e == hipSuccess) e = coa_launch_check_wcomb(d->wcomb, dbad, d->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(&hbad, dbad, sizeof(uint32_t), hipMemcpyDeviceToHost, d->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+  (void)hipFree(dbad);
+  HIP_TRY(e);
+  *bad_entries = hbad;
+  return COA_OK;
 }
 
 size_t coa_verify_workspace_bytes(size_t n) { return ws_bytes(n); }

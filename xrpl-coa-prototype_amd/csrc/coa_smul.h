@@ -4,6 +4,7 @@
 #pragma once
 #include "coa_fe.h"
 #include "coa_ge.h"
+#include "coa_halved.h"
 
 // ---------------------------------------------------------------------------
 // Fixed-base table: entry j (0..127) = (j+1)·B as affine Niels
@@ -119,6 +120,63 @@ COA_DEV void comb_select(ge_niels& q, const uint32_t* __restrict__ comb, int j, 
   }
   if (m == 0) ge_niels_identity(q);
   ge_niels_cneg(q, e < 0);
+}
+
+// ---------------------------------------------------------------------------
+// Wide B comb, HBM resident: COA_WCOMB_POS positions x 2^(W-1) magnitudes,
+// entry (j, m-1) = m * 2^(W j) * B as canonical affine Niels (24 dwords).
+// A scalar x < 2^253 is recoded as the W-bit digits of
+// x + sum_j 2^(W j + W - 1) minus 2^(W-1), so [x]B is COA_WCOMB_POS mixed
+// additions instead of the 32 of the radix-256 comb above.  W = 20: 13
+// positions, 6.8 M entries, 654 MB of the 288 GB HBM.
+// ---------------------------------------------------------------------------
+static_assert(COA_WCOMB_W * COA_WCOMB_POS >= 255 && COA_WCOMB_W * COA_WCOMB_POS <= 288, "wide comb recoding");
+
+// x (8 words, < 2^253) -> 9 words of x + sum_j 2^(W j + W - 1): the offsets
+// are single distinct bits, so the constant is a bit pattern.
+COA_DEV void wcomb_recode(uint32_t* r, const uint32_t* x) {
+  uint32_t c[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < COA_WCOMB_POS; j++) {
+    const int b = COA_WCOMB_W * j + COA_WCOMB_W - 1;
+    c[b >> 5] |= 1u << (b & 31);
+  }
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r[i] = addc32(x[i], c[i], cy, cy);
+  r[8] = c[8] + cy;
+}
+// Low W bits of r as a signed digit, then r >>= W.
+COA_DEV int wcomb_take_digit(uint32_t* r) {
+  const int d = (int)(r[0] & ((1u << COA_WCOMB_W) - 1)) - (int)COA_WCOMB_MAG;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r[i] = __builtin_amdgcn_alignbit(r[i + 1], r[i], COA_WCOMB_W);
+  r[8] >>= COA_WCOMB_W;
+  return d;
+}
+// Raw 24 words of entry (j, |d|) (entry (j, 0) for d == 0; ignored then).
+COA_DEV void wcomb_load(uint32_t* w, const uint32_t* __restrict__ tab, int j, int d) {
+  const uint32_t m = (uint32_t)(d < 0 ? -d : d);
+  const uint64_t idx = (uint64_t)j * COA_WCOMB_MAG + (m ? m - 1 : 0);
+  const uint4* src = reinterpret_cast<const uint4*>(tab + idx * 24);
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    const uint4 v = src[i];
+    w[4 * i] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+}
+COA_DEV void wcomb_apply(ge_niels& q, const uint32_t* w, int d) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    q.yplusx.v[i] = w[i];
+    q.yminusx.v[i] = w[8 + i];
+    q.xy2d.v[i] = w[16 + i];
+  }
+  if (d == 0) ge_niels_identity(q);
+  ge_niels_cneg(q, d < 0);
 }
 
 COA_DEV uint32_t take_low_byte(uint32_t* x) {
