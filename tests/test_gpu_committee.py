@@ -299,18 +299,22 @@ def world(engine):
     return World(engine)
 
 
-@pytest.fixture(params=["64", "1/T0", "1/T256", "1/T512"])
+@pytest.fixture(params=["64", "1/T0", "1/T256", "1/T512", "1/T0/narrow"])
 def lanes(request):
     """Latency kernel (64) and throughput kernel with one signature per lane
     (T0 = default grid) or a grid of 256 / 512 lanes, so each lane shares one
-    inversion among several signatures (P compared with R's encoding)."""
-    lanes_, _, t = request.param.partition("/T")
-    os.environ["COA_CERT_LANES"] = lanes_
-    if t and t != "0":
-        os.environ["COA_CERT_LANES_TOTAL"] = t
-    yield int(lanes_)
+    inversion among several signatures (P compared with R's encoding).
+    `narrow`: [s]B from the radix-256 comb instead of the wide HBM comb."""
+    parts = request.param.split("/")
+    os.environ["COA_CERT_LANES"] = parts[0]
+    if len(parts) > 1 and parts[1] != "T0":
+        os.environ["COA_CERT_LANES_TOTAL"] = parts[1][1:]
+    if "narrow" in parts:
+        os.environ["COA_WCOMB"] = "0"
+    yield int(parts[0])
     del os.environ["COA_CERT_LANES"]
     os.environ.pop("COA_CERT_LANES_TOTAL", None)
+    os.environ.pop("COA_WCOMB", None)
 
 
 def test_fused_certificates_adversarial(engine, world, lanes):

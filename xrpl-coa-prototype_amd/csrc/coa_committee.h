@@ -38,6 +38,7 @@ struct CertArgs {
   const uint32_t* ktabs;        // [nk][COA_KEY_TAB_DWORDS] comb of -A per key
   uint32_t nk;
   const uint32_t* comb;         // B comb (coa_halved.h)
+  const uint32_t* wcomb;        // wide B comb (coa_smul.h) or null
   uint32_t* status;             // [nc], zeroed by the caller
 };
 

@@ -271,8 +271,15 @@ COA_DEV void job_comb(const CertArgs& a, uint32_t job, ge_p3& P, uint32_t& pre, 
   add_const_word(kd, 0x80808080u);
   const uint32_t* ktab = a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS;
   ge_p1p1 t;
+  // [s]B: 13 additions from the wide HBM comb when it is built, else the 32
+  // byte terms of the radix-256 comb (an s >= l only reaches Err verdicts)
+  int term = 0;
+  if (a.wcomb) {
+    wcomb_accumulate(P, sw, a.wcomb);
+    term = 32;
+  }
 #pragma unroll 1
-  for (int term = 0; term < 64; term++) {
+  for (; term < 64; term++) {
     const bool isb = term < 32;
     const int j = term & 31;
     const int e = (int)byte_of(isb ? sd : kd, j) - 128;

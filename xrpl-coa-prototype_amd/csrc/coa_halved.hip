@@ -634,25 +634,8 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_halved(const uint8_t* __r
 #pragma unroll
       for (int j = 0; j < 8; j++) e[j] = myrec[16 + j];
       if (wcomb) {
-        // [e]B from the wide HBM comb: 13 mixed additions; entry j+1 is
-        // loaded while addition j runs (one wave per SIMD hides nothing else)
-        uint32_t r[9], cur[24], nxt[24];
-        wcomb_recode(r, e);
-        int d = wcomb_take_digit(r);
-        wcomb_load(cur, wcomb, 0, d);
-#pragma unroll 1
-        for (int j = 0; j < COA_WCOMB_POS; j++) {
-          const int jn = j + 1 < COA_WCOMB_POS ? j + 1 : j;
-          const int dn = wcomb_take_digit(r);
-          wcomb_load(nxt, wcomb, jn, dn);
-          ge_niels qb;
-          wcomb_apply(qb, cur, d);
-          ge_madd(t, acc3, qb);
-          ge_p1p1_to_p3(acc3, t);
-          d = dn;
-#pragma unroll
-          for (int i = 0; i < 24; i++) cur[i] = nxt[i];
-        }
+        // [e]B from the wide HBM comb: 13 mixed additions
+        wcomb_accumulate(acc3, e, wcomb);
       } else {
         // [e]B by the doubling-free radix-256 comb
         add_const_word(e, 0x80808080u);

@@ -428,6 +428,7 @@ CertArgs cert_args(Dev& d, uint8_t* base, const CertPack& p, size_t nc, size_t n
   a.ktabs = d.ktabs.as<uint32_t>();
   a.nk = d.nkeys;
   a.comb = d.comb;
+  a.wcomb = wcomb_of(d);
   a.status = reinterpret_cast<uint32_t*>(base + p.status);
   return a;
 }
@@ -968,6 +969,7 @@ int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data,
   a.ktabs = d->ktabs.as<uint32_t>();
   a.nk = d->nkeys;
   a.comb = d->comb;
+  a.wcomb = wcomb_of(*d);
   a.status = d_status;
   const int lanes = cert_lanes(n + n_votes);
   HIP_TRY(hipMemsetAsync(d_status, 0, n * 4, s));

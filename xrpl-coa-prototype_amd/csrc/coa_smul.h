@@ -179,6 +179,29 @@ COA_DEV void wcomb_apply(ge_niels& q, const uint32_t* w, int d) {
   ge_niels_cneg(q, d < 0);
 }
 
+// acc += [x]B from the wide comb (x < 2^253; a larger x gives some point,
+// never an out-of-range entry).  Entry j+1 is loaded while addition j runs.
+COA_DEV void wcomb_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __restrict__ tab) {
+  uint32_t r[9], cur[24], nxt[24];
+  wcomb_recode(r, x);
+  int d = wcomb_take_digit(r);
+  wcomb_load(cur, tab, 0, d);
+  ge_p1p1 t;
+#pragma unroll 1
+  for (int j = 0; j < COA_WCOMB_POS; j++) {
+    const int jn = j + 1 < COA_WCOMB_POS ? j + 1 : j;
+    const int dn = wcomb_take_digit(r);
+    wcomb_load(nxt, tab, jn, dn);
+    ge_niels q;
+    wcomb_apply(q, cur, d);
+    ge_madd(t, acc, q);
+    ge_p1p1_to_p3(acc, t);
+    d = dn;
+#pragma unroll
+    for (int i = 0; i < 24; i++) cur[i] = nxt[i];
+  }
+}
+
 COA_DEV uint32_t take_low_byte(uint32_t* x) {
   const uint32_t lo = x[0] & 0xffu;
 #pragma unroll
