@@ -6,14 +6,16 @@ verify (crypto::Signature::verify == dalek verify_strict).  Inputs are
 synthesised with the reference's byte formats (workloads.py), signed on the
 device, and are resident in HBM before the timed region.
 
-A step = one pass of the hot path over the batch: the challenge kernel
-(k = SHA-512(R||A||M) mod l) and the verify kernel.  With N GPUs every rank
+A step = one pass of the hot path over the batch: one
+coa_ed25519_verify_strict_many_device call (k = SHA-512(R||A||M) mod l, the
+halving, decompressions and tables in k_pre_halve, the joint pass in
+k_verify_main).  With N GPUs every rank
 verifies its own 65,536 triples (weak scaling, contiguous index ranges, no
 data-path collective); value = all ranks' verifications / max-over-ranks time.
 
 Also reported:
-  roofline      the dominant kernel pair (k_halve + k_verify_halved) against
-                the INT32 VALU issue peak; algorithmic work = the dalek
+  roofline      the verify call (k_pre_halve + k_verify_main) against the
+                INT32 VALU issue peak; algorithmic work = the dalek
                 algorithm's field operation count (2,967 mul+sq per verify,
                 frozen by the instrumented C restatement: oracle/coa_oracle.c)
                 x 200 INT32 ops per field op (SURVEY.md 8(d) cost model); its
@@ -94,10 +96,31 @@ def cpu_baseline(msgs, pks, sigs, seconds):
                   f"{threads} threads, {el:.1f} s wall ({el * threads:.1f} thread-s)",
         "single_thread_value": 2048 / st,
     }
+    out["host"] = host_cpu()
     sodium = libsodium_baseline(m, p, s, threads, min(seconds, 1.0))
     if sodium:
         out["second_reference"] = sodium
     return out
+
+
+def host_cpu():
+    """CPU model and core counts of the box the baseline ran on (SURVEY 8(d):
+    report nproc and the CPU model).  `usable_cpus` is this process's
+    affinity set; `nproc` the whole machine."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
 
 
 def libsodium_baseline(m, p, s, threads, seconds):
@@ -330,7 +353,6 @@ def main():
     pks = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     sigs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
     coa_crypto.sign_many_device(local, seeds, msgs, pks, sigs)
-    kbuf = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     verdicts = torch.ones(n, dtype=torch.uint8, device=dev)
     ws = torch.empty(coa_crypto.verify_workspace_bytes(n), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
@@ -341,14 +363,13 @@ def main():
     torch.cuda.set_stream(stream)
 
     def step(evs=None):
+        # one Signature::verify call over the batch: challenge hash, halving,
+        # [e]B, decompressions, tables and the joint Horner pass
         if evs is not None:
             evs[0].record(stream)
-        coa_crypto.challenge_many_device(local, msgs, pks, sigs, kbuf, stream)
+        coa_crypto.verify_strict_many_device(local, msgs, pks, sigs, verdicts, ws, stream)
         if evs is not None:
             evs[1].record(stream)
-        coa_crypto.verify_prehashed_many_device(local, kbuf, pks, sigs, verdicts, ws, stream)
-        if evs is not None:
-            evs[2].record(stream)
 
     for _ in range(args.warmup):
         step()
@@ -357,7 +378,7 @@ def main():
     if not ok:
         raise SystemExit("engine rejected valid benchmark signatures")
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -369,8 +390,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = sharding.max_over_ranks(elapsed, dist, dev)
-    hram_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-    verify_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    verify_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     ok = ok and int(verdicts.sum().item()) == 0
 
     total = n * world * args.steps
@@ -394,7 +414,7 @@ def main():
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary:
         threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1, 64))
-        del kbuf, ws
+        del ws
         torch.cuda.empty_cache()
         secondary = {
             "c4_sha512": c4_sha512(local, dev, stream, [int(x) for x in args.c4_batches.split(",") if x], 2,
@@ -421,11 +441,11 @@ def main():
             "config": {"workload": "C2: 65,536 independent (32 B digest, pk, sig) triples per GPU, all valid, "
                                    "per-signature verify_strict",
                        "triples_per_gpu": n, "parallelism": f"index-range shards x{world}"},
-            "kernel_ms": {"k_hram": round(hram_ms, 4), "verify_stage": round(verify_ms, 4)},
+            "kernel_ms": {"verify_call": round(verify_ms, 4)},
             "verdicts_ok": ok,
             "roofline": {"bound": "valu-int32", "achieved": round(achieved, 3), "peak": round(PEAK_INT32_TOPS, 2),
                          "unit": "TOPS", "frac": round(achieved / PEAK_INT32_TOPS, 4), "traffic": traffic,
-                         "kernel": "k_halve+k_verify_halved (prehashed verify stage)",
+                         "kernel": "k_pre_halve+k_verify_main (the whole verify call, HIP events on its stream)",
                          "alg_int32_ops_per_verify": ALG_INT32_OPS_PER_VERIFY},
             "cpu_baseline": cpu,
             "secondary": secondary,

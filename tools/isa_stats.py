@@ -27,7 +27,10 @@ def stats(src, defines=()):
     out = {}
     for name in re.findall(r"^(_Z\w+):", s, re.M):
         i = s.index(name + ":")
-        body = s[i:s.index(".Lfunc_end", i)].split("\n")
+        j = s.find(".Lfunc_end", i)
+        if j < 0:
+            continue
+        body = s[i:j].split("\n")
         ins = [l.strip().split()[0] for l in body
                if l.startswith("\t") and l.strip() and not l.startswith("\t.") and not l.startswith("\t;")]
         c = collections.Counter(ins)

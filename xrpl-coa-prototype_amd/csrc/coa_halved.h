@@ -22,6 +22,16 @@ hipError_t coa_launch_halve(const uint32_t* kbuf, const uint8_t* sigs, uint32_t 
 hipError_t coa_launch_verify_halved(const uint8_t* pks, const uint8_t* sigs, const uint32_t* rec, uint32_t n,
                                     uint8_t* verdicts, uint32_t* scratch, uint32_t scratch_lanes,
                                     const uint32_t* comb, const uint32_t* wcomb, int waves, hipStream_t s);
+// Split verification of n <= COA_VERIFY_MAX_LANES items: k_pre_halve
+// (decompressions + slab tables, and k + halving + [e]B, in one two-role
+// launch) then k_verify_main.  k comes from kbuf, or is hashed in-kernel from
+// msgs (msg_len bytes per item, contiguous) when msgs is non-null.
+// flags: n bytes; scratch: n slabs of COA_HALVED_SCRATCH_PER_LANE bytes;
+// ebp: n x 128 bytes to compute [e]B in phase 1, or null for phase 2.
+hipError_t coa_launch_verify_split(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
+                                   const uint32_t* kbuf, uint32_t n, uint32_t* rec, uint8_t* flags,
+                                   uint8_t* verdicts, uint32_t* scratch, uint32_t* ebp, const uint32_t* comb,
+                                   const uint32_t* wcomb, hipStream_t s);
 // wide HBM comb of B (coa_smul.h, COA_WCOMB_*): build from the radix-256
 // comb, and the whole-table consistency check (count of bad entries in *bad,
 // zeroed by the caller)

@@ -26,6 +26,7 @@
 #include "coa_fe.h"
 #include "coa_ge.h"
 #include "coa_sc.h"
+#include "coa_sha512.h"
 #include "coa_smul.h"
 
 namespace {
@@ -497,45 +498,253 @@ __global__ void __launch_bounds__(256) k_check_wcomb(const uint32_t* __restrict_
 
 // (k, s) -> record {c'[8], d'[8], e[8], meta, pad[7]}: c' = c + 0x88..8,
 // d' = |d| + 0x88..8 (signed radix-16 recodings), meta = H | (d < 0) << 31.
+namespace {
+// One signature's halving record from k and s in registers; e = d*s (mod l,
+// negated with d) is also returned for the [e]B term.
+COA_DEV void halve_rec(uint32_t* k, const uint32_t* s, uint32_t i, uint32_t* __restrict__ rec, uint32_t* e_out) {
+  uint32_t c[8], d[8];
+  int cost;
+  bool neg;
+  halve(c, d, cost, neg, k);
+  sc e;
+  sc_mul(e, d, s);  // s may be non-canonical here; the verify kernel rejects those lanes
+  if (neg) {
+    sc en;
+    sc_neg(en, e.v);
+    e = en;
+  }
+  const int H = (cost + 2 + 3) / 4;  // c, d < 2^(4H - 2)
+  // signed radix-16 recoding offset over all 64 nibbles: nibble p of
+  // c + 0x88..8 minus 8 is digit p, and every digit at p >= H is 0
+  add_const_word(c, 0x88888888u);
+  add_const_word(d, 0x88888888u);
+  uint4* o = reinterpret_cast<uint4*>(rec + (uint64_t)i * 32);
+  o[0] = make_uint4(c[0], c[1], c[2], c[3]);
+  o[1] = make_uint4(c[4], c[5], c[6], c[7]);
+  o[2] = make_uint4(d[0], d[1], d[2], d[3]);
+  o[3] = make_uint4(d[4], d[5], d[6], d[7]);
+  o[4] = make_uint4(e.v[0], e.v[1], e.v[2], e.v[3]);
+  o[5] = make_uint4(e.v[4], e.v[5], e.v[6], e.v[7]);
+  o[6] = make_uint4((uint32_t)H | (neg ? 0x80000000u : 0u), 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 8; j++) e_out[j] = e.v[j];
+}
+
+// k_halve's per-signature body: k from kbuf.
+COA_DEV void halve_one(const uint32_t* __restrict__ kbuf, const uint8_t* __restrict__ sigs, uint32_t i,
+                       uint32_t* __restrict__ rec) {
+  uint32_t k[8], s[8], e[8];
+  const uint4* kq = reinterpret_cast<const uint4*>(kbuf + (uint64_t)i * 8);
+  const uint4* sq = reinterpret_cast<const uint4*>(sigs + (uint64_t)i * 64 + 32);
+  uint4 v0 = kq[0], v1 = kq[1];
+  k[0] = v0.x; k[1] = v0.y; k[2] = v0.z; k[3] = v0.w;
+  k[4] = v1.x; k[5] = v1.y; k[6] = v1.z; k[7] = v1.w;
+  v0 = sq[0];
+  v1 = sq[1];
+  s[0] = v0.x; s[1] = v0.y; s[2] = v0.z; s[3] = v0.w;
+  s[4] = v1.x; s[5] = v1.y; s[6] = v1.z; s[7] = v1.w;
+  halve_rec(k, s, i, rec, e);
+}
+
+COA_DEV void load8_u4(uint32_t* dst, const void* src) {
+  const uint4* q = reinterpret_cast<const uint4*>(src);
+  const uint4 a = q[0], b = q[1];
+  dst[0] = a.x; dst[1] = a.y; dst[2] = a.z; dst[3] = a.w;
+  dst[4] = b.x; dst[5] = b.y; dst[6] = b.z; dst[7] = b.w;
+}
+
+// The checks that do not need k (the "pre" role of k_pre_halve): s < l, A and
+// R decompress (dalek rules), neither is small order; then the tables
+// j*(-A) (tab 0) and j*(-R) (tab 1), j = 1..8, in slab i.  Returns ok.
+COA_DEV bool pre_one(const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs, uint32_t i,
+                     uint32_t* __restrict__ scr) {
+  uint32_t aw[8], rw[8], sw[8];
+  load8_u4(aw, pks + (uint64_t)i * 32);
+  load8_u4(rw, sigs + (uint64_t)i * 64);
+  load8_u4(sw, sigs + (uint64_t)i * 64 + 32);
+  bool ok = sc_is_canonical(sw);
+#pragma unroll 1
+  for (int which = 0; which < 2; which++) {
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[j] = which ? rw[j] : aw[j];
+    ge_p3 Q;
+    const bool dec = ge_decompress(Q, w);
+    const bool small = ge_is_small_order(Q);
+    ok = ok && dec && !small;
+    fe_neg(Q.X, Q.X);
+    fe_neg(Q.T, Q.T);
+    // A's table may be built for an item whose R then fails: flags[i] = 0
+    // keeps k_verify_main from reading it
+    if (ok) tab2_build(scr, i, which, Q);
+  }
+  return ok;
+}
+}  // namespace
+
 __global__ void __launch_bounds__(256) k_halve(const uint32_t* __restrict__ kbuf, const uint8_t* __restrict__ sigs,
                                                uint32_t n, uint32_t* __restrict__ rec) {
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    uint32_t k[8], s[8];
-    const uint4* kq = reinterpret_cast<const uint4*>(kbuf + (uint64_t)i * 8);
-    const uint4* sq = reinterpret_cast<const uint4*>(sigs + (uint64_t)i * 64 + 32);
-    uint4 v0 = kq[0], v1 = kq[1];
-    k[0] = v0.x; k[1] = v0.y; k[2] = v0.z; k[3] = v0.w;
-    k[4] = v1.x; k[5] = v1.y; k[6] = v1.z; k[7] = v1.w;
-    v0 = sq[0];
-    v1 = sq[1];
-    s[0] = v0.x; s[1] = v0.y; s[2] = v0.z; s[3] = v0.w;
-    s[4] = v1.x; s[5] = v1.y; s[6] = v1.z; s[7] = v1.w;
-    uint32_t c[8], d[8];
-    int cost;
-    bool neg;
-    halve(c, d, cost, neg, k);
-    sc e;
-    sc_mul(e, d, s);  // s may be non-canonical here; the verify kernel rejects those lanes
-    if (neg) {
-      sc en;
-      sc_neg(en, e.v);
-      e = en;
-    }
-    const int H = (cost + 2 + 3) / 4;  // c, d < 2^(4H - 2)
-    // signed radix-16 recoding offset over all 64 nibbles: nibble p of
-    // c + 0x88..8 minus 8 is digit p, and every digit at p >= H is 0
-    add_const_word(c, 0x88888888u);
-    add_const_word(d, 0x88888888u);
-    uint4* o = reinterpret_cast<uint4*>(rec + (uint64_t)i * 32);
-    o[0] = make_uint4(c[0], c[1], c[2], c[3]);
-    o[1] = make_uint4(c[4], c[5], c[6], c[7]);
-    o[2] = make_uint4(d[0], d[1], d[2], d[3]);
-    o[3] = make_uint4(d[4], d[5], d[6], d[7]);
-    o[4] = make_uint4(e.v[0], e.v[1], e.v[2], e.v[3]);
-    o[5] = make_uint4(e.v[4], e.v[5], e.v[6], e.v[7]);
-    o[6] = make_uint4((uint32_t)H | (neg ? 0x80000000u : 0u), 0, 0, 0);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) halve_one(kbuf, sigs, i, rec);
+}
+
+// Split verification, phase 1 (one launch, two roles): blocks below
+// pre_blocks run pre_one for item blockIdx*256 + t; the others, for item
+// (blockIdx - pre_blocks)*256 + t, take k (from kbuf, or hashed here as
+// SHA-512(R || A || M) mod l when msgs is set), the halving record, and [e]B
+// from the comb, stored in cached form in ebp (32 dwords per item).  Neither
+// role needs the other's output, and at <= 256 VGPRs two waves share each
+// SIMD, so the latency-bound halving (f64 quotient chains) and the hash issue
+// in the gaps of the decompressions.
+template <int WAVES>
+__global__ void __launch_bounds__(256, WAVES) k_pre_halve(const uint8_t* __restrict__ pks,
+                                                      const uint8_t* __restrict__ sigs,
+                                                      const uint8_t* __restrict__ msgs, uint32_t msg_len,
+                                                      int msgs_aligned, const uint32_t* __restrict__ kbuf,
+                                                      uint32_t n, uint32_t* __restrict__ rec,
+                                                      uint8_t* __restrict__ flags, uint32_t* __restrict__ scr,
+                                                      uint32_t* __restrict__ ebp, const uint32_t* __restrict__ comb,
+                                                      const uint32_t* __restrict__ wcomb, uint32_t pre_blocks) {
+  if (blockIdx.x < pre_blocks) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flags[i] = pre_one(pks, sigs, i, scr) ? 1 : 0;
+    return;
   }
+  const uint32_t i = (blockIdx.x - pre_blocks) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8], sw[8], e[8];
+  if (msgs) {
+    coa_sha::Segs sg;
+    sg.p[0] = sigs + (uint64_t)i * 64;
+    sg.len[0] = 32;
+    sg.p[1] = pks + (uint64_t)i * 32;
+    sg.len[1] = 32;
+    sg.p[2] = msgs + (uint64_t)i * msg_len;
+    sg.len[2] = msg_len;
+    uint64_t st[8];
+    coa_sha::hash_segs(st, sg, msgs_aligned != 0);
+    uint32_t h[16];
+    coa_sha::state_to_le_words(h, st);
+    sc kk;
+    sc_reduce512(kk, h);
+#pragma unroll
+    for (int j = 0; j < 8; j++) k[j] = kk.v[j];
+  } else {
+    load8_u4(k, kbuf + (uint64_t)i * 8);
+  }
+  load8_u4(sw, sigs + (uint64_t)i * 64 + 32);
+  halve_rec(k, sw, i, rec, e);
+  if (!ebp) return;  // [e]B left to k_verify_main
+  ge_p3 P;
+  ge_p3_identity(P);
+  if (wcomb) {
+    wcomb_accumulate(P, e, wcomb);
+  } else {
+    ge_p1p1 t;
+    add_const_word(e, 0x80808080u);
+#pragma unroll 1
+    for (int j = 0; j < 32; j++) {
+      const int ej = (int)take_low_byte(e) - 128;
+      ge_niels qb;
+      comb_select(qb, comb, j, ej);
+      ge_madd(t, P, qb);
+      ge_p1p1_to_p3(P, t);
+    }
+  }
+  ge_cached c;
+  ge_p3_to_cached(c, P);
+  const fe* f[4] = {&c.YplusX, &c.YminusX, &c.Z, &c.T2d};
+  uint4* o = reinterpret_cast<uint4*>(ebp + (uint64_t)i * 32);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    o[2 * q] = make_uint4(f[q]->v[0], f[q]->v[1], f[q]->v[2], f[q]->v[3]);
+    o[2 * q + 1] = make_uint4(f[q]->v[4], f[q]->v[5], f[q]->v[6], f[q]->v[7]);
+  }
+}
+
+// Split verification, phase 2: one lane per item (n <= grid), Q = [c](-A) +
+// [|d|](-sign(d) R) from the slab tables (for d < 0 the R digits are negated
+// instead of the table), plus the [e]B point of phase 1.
+template <int WAVES>
+__global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __restrict__ rec,
+                                                        const uint8_t* __restrict__ flags, uint32_t n,
+                                                        uint8_t* __restrict__ verdicts,
+                                                        const uint32_t* __restrict__ scr,
+                                                        const uint32_t* __restrict__ ebp,
+                                                        const uint32_t* __restrict__ comb,
+                                                        const uint32_t* __restrict__ wcomb) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < n;
+  const bool ok = live && flags[i] != 0;
+  const uint32_t* myrec = rec + (uint64_t)(live ? i : 0) * 32;
+  const uint32_t meta = live ? myrec[24] : 0u;
+  const int H = wave_max(ok ? (int)(meta & 0xffu) : 0);
+  const bool dneg = (meta >> 31) != 0;
+  uint8_t verdict = 1;
+  if (ok) {
+    ge_p3 acc3;
+    ge_p2 acc2;
+    ge_p1p1 t;
+    ge_p3_identity(acc3);
+#pragma unroll 1
+    for (int pos = H - 1; pos >= 0; pos--) {
+      const int sh = 4 * (pos & 7);
+      const int dc = (int)((myrec[pos >> 3] >> sh) & 15u) - 8;
+      const int dd = (int)((myrec[8 + (pos >> 3)] >> sh) & 15u) - 8;
+      if (pos != H - 1) {
+#pragma unroll 1
+        for (int k = 0; k < 3; k++) {
+          ge_p2_dbl(t, acc2);
+          ge_p1p1_to_p2(acc2, t);
+        }
+        ge_p2_dbl(t, acc2);
+        ge_p1p1_to_p3(acc3, t);
+      }
+      ge_cached q;
+      tab2_select(q, scr, i, 0, dc);
+      ge_add(t, acc3, q);
+      ge_p1p1_to_p3(acc3, t);
+      tab2_select(q, scr, i, 1, dneg ? -dd : dd);
+      ge_add(t, acc3, q);
+      if (pos != 0) ge_p1p1_to_p2(acc2, t);
+    }
+    ge_p1p1_to_p3(acc3, t);
+    if (!ebp) {  // [e]B here, from the combs
+      uint32_t e[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) e[j] = myrec[16 + j];
+      if (wcomb) {
+        wcomb_accumulate(acc3, e, wcomb);
+      } else {
+        add_const_word(e, 0x80808080u);
+#pragma unroll 1
+        for (int j = 0; j < 32; j++) {
+          const int ej = (int)take_low_byte(e) - 128;
+          ge_niels qb;
+          comb_select(qb, comb, j, ej);
+          ge_madd(t, acc3, qb);
+          ge_p1p1_to_p3(acc3, t);
+        }
+      }
+    } else {
+    // + [e]B, computed by the halving role
+    ge_cached eb;
+    fe* f[4] = {&eb.YplusX, &eb.YminusX, &eb.Z, &eb.T2d};
+    const uint4* src = reinterpret_cast<const uint4*>(ebp + (uint64_t)i * 32);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint4 v0 = src[2 * q], v1 = src[2 * q + 1];
+      f[q]->v[0] = v0.x; f[q]->v[1] = v0.y; f[q]->v[2] = v0.z; f[q]->v[3] = v0.w;
+      f[q]->v[4] = v1.x; f[q]->v[5] = v1.y; f[q]->v[6] = v1.z; f[q]->v[7] = v1.w;
+    }
+    ge_add(t, acc3, eb);
+    ge_p1p1_to_p3(acc3, t);
+    }
+    ge_p2 q2;
+    ge_p3_to_p2(q2, acc3);
+    verdict = ge_p2_is_identity(q2) ? 0 : 1;
+  }
+  if (live) verdicts[i] = verdict;
 }
 
 template <int WAVES>
@@ -676,6 +885,22 @@ hipError_t coa_launch_build_wcomb(uint32_t* wcomb, const uint32_t* comb, hipStre
 }
 hipError_t coa_launch_check_wcomb(const uint32_t* wcomb, uint32_t* bad, hipStream_t s) {
   hipLaunchKernelGGL(k_check_wcomb, dim3((uint32_t)((COA_WCOMB_ENTRIES + 255) / 256)), dim3(256), 0, s, wcomb, bad);
+  return hipGetLastError();
+}
+
+hipError_t coa_launch_verify_split(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
+                                   const uint32_t* kbuf, uint32_t n, uint32_t* rec, uint8_t* flags,
+                                   uint8_t* verdicts, uint32_t* scratch, uint32_t* ebp, const uint32_t* comb,
+                                   const uint32_t* wcomb, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t blocks = (n + COA_VERIFY_BLOCK - 1) / COA_VERIFY_BLOCK;
+  const int aligned = ((msg_len & 3) == 0) && (((uintptr_t)msgs & 3) == 0);
+  hipLaunchKernelGGL(k_pre_halve<2>, dim3(2 * blocks), dim3(COA_VERIFY_BLOCK), 0, s, pks, sigs, msgs, msg_len, aligned,
+                     kbuf, n, rec, flags, scratch, ebp, comb, wcomb, blocks);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_verify_main<2>, dim3(blocks), dim3(COA_VERIFY_BLOCK), 0, s, rec, flags, n, verdicts, scratch,
+                     ebp, comb, wcomb);
   return hipGetLastError();
 }
 

@@ -217,11 +217,13 @@ std::vector<Range> shard(size_t n) {
 struct Workspace {
   uint32_t* k;
   uint32_t* rec;
+  uint8_t* flags;  // split path: pre-check verdict per item
+  uint32_t* ebp;   // split path: [e]B per item (cached form, 128 B)
   uint32_t* scratch;
 };
 size_t ws_bytes(size_t n) {
   n = std::max<size_t>(n, 1);
-  return align_up(n * 32, 256) + align_up(n * COA_HALVE_REC_BYTES, 256) +
+  return align_up(n * 32, 256) + align_up(n * COA_HALVE_REC_BYTES, 256) + align_up(n, 256) + n * 128 +
          (size_t)verify_lanes(n) * COA_HALVED_SCRATCH_PER_LANE;
 }
 Workspace ws_carve(void* base, size_t n) {
@@ -232,8 +234,31 @@ Workspace ws_carve(void* base, size_t n) {
   p += align_up(n * 32, 256);
   w.rec = reinterpret_cast<uint32_t*>(p);
   p += align_up(n * COA_HALVE_REC_BYTES, 256);
+  w.flags = p;
+  p += align_up(n, 256);
+  w.ebp = reinterpret_cast<uint32_t*>(p);
+  p += n * 128;
   w.scratch = reinterpret_cast<uint32_t*>(p);
   return w;
+}
+
+// COA_VERIFY_SPLIT=0 selects the single-kernel k_halve + k_verify_halved path
+// (A/B runs; read per call); the default is the split path.
+bool split_impl() { return !env_is("COA_VERIFY_SPLIT", "0"); }
+
+// Split path in chunks of at most COA_VERIFY_MAX_LANES items (one slab each).
+// k from d_k, or hashed in k_pre_halve from d_msgs (msg_len bytes per item)
+// when d_k is null.
+int enqueue_split(Dev& d, const uint8_t* d_msgs, size_t msg_len, const uint32_t* d_k, const uint8_t* d_pks,
+                  const uint8_t* d_sigs, size_t n, uint8_t* d_verdicts, const Workspace& w, hipStream_t s) {
+  for (size_t lo = 0; lo < n; lo += COA_VERIFY_MAX_LANES) {
+    const uint32_t cnt = (uint32_t)std::min<size_t>(COA_VERIFY_MAX_LANES, n - lo);
+    HIP_TRY(coa_launch_verify_split(d_pks + lo * 32, d_sigs + lo * 64, d_k ? nullptr : d_msgs + lo * msg_len,
+                                    (uint32_t)msg_len, d_k ? d_k + lo * 8 : nullptr, cnt, w.rec + lo * 32,
+                                    w.flags + lo, d_verdicts + lo, w.scratch,
+                                    env_is("COA_SPLIT_EB", "1") ? w.ebp : nullptr, d.comb, wcomb_of(d), s));
+  }
+  return COA_OK;
 }
 
 // Verify with k already in w.k: halved path (k_halve + k_verify_halved) or
@@ -245,6 +270,7 @@ int enqueue_verify_prehashed(Dev& d, const uint8_t* d_pks, const uint8_t* d_sigs
     HIP_TRY(coa_launch_verify_strict(d_pks, d_sigs, d_k, (uint32_t)n, d_verdicts, w.scratch, lanes, d.btab, s));
     return COA_OK;
   }
+  if (split_impl()) return enqueue_split(d, nullptr, 0, d_k, d_pks, d_sigs, n, d_verdicts, w, s);
   HIP_TRY(coa_launch_halve(d_k, d_sigs, (uint32_t)n, w.rec, s));
   HIP_TRY(coa_launch_verify_halved(d_pks, d_sigs, w.rec, (uint32_t)n, d_verdicts, w.scratch, lanes, d.comb,
                                    wcomb_of(d), verify_waves(), s));
@@ -254,6 +280,8 @@ int enqueue_verify_prehashed(Dev& d, const uint8_t* d_pks, const uint8_t* d_sigs
 // Enqueue k = H(R||A||M) then the verification for device-resident inputs.
 int enqueue_verify(Dev& d, const uint8_t* d_msgs, size_t msg_len, const uint8_t* d_pks, const uint8_t* d_sigs,
                    size_t n, uint8_t* d_verdicts, const Workspace& w, hipStream_t s) {
+  if (split_impl() && !full_impl() && !env_is("COA_SPLIT_HRAM", "kernel") && (d_msgs || msg_len == 0))
+    return enqueue_split(d, d_msgs ? d_msgs : d_pks, msg_len, nullptr, d_pks, d_sigs, n, d_verdicts, w, s);
   HIP_TRY(coa_launch_hram(d_msgs, (uint32_t)msg_len, msg_len, nullptr, d_pks, d_sigs, (uint32_t)n, w.k, s));
   return enqueue_verify_prehashed(d, d_pks, d_sigs, n, d_verdicts, w.k, w, s);
 }
