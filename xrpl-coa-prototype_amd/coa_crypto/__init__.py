@@ -32,7 +32,8 @@ import os
 import numpy as np
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "lib", "libcoa_verify.so")
+# COA_VERIFY_LIB overrides the library (A/B runs of two builds in one session)
+LIB_PATH = os.environ.get("COA_VERIFY_LIB") or os.path.join(_PKG, "lib", "libcoa_verify.so")
 
 COA_OK, COA_REJECT = 0, 1
 _ERRORS = {-1: "COA_EINVAL", -2: "COA_ENODEVICE", -3: "COA_EHIP", -4: "COA_ENOMEM"}
