@@ -93,11 +93,12 @@ def test_random_mixed_vs_oracle(engine):
     assert (got == exp).all(), np.nonzero(got != exp)
 
 
-def test_grid_stride_large_n_all_valid(engine):
-    """More items than verify lanes (grid-stride path) -- size-independent
-    property: every honestly generated signature is accepted, and flipping
-    one bit of s in every 7th item is rejected exactly there."""
-    n = 300_000
+@pytest.mark.parametrize("n", [300_000, 2_100_000])
+def test_grid_stride_large_n_all_valid(engine, n):
+    """More items than verify lanes (grid-stride path), and more than one
+    split chunk (2^21 items) -- size-independent property: every honestly
+    generated signature is accepted, and flipping one bit of s in every 7th
+    item is rejected exactly there."""
     rng = np.random.default_rng(1)
     seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
     msgs = rng.integers(0, 256, (n, 32), dtype=np.uint8)

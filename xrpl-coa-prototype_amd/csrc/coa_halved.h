@@ -22,7 +22,10 @@ hipError_t coa_launch_halve(const uint32_t* kbuf, const uint8_t* sigs, uint32_t 
 hipError_t coa_launch_verify_halved(const uint8_t* pks, const uint8_t* sigs, const uint32_t* rec, uint32_t n,
                                     uint8_t* verdicts, uint32_t* scratch, uint32_t scratch_lanes,
                                     const uint32_t* comb, const uint32_t* wcomb, int waves, hipStream_t s);
-// Split verification of n <= COA_VERIFY_MAX_LANES items: k_pre_halve
+// Items per launch pair of the split path (one 2 KiB slab each: 4 GiB of HBM
+// at 2^21, i.e. eight waves per SIMD in k_verify_main).
+#define COA_SPLIT_CHUNK (1u << 21)
+// Split verification of n <= COA_SPLIT_CHUNK items: k_pre_halve
 // (decompressions + slab tables, and k + halving + [e]B, in one two-role
 // launch) then k_verify_main.  k comes from kbuf, or is hashed in-kernel from
 // msgs (msg_len bytes per item, contiguous) when msgs is non-null.

@@ -223,8 +223,11 @@ struct Workspace {
 };
 size_t ws_bytes(size_t n) {
   n = std::max<size_t>(n, 1);
+  // scratch: per-lane slabs (single-kernel path) or per-item slabs of one
+  // split chunk, whichever is larger (the path is chosen per call)
+  const size_t slabs = std::max<size_t>(verify_lanes(n), std::min<size_t>(n, COA_SPLIT_CHUNK));
   return align_up(n * 32, 256) + align_up(n * COA_HALVE_REC_BYTES, 256) + align_up(n, 256) + n * 128 +
-         (size_t)verify_lanes(n) * COA_HALVED_SCRATCH_PER_LANE;
+         slabs * COA_HALVED_SCRATCH_PER_LANE;
 }
 Workspace ws_carve(void* base, size_t n) {
   n = std::max<size_t>(n, 1);
@@ -246,13 +249,13 @@ Workspace ws_carve(void* base, size_t n) {
 // (A/B runs; read per call); the default is the split path.
 bool split_impl() { return !env_is("COA_VERIFY_SPLIT", "0"); }
 
-// Split path in chunks of at most COA_VERIFY_MAX_LANES items (one slab each).
+// Split path in chunks of at most COA_SPLIT_CHUNK items (one slab each).
 // k from d_k, or hashed in k_pre_halve from d_msgs (msg_len bytes per item)
 // when d_k is null.
 int enqueue_split(Dev& d, const uint8_t* d_msgs, size_t msg_len, const uint32_t* d_k, const uint8_t* d_pks,
                   const uint8_t* d_sigs, size_t n, uint8_t* d_verdicts, const Workspace& w, hipStream_t s) {
-  for (size_t lo = 0; lo < n; lo += COA_VERIFY_MAX_LANES) {
-    const uint32_t cnt = (uint32_t)std::min<size_t>(COA_VERIFY_MAX_LANES, n - lo);
+  for (size_t lo = 0; lo < n; lo += COA_SPLIT_CHUNK) {
+    const uint32_t cnt = (uint32_t)std::min<size_t>(COA_SPLIT_CHUNK, n - lo);
     HIP_TRY(coa_launch_verify_split(d_pks + lo * 32, d_sigs + lo * 64, d_k ? nullptr : d_msgs + lo * msg_len,
                                     (uint32_t)msg_len, d_k ? d_k + lo * 8 : nullptr, cnt, w.rec + lo * 32,
                                     w.flags + lo, d_verdicts + lo, w.scratch,
