@@ -304,17 +304,20 @@ def lanes(request):
     """Latency kernel (64) and throughput kernel with one signature per lane
     (T0 = default grid) or a grid of 256 / 512 lanes, so each lane shares one
     inversion among several signatures (P compared with R's encoding).
-    `narrow`: [s]B from the radix-256 comb instead of the wide HBM comb."""
+    `narrow`: [s]B and [k](-A) from the radix-256 combs instead of the wide
+    HBM comb of B and the keys' wide combs."""
     parts = request.param.split("/")
     os.environ["COA_CERT_LANES"] = parts[0]
     if len(parts) > 1 and parts[1] != "T0":
         os.environ["COA_CERT_LANES_TOTAL"] = parts[1][1:]
     if "narrow" in parts:
         os.environ["COA_WCOMB"] = "0"
+        os.environ["COA_KEY_WCOMB"] = "0"
     yield int(parts[0])
     del os.environ["COA_CERT_LANES"]
     os.environ.pop("COA_CERT_LANES_TOTAL", None)
     os.environ.pop("COA_WCOMB", None)
+    os.environ.pop("COA_KEY_WCOMB", None)
 
 
 def test_fused_certificates_adversarial(engine, world, lanes):

@@ -8,6 +8,15 @@
 #define COA_KEY_TAB_ENTRIES (32 * 128)
 #define COA_KEY_TAB_DWORDS (COA_KEY_TAB_ENTRIES * 24)
 
+// per-key wide comb of -A (coa_smul.h wc_*): 16 positions x 2^15 multiples,
+// entry (j, m-1) = m * 2^(16 j) * (-A), exact integer multiples (torsion
+// kept), 24 dwords each: 48 MiB per key, built at registration when the
+// committee fits the COA_KEY_WCOMB_MB budget
+#define COA_KWCOMB_W 16
+#define COA_KWCOMB_POS 16
+#define COA_KWCOMB_ENTRIES ((uint64_t)COA_KWCOMB_POS << (COA_KWCOMB_W - 1))
+#define COA_KWCOMB_DWORDS (COA_KWCOMB_ENTRIES * 24)
+
 // key flag bits (k_key_flags)
 #define COA_KEY_DECOMPRESSES 1u   // CompressedEdwardsY::decompress succeeds
 #define COA_KEY_SMALL_ORDER 2u    // [8]A == O  (verify_strict rejects)
@@ -36,6 +45,7 @@ struct CertArgs {
   const uint32_t* keys;         // [nk][8] registered keys, sorted as dword tuples
   const uint32_t* kflags;       // [nk]
   const uint32_t* ktabs;        // [nk][COA_KEY_TAB_DWORDS] comb of -A per key
+  const uint32_t* kwtabs;       // [nk][COA_KWCOMB_DWORDS] wide comb of -A per key, or null
   uint32_t nk;
   const uint32_t* comb;         // B comb (coa_halved.h)
   const uint32_t* wcomb;        // wide B comb (coa_smul.h) or null
@@ -44,6 +54,8 @@ struct CertArgs {
 
 hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s);
 hipError_t coa_launch_key_tables(const uint32_t* keys, uint32_t nk, uint32_t* tabs, hipStream_t s);
+// wide combs from the radix-256 key combs (tabs already built)
+hipError_t coa_launch_key_wcombs(const uint32_t* tabs, uint32_t nk, uint32_t* wtabs, hipStream_t s);
 // lanes_per_sig: 64 (latency: two waves per signature, comb terms split over
 // a wave's lanes and summed by a butterfly) or 1 (throughput: K signatures
 // per lane, K from the job count).

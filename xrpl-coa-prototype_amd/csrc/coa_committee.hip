@@ -272,21 +272,30 @@ COA_DEV void job_comb(const CertArgs& a, uint32_t job, ge_p3& P, uint32_t& pre, 
   const uint32_t* ktab = a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS;
   ge_p1p1 t;
   // [s]B: 13 additions from the wide HBM comb when it is built, else the 32
-  // byte terms of the radix-256 comb (an s >= l only reaches Err verdicts)
-  int term = 0;
+  // byte terms of the radix-256 comb (an s >= l only reaches Err verdicts);
+  // [k](-A): 16 additions from the key's wide comb when the committee has
+  // them, else its 32 radix-256 terms
   if (a.wcomb) {
     wcomb_accumulate(P, sw, a.wcomb);
-    term = 32;
-  }
+  } else {
 #pragma unroll 1
-  for (; term < 64; term++) {
-    const bool isb = term < 32;
-    const int j = term & 31;
-    const int e = (int)byte_of(isb ? sd : kd, j) - 128;
-    ge_niels q;
-    comb_select(q, isb ? a.comb : ktab, j, e);
-    ge_madd(t, P, q);
-    ge_p1p1_to_p3(P, t);
+    for (int j = 0; j < 32; j++) {
+      ge_niels q;
+      comb_select(q, a.comb, j, (int)byte_of(sd, j) - 128);
+      ge_madd(t, P, q);
+      ge_p1p1_to_p3(P, t);
+    }
+  }
+  if (a.kwtabs) {
+    wc_accumulate<COA_KWCOMB_W, COA_KWCOMB_POS>(P, k.v, a.kwtabs + (uint64_t)slot * COA_KWCOMB_DWORDS);
+  } else {
+#pragma unroll 1
+    for (int j = 0; j < 32; j++) {
+      ge_niels q;
+      comb_select(q, ktab, j, (int)byte_of(kd, j) - 128);
+      ge_madd(t, P, q);
+      ge_p1p1_to_p3(P, t);
+    }
   }
 }
 
@@ -650,6 +659,43 @@ uint64_t cert_tp_lanes(uint64_t jobs) {
 hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s) {
   if (nk == 0) return hipSuccess;
   hipLaunchKernelGGL(k_key_flags, dim3((nk + 255) / 256), dim3(256), 0, s, keys, nk, flags);
+  return hipGetLastError();
+}
+
+// Wide comb entry (key, j, m-1) = m * 2^(16 j) * (-A): with m = lo + 256 hi,
+// lo a signed byte, it is the sum of the exact radix-256 comb entries
+// (2j, lo) and (2j+1, hi) -- an integer multiple, torsion kept -- made affine.
+__global__ void __launch_bounds__(256) k_key_wcomb(const uint32_t* __restrict__ tabs, uint32_t nk,
+                                                   uint32_t* __restrict__ wtabs) {
+  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t key = (uint32_t)(id / COA_KWCOMB_ENTRIES);
+  if (key >= nk) return;
+  const uint32_t e = (uint32_t)(id % COA_KWCOMB_ENTRIES);
+  const int j = (int)(e >> (COA_KWCOMB_W - 1));
+  const int m = (int)(e & ((1u << (COA_KWCOMB_W - 1)) - 1)) + 1;
+  int lo = m & 255, hi = m >> 8;
+  if (lo >= 128) {
+    lo -= 256;
+    hi += 1;
+  }
+  const uint32_t* ktab = tabs + (uint64_t)key * COA_KEY_TAB_DWORDS;
+  ge_p3 P;
+  ge_p3_identity(P);
+  ge_p1p1 t;
+  ge_niels q;
+  comb_select(q, ktab, 2 * j, lo);
+  ge_madd(t, P, q);
+  ge_p1p1_to_p3(P, t);
+  comb_select(q, ktab, 2 * j + 1, hi);
+  ge_madd(t, P, q);
+  ge_p1p1_to_p3(P, t);
+  store_niels(wtabs + (uint64_t)key * COA_KWCOMB_DWORDS + (uint64_t)e * 24, P);
+}
+
+hipError_t coa_launch_key_wcombs(const uint32_t* tabs, uint32_t nk, uint32_t* wtabs, hipStream_t s) {
+  if (nk == 0) return hipSuccess;
+  const uint64_t total = (uint64_t)nk * COA_KWCOMB_ENTRIES;
+  hipLaunchKernelGGL(k_key_wcomb, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, tabs, nk, wtabs);
   return hipGetLastError();
 }
 

@@ -98,13 +98,14 @@ struct Dev {
   uint32_t* wcomb = nullptr;  // wide B comb, COA_WCOMB_POS x 2^(W-1) entries (654 MB at W = 20)
   DevBuf msgs, pks, sigs, kbuf, rec, verdicts, scratch, aux, rbuf, seeds, offs, data, out, idx, zs, terms, flags;
   // committee key cache (f2): sorted keys, flags, one comb of -A per key
-  DevBuf ckeys, kflags, ktabs, cert, cscr;
+  DevBuf ckeys, kflags, ktabs, kwtabs, cert, cscr;
+  bool kwide = false;  // kwtabs holds the committee's wide combs
   uint32_t nkeys = 0;
   PinBuf pin;
   std::mutex mu;
   std::vector<DevBuf*> all() {
     return {&msgs,  &pks,  &sigs, &kbuf, &rec, &verdicts, &scratch, &aux,  &rbuf,   &seeds, &offs,
-            &data,  &out,  &idx,  &zs,   &terms, &flags,  &ckeys,   &kflags, &ktabs, &cert, &cscr};
+            &data,  &out,  &idx,  &zs,   &terms, &flags,  &ckeys,   &kflags, &ktabs, &kwtabs, &cert, &cscr};
   }
 };
 
@@ -121,6 +122,12 @@ bool env_is(const char* name, const char* value) {
 // The wide comb is built at device open unless COA_WCOMB=0 then; COA_WCOMB=0
 // at call time selects the radix-256 comb (A/B runs; read per call).
 const uint32_t* wcomb_of(const Dev& d) { return env_is("COA_WCOMB", "0") ? nullptr : d.wcomb; }
+// Bytes of HBM the committee's wide key combs may take (COA_KEY_WCOMB_MB,
+// default 16 GiB: committees up to 341 keys; 0 disables them).
+double key_wcomb_budget() {
+  const char* v = getenv("COA_KEY_WCOMB_MB");
+  return (v ? atof(v) : 16384.0) * 1048576.0;
+}
 // COA_VERIFY_WAVES=3 selects the 168-VGPR instance of k_verify_halved.
 int verify_waves() {
   const char* w = getenv("COA_VERIFY_WAVES");
@@ -460,6 +467,7 @@ CertArgs cert_args(Dev& d, uint8_t* base, const CertPack& p, size_t nc, size_t n
   a.nk = d.nkeys;
   a.comb = d.comb;
   a.wcomb = wcomb_of(d);
+  a.kwtabs = (d.kwide && !env_is("COA_KEY_WCOMB", "0")) ? d.kwtabs.as<uint32_t>() : nullptr;
   a.status = reinterpret_cast<uint32_t*>(base + p.status);
   return a;
 }
@@ -923,6 +931,13 @@ int coa_committee_register(const uint8_t* pks, size_t n) {
     HIP_TRY(hipMemcpyAsync(d.ckeys.p, keys.data(), nk * 32, hipMemcpyHostToDevice, d.stream));
     HIP_TRY(coa_launch_key_flags(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.kflags.as<uint32_t>(), d.stream));
     HIP_TRY(coa_launch_key_tables(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.ktabs.as<uint32_t>(), d.stream));
+    // wide combs (48 MiB per key) when the committee fits the budget
+    d.kwide = false;
+    if ((double)nk * COA_KWCOMB_DWORDS * 4 <= key_wcomb_budget()) {
+      HIP_TRY(d.kwtabs.ensure(nk * (size_t)COA_KWCOMB_DWORDS * 4));
+      HIP_TRY(coa_launch_key_wcombs(d.ktabs.as<uint32_t>(), (uint32_t)nk, d.kwtabs.as<uint32_t>(), d.stream));
+      d.kwide = true;
+    }
     HIP_TRY(hipStreamSynchronize(d.stream));
     d.nkeys = (uint32_t)nk;
   }
@@ -1001,6 +1016,7 @@ int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data,
   a.nk = d->nkeys;
   a.comb = d->comb;
   a.wcomb = wcomb_of(*d);
+  a.kwtabs = (d->kwide && !env_is("COA_KEY_WCOMB", "0")) ? d->kwtabs.as<uint32_t>() : nullptr;
   a.status = d_status;
   const int lanes = cert_lanes(n + n_votes);
   HIP_TRY(hipMemsetAsync(d_status, 0, n * 4, s));

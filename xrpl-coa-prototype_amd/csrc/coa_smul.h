@@ -130,15 +130,19 @@ COA_DEV void comb_select(ge_niels& q, const uint32_t* __restrict__ comb, int j, 
 // additions instead of the 32 of the radix-256 comb above.  W = 20: 13
 // positions, 6.8 M entries, 654 MB of the 288 GB HBM.
 // ---------------------------------------------------------------------------
-static_assert(COA_WCOMB_W * COA_WCOMB_POS >= 255 && COA_WCOMB_W * COA_WCOMB_POS <= 288, "wide comb recoding");
 
-// x (8 words, < 2^253) -> 9 words of x + sum_j 2^(W j + W - 1): the offsets
-// are single distinct bits, so the constant is a bit pattern.
-COA_DEV void wcomb_recode(uint32_t* r, const uint32_t* x) {
+// Generic wide comb of a point P: POS positions x 2^(W-1) magnitudes,
+// entry (j, m-1) = m * 2^(W j) * P as affine Niels (24 dwords).  A scalar
+// x < 2^253 is recoded as the W-bit digits of x + sum_j 2^(W j + W - 1)
+// minus 2^(W-1); the offsets are single distinct bits, so the constant is a
+// bit pattern.
+template <int W, int POS>
+COA_DEV void wc_recode(uint32_t* r, const uint32_t* x) {
+  static_assert(W * POS >= 255 && W * POS <= 288, "wide comb recoding");
   uint32_t c[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-  for (int j = 0; j < COA_WCOMB_POS; j++) {
-    const int b = COA_WCOMB_W * j + COA_WCOMB_W - 1;
+  for (int j = 0; j < POS; j++) {
+    const int b = W * j + W - 1;
     c[b >> 5] |= 1u << (b & 31);
   }
   uint32_t cy = 0;
@@ -147,17 +151,19 @@ COA_DEV void wcomb_recode(uint32_t* r, const uint32_t* x) {
   r[8] = c[8] + cy;
 }
 // Low W bits of r as a signed digit, then r >>= W.
-COA_DEV int wcomb_take_digit(uint32_t* r) {
-  const int d = (int)(r[0] & ((1u << COA_WCOMB_W) - 1)) - (int)COA_WCOMB_MAG;
+template <int W>
+COA_DEV int wc_take_digit(uint32_t* r) {
+  const int d = (int)(r[0] & ((1u << W) - 1)) - (1 << (W - 1));
 #pragma unroll
-  for (int i = 0; i < 8; i++) r[i] = __builtin_amdgcn_alignbit(r[i + 1], r[i], COA_WCOMB_W);
-  r[8] >>= COA_WCOMB_W;
+  for (int i = 0; i < 8; i++) r[i] = __builtin_amdgcn_alignbit(r[i + 1], r[i], W);
+  r[8] >>= W;
   return d;
 }
 // Raw 24 words of entry (j, |d|) (entry (j, 0) for d == 0; ignored then).
-COA_DEV void wcomb_load(uint32_t* w, const uint32_t* __restrict__ tab, int j, int d) {
+template <int W>
+COA_DEV void wc_load(uint32_t* w, const uint32_t* __restrict__ tab, int j, int d) {
   const uint32_t m = (uint32_t)(d < 0 ? -d : d);
-  const uint64_t idx = (uint64_t)j * COA_WCOMB_MAG + (m ? m - 1 : 0);
+  const uint64_t idx = (uint64_t)j * (1u << (W - 1)) + (m ? m - 1 : 0);
   const uint4* src = reinterpret_cast<const uint4*>(tab + idx * 24);
 #pragma unroll
   for (int i = 0; i < 6; i++) {
@@ -178,20 +184,20 @@ COA_DEV void wcomb_apply(ge_niels& q, const uint32_t* w, int d) {
   if (d == 0) ge_niels_identity(q);
   ge_niels_cneg(q, d < 0);
 }
-
-// acc += [x]B from the wide comb (x < 2^253; a larger x gives some point,
+// acc += [x]P from P's wide comb (x < 2^253; a larger x gives some point,
 // never an out-of-range entry).  Entry j+1 is loaded while addition j runs.
-COA_DEV void wcomb_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __restrict__ tab) {
+template <int W, int POS>
+COA_DEV void wc_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __restrict__ tab) {
   uint32_t r[9], cur[24], nxt[24];
-  wcomb_recode(r, x);
-  int d = wcomb_take_digit(r);
-  wcomb_load(cur, tab, 0, d);
+  wc_recode<W, POS>(r, x);
+  int d = wc_take_digit<W>(r);
+  wc_load<W>(cur, tab, 0, d);
   ge_p1p1 t;
 #pragma unroll 1
-  for (int j = 0; j < COA_WCOMB_POS; j++) {
-    const int jn = j + 1 < COA_WCOMB_POS ? j + 1 : j;
-    const int dn = wcomb_take_digit(r);
-    wcomb_load(nxt, tab, jn, dn);
+  for (int j = 0; j < POS; j++) {
+    const int jn = j + 1 < POS ? j + 1 : j;
+    const int dn = wc_take_digit<W>(r);
+    wc_load<W>(nxt, tab, jn, dn);
     ge_niels q;
     wcomb_apply(q, cur, d);
     ge_madd(t, acc, q);
@@ -200,6 +206,14 @@ COA_DEV void wcomb_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __r
 #pragma unroll
     for (int i = 0; i < 24; i++) cur[i] = nxt[i];
   }
+}
+
+// The wide comb of B (COA_WCOMB_*, coa_halved.h).
+COA_DEV void wcomb_load(uint32_t* w, const uint32_t* __restrict__ tab, int j, int d) {
+  wc_load<COA_WCOMB_W>(w, tab, j, d);
+}
+COA_DEV void wcomb_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __restrict__ tab) {
+  wc_accumulate<COA_WCOMB_W, COA_WCOMB_POS>(acc, x, tab);
 }
 
 COA_DEV uint32_t take_low_byte(uint32_t* x) {
