@@ -26,7 +26,7 @@ def lib(count=False):
     if key not in _libs:
         build()
         L = ctypes.CDLL(os.path.join(BUILD, "libcoa_oracle_count.so" if count else "libcoa_oracle.so"))
-        P8 = ctypes.POINTER(ctypes.c_uint8)
+        P8 = ctypes.c_void_p  # numpy addresses (_p) or bytes objects, no pointer objects
         sz = ctypes.c_size_t
         L.coa_oracle_verify_strict.argtypes = [P8, sz, P8, P8]
         L.coa_oracle_verify_strict.restype = ctypes.c_int
@@ -36,7 +36,7 @@ def lib(count=False):
         L.coa_oracle_verify_strict_many.restype = None
         L.coa_oracle_sha512.argtypes = [P8, sz, P8]
         L.coa_oracle_sha512.restype = None
-        L.coa_oracle_sha512_many_mt.argtypes = [P8, ctypes.POINTER(ctypes.c_uint64), sz, P8, ctypes.c_int]
+        L.coa_oracle_sha512_many_mt.argtypes = [P8, ctypes.c_void_p, sz, P8, ctypes.c_int]
         L.coa_oracle_sha512_many_mt.restype = None
         if count:
             L.coa_oracle_counts.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 2
@@ -54,7 +54,7 @@ def sodium_verify_many(msgs, pks, sigs, nthreads=1, path=SODIUM):
     if "sodium" not in _libs:
         build()
         L = ctypes.CDLL(os.path.join(BUILD, "libcoa_sodium_drive.so"))
-        P8 = ctypes.POINTER(ctypes.c_uint8)
+        P8 = ctypes.c_void_p
         L.coa_sodium_verify_many.argtypes = [ctypes.c_char_p, P8, ctypes.c_size_t, P8, P8, ctypes.c_size_t, P8,
                                              ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]
         L.coa_sodium_verify_many.restype = ctypes.c_int
@@ -71,7 +71,7 @@ def sodium_verify_many(msgs, pks, sigs, nthreads=1, path=SODIUM):
 
 
 def _p(a):
-    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+    return a.ctypes.data
 
 
 def _arr(b):
@@ -80,17 +80,17 @@ def _arr(b):
 
 def verify_strict(msg, pk, sig, L=None):
     L = L or lib()
-    m, p, s = _arr(msg), _arr(pk), _arr(sig)
-    return L.coa_oracle_verify_strict(_p(m), len(msg), _p(p), _p(s)) == 0
+    m = bytes(msg)
+    return L.coa_oracle_verify_strict(m if m else b"\0", len(m), bytes(pk), bytes(sig)) == 0
 
 
 def verify_batch(msg, pks, sigs, zs):
     n = len(pks)
-    m = _arr(msg)
-    P = _arr(b"".join(pks)) if n else np.zeros(1, np.uint8)
-    S = _arr(b"".join(sigs)) if n else np.zeros(1, np.uint8)
-    Z = _arr(b"".join(z.to_bytes(16, "little") for z in zs)) if n else np.zeros(1, np.uint8)
-    return lib().coa_oracle_verify_batch(_p(m), len(msg), _p(P), _p(S), n, _p(Z)) == 0
+    m = bytes(msg)
+    P = b"".join(bytes(p) for p in pks) or b"\0"
+    S = b"".join(bytes(s) for s in sigs) or b"\0"
+    Z = b"".join(z.to_bytes(16, "little") for z in zs) or b"\0"
+    return lib().coa_oracle_verify_batch(m if m else b"\0", len(m), P, S, n, Z) == 0
 
 
 def verify_strict_many(msgs, pks, sigs, nthreads=1):
@@ -104,10 +104,10 @@ def verify_strict_many(msgs, pks, sigs, nthreads=1):
 
 
 def sha512(data):
-    d = _arr(data)
-    out = np.zeros(64, np.uint8)
-    lib().coa_oracle_sha512(_p(d), len(data), _p(out))
-    return bytes(out)
+    d = bytes(data)
+    out = ctypes.create_string_buffer(64)
+    lib().coa_oracle_sha512(d if d else b"\0", len(d), out)
+    return out.raw
 
 
 def field_op_counts(msg, pk, sig):
@@ -127,8 +127,7 @@ def sha512_many(data, offsets, nthreads=1):
     offsets = np.ascontiguousarray(offsets, np.uint64)
     n = offsets.shape[0] - 1
     out = np.zeros((n, 64), np.uint8)
-    lib().coa_oracle_sha512_many_mt(_p(data), offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n, _p(out),
-                                    nthreads)
+    lib().coa_oracle_sha512_many_mt(_p(data), offsets.ctypes.data, n, _p(out), nthreads)
     return out
 
 
