@@ -22,7 +22,8 @@ Also reported:
                 time is measured here with HIP events on the stream it runs on.
   cpu_baseline  the C restatement of dalek's algorithms (oracle/, "port")
                 on this host's cores, rank 0 at N=1 only, on a bounded sample.
-  secondary     (rank 0, N=1) C4 worker-batch SHA-512 GB/s; C3 and C1
+  secondary     (rank 0, N=1) one C5 shard (2^21 triples) per verify call;
+                C4 worker-batch SHA-512 GB/s; C3 and C1
                 Certificate::verify -- certificates/s for a round resident in
                 HBM and p50/p99 latency of one certificate through the
                 host-pointer C ABI, beside the single-core CPU restatement.
@@ -172,6 +173,42 @@ def worker_batches_on_device(nb, dev):
         data[:, pos + 9 + k] = ((ctr >> (8 * (7 - k))) & 0xFF).to(torch.uint8)
     offs = torch.arange(nb + 1, device=dev, dtype=torch.int64) * blen
     return data.reshape(-1), offs, blen
+
+
+def c5_shard(local, dev, stream, n=1 << 21, steps=3):
+    """One C5 shard per GPU (2^24 triples / 8 GPUs = 2,097,152, BASELINE.json
+    configs[4]) as ONE verify call, all valid: the per-GPU rate behind the
+    north star's 8-GPU target.  (Its 1 % adversarial parity run is
+    tools/c5_parity.py.)"""
+    import torch
+
+    import coa_crypto
+    import workloads
+
+    seeds = torch.from_numpy(workloads.key_seeds(n)).to(dev)
+    msgs = torch.from_numpy(workloads.messages(n)).to(dev)
+    pks = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    sigs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    coa_crypto.sign_many_device(local, seeds, msgs, pks, sigs)
+    del seeds
+    verdicts = torch.ones(n, dtype=torch.uint8, device=dev)
+    ws = torch.empty(coa_crypto.verify_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    coa_crypto.verify_strict_many_device(local, msgs, pks, sigs, verdicts, ws, stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        coa_crypto.verify_strict_many_device(local, msgs, pks, sigs, verdicts, ws, stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    ok = int(verdicts.sum().item()) == 0
+    del msgs, pks, sigs, verdicts, ws
+    torch.cuda.empty_cache()
+    return {"workload": f"C5 shard: {n:,} triples (2^24 / 8 GPUs) per verify call, all valid",
+            "ms_per_call": round(ms, 3), "verifications_per_s": round(n / (ms * 1e-3), 1),
+            "frac": round(ALG_INT32_OPS_PER_VERIFY * n / (ms * 1e-3) / 1e12 / PEAK_INT32_TOPS, 4),
+            "verdicts_ok": ok}
 
 
 def c4_sha512(local, dev, stream, counts, steps, cpu_threads):
@@ -417,6 +454,7 @@ def main():
         del ws
         torch.cuda.empty_cache()
         secondary = {
+            "c5_shard": c5_shard(local, dev, stream),
             "c4_sha512": c4_sha512(local, dev, stream, [int(x) for x in args.c4_batches.split(",") if x], 2,
                                    threads),
             "c3_certificate_verify": certificate_config(args.c3_certs, 1000, threads, dev, stream),
