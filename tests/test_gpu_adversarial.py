@@ -56,14 +56,24 @@ def test_adversarial_device_path(engine):
     assert (out.cpu().numpy() == exp).all()
 
 
-@pytest.mark.parametrize("impl", ["halved", "full"])
-def test_both_verify_kernels_agree(engine, impl, monkeypatch):
-    """The halved-scalar kernel (default) and the full-length kernel
-    (COA_VERIFY_IMPL=full) both match the oracle on the same adversarial mix."""
+VERIFY_PATHS = {
+    "split": {},                                            # default: k_pre_halve + k_verify_main
+    "split/narrow": {"COA_WCOMB": "0"},                     # [e]B from the radix-256 comb
+    "single": {"COA_VERIFY_SPLIT": "0"},                    # k_halve + k_verify_halved
+    "single/narrow": {"COA_VERIFY_SPLIT": "0", "COA_WCOMB": "0"},
+    "full": {"COA_VERIFY_IMPL": "full"},                    # k_hram + k_verify_strict, no halving
+}
+
+
+@pytest.mark.parametrize("impl", list(VERIFY_PATHS))
+def test_every_verify_path_agrees(engine, impl, monkeypatch):
+    """Every verification path (read per call) matches the oracle on the same
+    adversarial mix: the split launch pair (default), the single-kernel
+    halved path, the full-length kernel, each comb of B."""
     from workloads import adversarial_mix, key_seeds, messages
 
-    if impl == "full":
-        monkeypatch.setenv("COA_VERIFY_IMPL", "full")
+    for k, v in VERIFY_PATHS[impl].items():
+        monkeypatch.setenv(k, v)
     n = 20_000
     pks, sigs = engine.sign_many(key_seeds(n, 7), messages(n, 7))
     msgs, pks, sigs, cls = adversarial_mix(messages(n, 7), pks, sigs, frac=0.05, seed=77, mixed_pool=_pool())
