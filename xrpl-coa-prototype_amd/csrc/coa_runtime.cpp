@@ -47,12 +47,13 @@ int fail(int code, const std::string& msg) {
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
+  // exact: no 25 % growth headroom (multi-GB tables)
+  hipError_t ensure(size_t bytes, bool exact = false) {
     if (bytes <= cap) return hipSuccess;
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+    const size_t want = exact ? bytes : std::max<size_t>(bytes + bytes / 4, 4096);
     hipError_t e = hipMalloc(&p, want);
     if (e == hipSuccess) cap = want;
     return e;
@@ -147,9 +148,15 @@ int open_device(int d) {
   HIP_TRY(coa_launch_build_btable(dev->btab, dev->stream));
   HIP_TRY(hipMalloc(&dev->comb, COA_COMB_DWORDS * sizeof(uint32_t)));
   HIP_TRY(coa_launch_build_comb(dev->comb, dev->btab, dev->stream));
+  // the wide comb only speeds things up: without the memory for it the
+  // radix-256 comb serves every call
   if (!env_is("COA_WCOMB", "0")) {
-    HIP_TRY(hipMalloc(&dev->wcomb, COA_WCOMB_DWORDS * sizeof(uint32_t)));
-    HIP_TRY(coa_launch_build_wcomb(dev->wcomb, dev->comb, dev->stream));
+    if (hipMalloc(&dev->wcomb, COA_WCOMB_DWORDS * sizeof(uint32_t)) == hipSuccess) {
+      HIP_TRY(coa_launch_build_wcomb(dev->wcomb, dev->comb, dev->stream));
+    } else {
+      dev->wcomb = nullptr;
+      (void)hipGetLastError();
+    }
   }
   HIP_TRY(hipStreamSynchronize(dev->stream));
   g_devs.push_back(std::move(dev));
@@ -932,11 +939,18 @@ int coa_committee_register(const uint8_t* pks, size_t n) {
     HIP_TRY(coa_launch_key_flags(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.kflags.as<uint32_t>(), d.stream));
     HIP_TRY(coa_launch_key_tables(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.ktabs.as<uint32_t>(), d.stream));
     // wide combs (48 MiB per key) when the committee fits the budget
+    // (speed only: without the memory the radix-256 key combs serve)
     d.kwide = false;
     if ((double)nk * COA_KWCOMB_DWORDS * 4 <= key_wcomb_budget()) {
-      HIP_TRY(d.kwtabs.ensure(nk * (size_t)COA_KWCOMB_DWORDS * 4));
-      HIP_TRY(coa_launch_key_wcombs(d.ktabs.as<uint32_t>(), (uint32_t)nk, d.kwtabs.as<uint32_t>(), d.stream));
-      d.kwide = true;
+      if (d.kwtabs.ensure(nk * (size_t)COA_KWCOMB_DWORDS * 4, true) == hipSuccess) {
+        HIP_TRY(coa_launch_key_wcombs(d.ktabs.as<uint32_t>(), (uint32_t)nk, d.kwtabs.as<uint32_t>(), d.stream));
+        d.kwide = true;
+      } else {
+        d.kwtabs.release();
+        (void)hipGetLastError();
+      }
+    } else {
+      d.kwtabs.release();  // a smaller committee's tables are not kept
     }
     HIP_TRY(hipStreamSynchronize(d.stream));
     d.nkeys = (uint32_t)nk;
