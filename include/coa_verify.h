@@ -123,6 +123,23 @@ int coa_ed25519_verify_batch_groups_z(const uint8_t* msgs, const uint8_t* pks, c
                                       const uint64_t* group_offsets, size_t n_groups, const uint8_t* zs,
                                       uint8_t* group_verdicts_out);
 
+/* Pippenger form of the call above for ONE group whose buffers are resident
+ * in the HBM of `device` (dalek's verify_batch switches to Pippenger above
+ * 190 points; the host-pointer entries above route groups of at least
+ * COA_MSM_MIN signatures, default 16384, here as well).
+ *   d_msg        32 bytes, the digest every signature signs
+ *   d_pks        n * 32, d_sigs n * 64
+ *   d_zs         n * 16 explicit weights (parity tests) or NULL = derived
+ *                from rng_seed (0 = fresh OS entropy)
+ *   *d_verdict   0 Ok / 1 Err, same rules as coa_ed25519_verify_batch
+ * `workspace` NULL = engine-owned (the call then waits for the stream), else
+ * at least coa_verify_batch_workspace_bytes(n) bytes on `device` (the call
+ * only enqueues). */
+size_t coa_verify_batch_workspace_bytes(size_t n);
+int coa_ed25519_verify_batch_device(int device, const uint8_t* d_msg, const uint8_t* d_pks, const uint8_t* d_sigs,
+                                    size_t n, const uint8_t* d_zs, uint64_t rng_seed, uint8_t* d_verdict,
+                                    void* workspace, void* stream);
+
 /* ------------------------------------------------------------------ Digest
  * Replaces Sha512::digest at worker/src/processor.rs:38 (500 KB batch
  * digests) and the Header/Vote/Certificate digests

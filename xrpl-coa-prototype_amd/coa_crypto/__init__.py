@@ -88,6 +88,9 @@ def lib():
         "coa_ed25519_verify_batch": ([P8, P8, P8, sz, ctypes.c_uint64], ctypes.c_int),
         "coa_ed25519_verify_batch_groups": ([P8, P8, P8, P64, sz, P8, ctypes.c_uint64], ctypes.c_int),
         "coa_ed25519_verify_batch_groups_z": ([P8, P8, P8, P64, sz, P8, P8], ctypes.c_int),
+        "coa_verify_batch_workspace_bytes": ([sz], sz),
+        "coa_ed25519_verify_batch_device": ([ctypes.c_int, vp, vp, vp, sz, vp, ctypes.c_uint64, vp, vp, vp],
+                                            ctypes.c_int),
         "coa_sha512_many": ([P8, P64, sz, P8], ctypes.c_int),
         "coa_sha512_trunc32_many": ([P8, P64, sz, P8], ctypes.c_int),
         "coa_sha512_many_device": ([ctypes.c_int, vp, vp, sz, vp, vp], ctypes.c_int),
@@ -361,6 +364,29 @@ def public_keys(seeds):
 # ----------------------------------------------------------- device level
 def verify_workspace_bytes(n):
     return lib().coa_verify_workspace_bytes(n)
+
+
+def verify_batch_workspace_bytes(n):
+    return lib().coa_verify_batch_workspace_bytes(n)
+
+
+def verify_batch_device(device, msg, pks, sigs, verdict, zs=None, rng_seed=0, workspace=None, stream=None):
+    """Enqueue the Pippenger batch equation over ONE group of HBM-resident
+    torch uint8 tensors (msg [32], pks [n, 32], sigs [n, 64], zs [n, 16] or
+    None); verdict[0] = 0 Ok / 1 Err."""
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    n = pks.shape[0]
+    assert tuple(sigs.shape) == (n, 64) and msg.numel() == 32
+    zp = zs.data_ptr() if zs is not None else None
+    if zs is not None:
+        assert tuple(zs.shape) == (n, 16)
+    ws = workspace.data_ptr() if workspace is not None else None
+    _check(lib().coa_ed25519_verify_batch_device(device, msg.data_ptr(), pks.data_ptr(), sigs.data_ptr(), n, zp,
+                                                 rng_seed, verdict.data_ptr(), ws, handle))
 
 
 def verify_strict_many_device(device, msgs, pks, sigs, verdicts, workspace=None, stream=None):

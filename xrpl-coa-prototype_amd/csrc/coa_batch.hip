@@ -130,8 +130,8 @@ COA_DEV uint32_t top_nibble(uint32_t* x) {
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_batch_z(const uint32_t* __restrict__ kbuf, const uint8_t* __restrict__ sigs,
-                                                 const uint32_t* __restrict__ group_of, uint32_t n, uint64_t seed,
-                                                 uint32_t* __restrict__ zs) {
+                                                 const uint32_t* __restrict__ group_of, uint32_t group_const,
+                                                 uint32_t n, uint64_t seed, uint32_t* __restrict__ zs) {
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     // one block: "coa-batch-z"(11) pad to 16 | seed 8 | group 4 | i 4 | h 32 | s 32 = 96 bytes
@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(256) k_batch_z(const uint32_t* __restrict__ kb
     m[3] = 0;
     m[4] = (uint32_t)seed;
     m[5] = (uint32_t)(seed >> 32);
-    m[6] = group_of[i];
+    m[6] = group_of ? group_of[i] : group_const;
     m[7] = i;
 #pragma unroll
     for (int j = 0; j < 8; j++) m[8 + j] = kbuf[(uint64_t)i * 8 + j];
@@ -339,11 +339,11 @@ __global__ void __launch_bounds__(BATCH_BLOCK) k_batch_reduce(const uint64_t* __
   }
 }
 
-hipError_t coa_launch_batch_z(const uint32_t* kbuf, const uint8_t* sigs, const uint32_t* group_of, uint32_t n,
-                              uint64_t seed, uint32_t* zs, hipStream_t s) {
+hipError_t coa_launch_batch_z(const uint32_t* kbuf, const uint8_t* sigs, const uint32_t* group_of,
+                              uint32_t group_const, uint32_t n, uint64_t seed, uint32_t* zs, hipStream_t s) {
   if (n == 0) return hipSuccess;
   uint32_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(k_batch_z, dim3(blocks), dim3(256), 0, s, kbuf, sigs, group_of, n, seed, zs);
+  hipLaunchKernelGGL(k_batch_z, dim3(blocks), dim3(256), 0, s, kbuf, sigs, group_of, group_const, n, seed, zs);
   return hipGetLastError();
 }
 

@@ -1,0 +1,654 @@
+// Pippenger batch equation for gfx950: crypto::Signature::verify_batch
+// (crypto/src/lib.rs:206-219) -> ed25519-dalek 1.0.1 verify_batch over ONE
+// large group (dalek switches from Straus to Pippenger above 190 points;
+// SURVEY.md §2 row 2).  Same equation and acceptance rules as coa_batch.hip:
+//   Ok  iff  every s_i < l, every A_i and R_i decompresses, and
+//            [-(sum z_i s_i mod l)]B + sum [z_i]R_i + sum [z_i h_i mod l]A_i == O
+// computed exactly, so with the same z_i the verdict equals dalek's bit for
+// bit (torsion components included) and equals the per-vote path's.
+//
+// Points (np = 2n + 1): R_0..R_{n-1}, A_0..A_{n-1}, B, affine Niels form
+// (decompression yields Z = 1, so no inversion).  Scalars are recoded into
+// signed radix-2^9 digits |d| <= 256: 15 windows for the 128-bit weights of
+// R_i, 29 for the 253-bit scalars of A_i and B.
+//
+// Kernels:
+//   k_msm_prep    one lane per signature: encoding checks, decompression of
+//                 A_i and R_i to Niels form, z h mod l, digits, block partial
+//                 sums of z s (288-bit integers)
+//   k_msm_bpoint  one workgroup: b = -(sum z s) mod l, B and its digits
+//   k_msm_bucket  one workgroup per (chunk of 256·run points, window):
+//                 LDS counting sort of the chunk's points by |digit|; every
+//                 lane then adds `run` consecutive sorted points (balanced
+//                 whatever the digit distribution), flushing each completed
+//                 bucket segment to LDS; lane t gathers bucket t+1 from its
+//                 owner's segment and the continuation segments of the lanes
+//                 after it; sum_j j·B_j by a 256-lane suffix scan plus a
+//                 reduction (wave shuffles, LDS across the four waves)
+//   k_msm_wsum    one workgroup per window: sum of the chunk partials
+//   k_msm_final   one wave: Horner over the windows (9 doublings each) with
+//                 the four squarings / three products of every doubling on
+//                 four lanes at once, identity test, encoding flag -> verdict
+#include "coa_msm.h"
+
+#include <cstdlib>
+
+#include "coa_fe.h"
+#include "coa_ge.h"
+#include "coa_sc.h"
+
+namespace {
+
+constexpr int NB = COA_MSM_NB;
+constexpr int WA = COA_MSM_WA;
+constexpr int WR = COA_MSM_WR;
+constexpr int MAXRUN = COA_MSM_RUN;
+constexpr int CHUNK = COA_MSM_CHUNK;
+
+// Signed radix-2^9 recoding of an 8-word little-endian scalar: W digits in
+// [-256, 255] (a digit of value 256 never occurs: 511 + carry = 512 is 0
+// with carry).  The scalars are < 2^253 (W = 29) or < 2^128 (W = 15), so
+// the final carry is 0.
+template <int W>
+COA_DEV void recode(int* d, const uint32_t* x) {
+  uint32_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    const int b = 9 * w, k = b >> 5, s = b & 31;
+    uint32_t v = x[k] >> s;
+    if (s > 23 && k + 1 < 8) v |= x[k + 1] << (32 - s);
+    v = (v & 511u) + carry;
+    carry = v >= 256u ? 1u : 0u;
+    d[w] = (int)v - (int)(carry << 9);
+  }
+}
+
+COA_DEV void niels_store(uint32_t* dst, const ge_p3& p) {  // p affine (Z = 1)
+  fe ypx, ymx, t2d, d2;
+  fe_add(ypx, p.Y, p.X);
+  fe_sub(ymx, p.Y, p.X);
+  fe_const_d2(d2);
+  fe_mul(t2d, p.T, d2);
+  uint4* o = reinterpret_cast<uint4*>(dst);
+  o[0] = make_uint4(ypx.v[0], ypx.v[1], ypx.v[2], ypx.v[3]);
+  o[1] = make_uint4(ypx.v[4], ypx.v[5], ypx.v[6], ypx.v[7]);
+  o[2] = make_uint4(ymx.v[0], ymx.v[1], ymx.v[2], ymx.v[3]);
+  o[3] = make_uint4(ymx.v[4], ymx.v[5], ymx.v[6], ymx.v[7]);
+  o[4] = make_uint4(t2d.v[0], t2d.v[1], t2d.v[2], t2d.v[3]);
+  o[5] = make_uint4(t2d.v[4], t2d.v[5], t2d.v[6], t2d.v[7]);
+}
+COA_DEV void niels_load(ge_niels& q, const uint32_t* src) {
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  fe* f[3] = {&q.yplusx, &q.yminusx, &q.xy2d};
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    const uint4 a = s[2 * c], b = s[2 * c + 1];
+    f[c]->v[0] = a.x;
+    f[c]->v[1] = a.y;
+    f[c]->v[2] = a.z;
+    f[c]->v[3] = a.w;
+    f[c]->v[4] = b.x;
+    f[c]->v[5] = b.y;
+    f[c]->v[6] = b.z;
+    f[c]->v[7] = b.w;
+  }
+}
+
+COA_DEV void p3_add(ge_p3& r, const ge_p3& a, const ge_p3& b) {
+  ge_cached c;
+  ge_p3_to_cached(c, b);
+  ge_p1p1 t;
+  ge_add(t, a, c);
+  ge_p1p1_to_p3(r, t);
+}
+
+// LDS point arrays are word-major (word * slots + slot): lanes touching
+// different slots hit different banks.
+COA_DEV void lds_put(uint32_t* base, int slots, int slot, const ge_p3& p) {
+  const fe* f[4] = {&p.X, &p.Y, &p.Z, &p.T};
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+#pragma unroll
+    for (int i = 0; i < 8; i++) base[(c * 8 + i) * slots + slot] = f[c]->v[i];
+}
+COA_DEV void lds_get(ge_p3& p, const uint32_t* base, int slots, int slot) {
+  fe* f[4] = {&p.X, &p.Y, &p.Z, &p.T};
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+#pragma unroll
+    for (int i = 0; i < 8; i++) f[c]->v[i] = base[(c * 8 + i) * slots + slot];
+}
+COA_DEV void gbl_put(uint32_t* dst, const ge_p3& p) {
+  const fe* f[4] = {&p.X, &p.Y, &p.Z, &p.T};
+  uint4* o = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    o[2 * c] = make_uint4(f[c]->v[0], f[c]->v[1], f[c]->v[2], f[c]->v[3]);
+    o[2 * c + 1] = make_uint4(f[c]->v[4], f[c]->v[5], f[c]->v[6], f[c]->v[7]);
+  }
+}
+COA_DEV void gbl_get(ge_p3& p, const uint32_t* src) {
+  fe* f[4] = {&p.X, &p.Y, &p.Z, &p.T};
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const uint4 a = s[2 * c], b = s[2 * c + 1];
+    f[c]->v[0] = a.x;
+    f[c]->v[1] = a.y;
+    f[c]->v[2] = a.z;
+    f[c]->v[3] = a.w;
+    f[c]->v[4] = b.x;
+    f[c]->v[5] = b.y;
+    f[c]->v[6] = b.z;
+    f[c]->v[7] = b.w;
+  }
+}
+COA_DEV void p3_shfl_down(ge_p3& r, const ge_p3& p, int delta) {
+  const fe* f[4] = {&p.X, &p.Y, &p.Z, &p.T};
+  fe* g[4] = {&r.X, &r.Y, &r.Z, &r.T};
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+#pragma unroll
+    for (int i = 0; i < 8; i++) g[c]->v[i] = __shfl_down(f[c]->v[i], delta, 64);
+}
+COA_DEV void p3_select(ge_p3& r, const ge_p3& a, bool c) {  // r = c ? a : r
+  fe_cmov(r.X, a.X, c);
+  fe_cmov(r.Y, a.Y, c);
+  fe_cmov(r.Z, a.Z, c);
+  fe_cmov(r.T, a.T, c);
+}
+
+// Block-wide sum of one point per lane (256 lanes); the result is valid in
+// thread 0.  `tmp` holds 4 slots of LDS points.
+COA_DEV void block_sum(ge_p3& acc, uint32_t* tmp) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+#pragma unroll 1
+  for (int delta = 32; delta > 0; delta >>= 1) {
+    ge_p3 q;
+    p3_shfl_down(q, acc, delta);
+    p3_add(acc, acc, q);
+  }
+  if (lane == 0) lds_put(tmp, 4, wave, acc);
+  __syncthreads();
+  if (t == 0) {
+#pragma unroll 1
+    for (int w = 1; w < 4; w++) {
+      ge_p3 q;
+      lds_get(q, tmp, 4, w);
+      p3_add(acc, acc, q);
+    }
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ prep
+__global__ void __launch_bounds__(256) k_msm_prep(const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
+                                                  const uint32_t* __restrict__ kbuf, const uint32_t* __restrict__ zs,
+                                                  uint32_t n, uint32_t np, uint32_t* __restrict__ pts,
+                                                  int16_t* __restrict__ dig, uint32_t* __restrict__ zpart,
+                                                  uint32_t* __restrict__ bad) {
+  __shared__ uint32_t red[9 * 256];
+  uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint32_t aw[8], rw[8], sw[8], hw[8], z[8];
+    const uint32_t* pk = reinterpret_cast<const uint32_t*>(pks + (uint64_t)i * 32);
+    const uint32_t* sg = reinterpret_cast<const uint32_t*>(sigs + (uint64_t)i * 64);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      aw[j] = pk[j];
+      rw[j] = sg[j];
+      sw[j] = sg[8 + j];
+      hw[j] = kbuf[(uint64_t)i * 8 + j];
+      z[j] = j < 4 ? zs[(uint64_t)i * 4 + j] : 0;
+    }
+    bool ok = sc_is_canonical(sw);
+    ge_p3 P;
+    ok = ge_decompress(P, aw) && ok;
+    niels_store(pts + (uint64_t)(n + i) * 24, P);
+    ok = ge_decompress(P, rw) && ok;
+    niels_store(pts + (uint64_t)i * 24, P);
+    if (!ok) atomicOr(bad, 1u);
+    sc a, zsv;
+    sc_mul(a, z, hw);
+    sc_mul(zsv, z, sw);
+    if (!ok) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        a.v[j] = 0;
+        z[j] = 0;
+        zsv.v[j] = 0;
+      }
+    }
+    int d[WA];
+    recode<WR>(d, z);
+#pragma unroll
+    for (int w = 0; w < WR; w++) dig[(uint64_t)w * np + i] = (int16_t)d[w];
+    recode<WA>(d, a.v);
+#pragma unroll
+    for (int w = 0; w < WA; w++) dig[(uint64_t)w * np + n + i] = (int16_t)d[w];
+    uint32_t cy = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) acc[j] = addc32(acc[j], zsv.v[j], cy, cy);
+    acc[8] += cy;
+  }
+  // block partial of sum z s (288-bit, no reduction)
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 9; j++) red[j * 256 + t] = acc[j];
+  __syncthreads();
+  for (int half = 128; half > 0; half >>= 1) {
+    if (t < half) {
+      uint32_t cy = 0;
+#pragma unroll
+      for (int j = 0; j < 9; j++) red[j * 256 + t] = addc32(red[j * 256 + t], red[j * 256 + t + half], cy, cy);
+    }
+    __syncthreads();
+  }
+  if (t < 9) zpart[blockIdx.x * 9 + t] = red[t * 256];
+}
+
+// ------------------------------------------------------------ B and -b
+__global__ void __launch_bounds__(256) k_msm_bpoint(const uint32_t* __restrict__ zpart, uint32_t nparts, uint32_t n,
+                                                    uint32_t np, uint32_t* __restrict__ pts,
+                                                    int16_t* __restrict__ dig) {
+  __shared__ uint32_t red[10 * 256];
+  const int t = threadIdx.x;
+  uint32_t acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t p = t; p < nparts; p += 256) {
+    uint32_t cy = 0;
+#pragma unroll
+    for (int j = 0; j < 9; j++) acc[j] = addc32(acc[j], zpart[p * 9 + j], cy, cy);
+    acc[9] += cy;
+  }
+#pragma unroll
+  for (int j = 0; j < 10; j++) red[j * 256 + t] = acc[j];
+  __syncthreads();
+  for (int half = 128; half > 0; half >>= 1) {
+    if (t < half) {
+      uint32_t cy = 0;
+#pragma unroll
+      for (int j = 0; j < 10; j++) red[j * 256 + t] = addc32(red[j * 256 + t], red[j * 256 + t + half], cy, cy);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    uint32_t x[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) x[j] = j < 10 ? red[j * 256] : 0;
+    sc b, nb;
+    sc_reduce512(b, x);
+    sc_neg(nb, b.v);
+    ge_p3 B;
+    ge_basepoint(B);
+    niels_store(pts + (uint64_t)2 * n * 24, B);
+    int d[WA];
+    recode<WA>(d, nb.v);
+#pragma unroll
+    for (int w = 0; w < WA; w++) dig[(uint64_t)w * np + 2 * n] = (int16_t)d[w];
+  }
+}
+
+// ------------------------------------------------------- bucket phase
+__global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restrict__ pts,
+                                                       const int16_t* __restrict__ dig, uint32_t n, uint32_t np,
+                                                       uint32_t run, uint32_t nchunks, uint32_t* __restrict__ segs,
+                                                       uint32_t* __restrict__ part) {
+  // 66 KiB of LDS: two workgroups per CU.  The bucket segments go to this
+  // block's 64 KiB slice of `segs` (owner segments by bucket, continuation
+  // segments by lane): written once, read once, L2-resident.
+  __shared__ uint16_t s_sorted[CHUNK];     // (local << 1) | negative, grouped by |digit|
+  __shared__ uint32_t s_tmp[32 * 4];       // wave totals / block sum
+  __shared__ uint32_t s_hist[NB + 2];      // histogram, then scatter cursors
+  __shared__ uint32_t s_off[NB + 2];       // s_off[j] = first sorted entry of bucket j
+  __shared__ uint32_t s_wtot[4];
+
+  // XCD-aware order: consecutive hardware blocks go round-robin over the 8
+  // XCDs, so hardware block h takes logical block (h % 8) * (G8 / 8) + h / 8
+  // and each XCD works through whole chunks, window after window (the
+  // chunk's points stay in that XCD's L2).
+  const uint32_t G = nchunks * WA, per = gridDim.x >> 3;
+  const uint32_t L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (L >= G) return;
+  const uint32_t ch = L / WA, w = L % WA;
+  const uint32_t chunk = 256 * run;
+  const uint32_t base = ch * chunk;
+  const uint32_t cnt = min(chunk, np - base);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t* out = part + ((uint64_t)w * nchunks + ch) * 32;
+  if (w >= WR && base + cnt <= n) {  // only R points (weights have 15 windows)
+    if (t == 0) {
+      ge_p3 o;
+      ge_p3_identity(o);
+      gbl_put(out, o);
+    }
+    return;
+  }
+  const int16_t* dw = dig + (uint64_t)w * np + base;
+  const uint32_t rlo = (w >= WR && base < n) ? n - base : 0;  // skip R points above their windows
+
+  for (int j = t; j < NB + 2; j += 256) s_hist[j] = 0;
+  __syncthreads();
+  for (uint32_t l = t; l < cnt; l += 256) {
+    const int d = l < rlo ? 0 : dw[l];
+    if (d) atomicAdd(&s_hist[d < 0 ? -d : d], 1u);
+  }
+  __syncthreads();
+  {  // exclusive scan of hist[1..256] (thread t: bucket t + 1)
+    const uint32_t v = s_hist[t + 1];
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wtot[wave] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int k = 0; k < wave; k++) pre += s_wtot[k];
+    const uint32_t excl = pre + x - v;
+    s_off[t + 1] = excl;
+    if (t == 255) s_off[NB + 1] = pre + x;
+    __syncthreads();
+    s_hist[t + 1] = excl;
+  }
+  __syncthreads();
+  for (uint32_t l = t; l < cnt; l += 256) {
+    const int d = l < rlo ? 0 : dw[l];
+    if (d) {
+      const uint32_t pos = atomicAdd(&s_hist[d < 0 ? -d : d], 1u);
+      s_sorted[pos] = (uint16_t)((l << 1) | (d < 0 ? 1u : 0u));
+    }
+  }
+  __syncthreads();
+  const uint32_t nnz = s_off[NB + 1];
+
+  // balanced accumulation: lane t adds sorted entries [t·run, (t+1)·run),
+  // the next point's load in flight during each addition
+  uint32_t* const seg = segs + (uint64_t)L * 512 * 32;  // [bucket - 1] owners, [256 + lane] continuations
+  {
+    const uint32_t lo = t * run, hi = min(lo + run, nnz);
+    ge_p3 acc;
+    ge_p3_identity(acc);
+    if (lo < hi) {
+      const uint32_t* pb = pts + (uint64_t)base * 24;
+      uint32_t cur = 1;  // bucket of entry lo: last j with s_off[j] <= lo
+#pragma unroll
+      for (uint32_t step = 128; step > 0; step >>= 1)
+        if (s_off[cur + step] <= lo) cur += step;
+      bool owner = s_off[cur] == lo;
+      uint32_t nxt = s_off[cur + 1];
+      uint32_t ent = s_sorted[lo];
+      ge_niels q;
+      niels_load(q, pb + (uint64_t)(ent >> 1) * 24);
+#pragma unroll 1
+      for (uint32_t e = lo; e < hi; e++) {
+        if (e == nxt) {  // bucket cur is complete: flush, move to the bucket of e
+          gbl_put(seg + (owner ? cur - 1 : 256 + t) * 32, acc);
+          ge_p3_identity(acc);
+          owner = true;
+          do {
+            cur++;
+            nxt = s_off[cur + 1];
+          } while (nxt == e);
+        }
+        ge_niels qn;
+        const uint32_t entn = s_sorted[e + 1 < hi ? e + 1 : e];
+        niels_load(qn, pb + (uint64_t)(entn >> 1) * 24);
+        ge_niels_cneg(q, (ent & 1u) != 0);
+        ge_p1p1 r;
+        ge_madd(r, acc, q);
+        ge_p1p1_to_p3(acc, r);
+        q = qn;
+        ent = entn;
+      }
+      gbl_put(seg + (owner ? cur - 1 : 256 + t) * 32, acc);
+    }
+  }
+  __syncthreads();
+
+  // lane t gathers bucket t + 1: its owner's segment plus the continuation
+  // segments of the lanes whose runs start inside it
+  ge_p3 S;
+  ge_p3_identity(S);
+  {
+    const uint32_t o0 = s_off[t + 1], o1 = s_off[t + 2];
+    if (o1 > o0) {
+      gbl_get(S, seg + t * 32);
+#pragma unroll 1
+      for (uint32_t l = o0 / run + 1; l * run < o1; l++) {
+        ge_p3 h;
+        gbl_get(h, seg + (256 + l) * 32);
+        p3_add(S, S, h);
+      }
+    }
+  }
+  // sum_j j·B_j = sum_t S_t with S_t = sum_{t' >= t} B_{t'+1}: suffix scan
+  // inside each wave ...
+#pragma unroll 1
+  for (int delta = 1; delta < 64; delta <<= 1) {
+    ge_p3 q, id;
+    p3_shfl_down(q, S, delta);
+    ge_p3_identity(id);
+    p3_select(q, id, lane + delta >= 64);
+    p3_add(S, S, q);
+  }
+  if (lane == 0) lds_put(s_tmp, 4, wave, S);  // wave totals
+  __syncthreads();
+  // ... plus the totals of the waves above
+#pragma unroll 1
+  for (int k = wave + 1; k < 4; k++) {
+    ge_p3 q;
+    lds_get(q, s_tmp, 4, k);
+    p3_add(S, S, q);
+  }
+  __syncthreads();
+  block_sum(S, s_tmp);
+  if (t == 0) gbl_put(out, S);
+}
+
+// ----------------------------------------------------------- window sums
+__global__ void __launch_bounds__(256) k_msm_wsum(const uint32_t* __restrict__ part, uint32_t nchunks,
+                                                  uint32_t* __restrict__ wsum) {
+  __shared__ uint32_t tmp[32 * 4];
+  const uint32_t w = blockIdx.x;
+  ge_p3 acc;
+  ge_p3_identity(acc);
+  for (uint32_t c = threadIdx.x; c < nchunks; c += 256) {
+    ge_p3 q;
+    gbl_get(q, part + ((uint64_t)w * nchunks + c) * 32);
+    p3_add(acc, acc, q);
+  }
+  block_sum(acc, tmp);
+  if (threadIdx.x == 0) gbl_put(wsum + (uint64_t)w * 32, acc);
+}
+
+// ------------------------------------------------------ Horner + verdict
+namespace {
+// Lanes 0..3 each compute one field product; every lane then reads all four
+// results (v_readlane), so the accumulator stays replicated across the wave.
+COA_DEV void fe_bcast(fe& r, const fe& v, int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)v.v[i], lane);
+}
+COA_DEV void fe_sel4(fe& r, int k, const fe& a, const fe& b, const fe& c, const fe& d) {
+  r = a;
+  fe_cmov(r, b, k == 1);
+  fe_cmov(r, c, k == 2);
+  fe_cmov(r, d, k == 3);
+}
+// one product per lane: lane k gets x_k * y_k
+COA_DEV void mul4(fe& r0, fe& r1, fe& r2, fe& r3, int k, const fe& x0, const fe& y0, const fe& x1, const fe& y1,
+                  const fe& x2, const fe& y2, const fe& x3, const fe& y3) {
+  fe x, y, p;
+  fe_sel4(x, k, x0, x1, x2, x3);
+  fe_sel4(y, k, y0, y1, y2, y3);
+  fe_mul(p, x, y);
+  fe_bcast(r0, p, 0);
+  fe_bcast(r1, p, 1);
+  fe_bcast(r2, p, 2);
+  fe_bcast(r3, p, 3);
+}
+// p1p1 of 2P from projective P (ge_p2_dbl with the four squarings spread)
+COA_DEV void dbl4(ge_p1p1& r, const ge_p2& p, int k) {
+  fe s, xx, yy, zz, aa;
+  fe_add(s, p.X, p.Y);
+  mul4(xx, yy, zz, aa, k, p.X, p.X, p.Y, p.Y, p.Z, p.Z, s, s);
+  fe_add(zz, zz, zz);
+  fe_add(r.Y, yy, xx);
+  fe_sub(r.Z, yy, xx);
+  fe_sub(r.X, aa, r.Y);
+  fe_sub(r.T, zz, r.Z);
+}
+COA_DEV void to_p3_4(ge_p3& r, const ge_p1p1& p, int k) {
+  mul4(r.X, r.Y, r.Z, r.T, k, p.X, p.T, p.Y, p.Z, p.Z, p.T, p.X, p.Y);
+}
+COA_DEV void to_p2_4(ge_p2& r, const ge_p1p1& p, int k) {
+  fe unused;
+  mul4(r.X, r.Y, r.Z, unused, k, p.X, p.T, p.Y, p.Z, p.Z, p.T, p.Z, p.T);
+}
+COA_DEV void add4(ge_p1p1& r, const ge_p3& p, const ge_cached& q, int k) {
+  fe ypx, ymx, a, b, c, zz;
+  fe_add(ypx, p.Y, p.X);
+  fe_sub(ymx, p.Y, p.X);
+  mul4(b, a, c, zz, k, ypx, q.YplusX, ymx, q.YminusX, q.T2d, p.T, p.Z, q.Z);
+  fe_add(zz, zz, zz);
+  fe_sub(r.X, b, a);
+  fe_add(r.Y, b, a);
+  fe_add(r.Z, zz, c);
+  fe_sub(r.T, zz, c);
+}
+}  // namespace
+
+__global__ void __launch_bounds__(64) k_msm_final(const uint32_t* __restrict__ wsum, const uint32_t* __restrict__ bad,
+                                                  uint8_t* __restrict__ verdict) {
+  __shared__ uint32_t cw[WA * 32];  // cached form of every window sum
+  const int t = threadIdx.x;
+  if (t < WA) {
+    ge_p3 p;
+    gbl_get(p, wsum + (uint64_t)t * 32);
+    ge_cached c;
+    ge_p3_to_cached(c, p);
+    const fe* f[4] = {&c.YplusX, &c.YminusX, &c.Z, &c.T2d};
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int i = 0; i < 8; i++) cw[t * 32 + q * 8 + i] = f[q]->v[i];
+  }
+  __syncthreads();
+  const int k = t & 3;
+  ge_p3 top;
+  gbl_get(top, wsum + (uint64_t)(WA - 1) * 32);
+  ge_p2 acc;
+  ge_p3_to_p2(acc, top);
+  ge_p1p1 r;
+#pragma unroll 1
+  for (int w = WA - 2; w >= 0; w--) {
+#pragma unroll 1
+    for (int j = 0; j < COA_MSM_C - 1; j++) {
+      dbl4(r, acc, k);
+      to_p2_4(acc, r, k);
+    }
+    dbl4(r, acc, k);
+    ge_p3 a3;
+    to_p3_4(a3, r, k);
+    ge_cached c;
+    fe* f[4] = {&c.YplusX, &c.YminusX, &c.Z, &c.T2d};
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int i = 0; i < 8; i++) f[q]->v[i] = cw[w * 32 + q * 8 + i];
+    add4(r, a3, c, k);
+    to_p2_4(acc, r, k);
+  }
+  if (t == 0) verdict[0] = (ge_p2_is_identity(acc) && bad[0] == 0) ? 0 : 1;
+}
+
+// ----------------------------------------------------------------- host
+uint32_t coa_msm_chunks_run(size_t n, uint32_t run) {
+  const size_t np = 2 * n + 1, chunk = 256 * (size_t)run;
+  return (uint32_t)((np + chunk - 1) / chunk);
+}
+
+namespace {
+size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
+}  // namespace
+
+uint32_t coa_msm_run(size_t n);
+
+// Sized for the run length coa_msm_run(n) picks now (COA_MSM_RUN read at
+// this call); coa_launch_msm refuses a workspace too small for its run.
+size_t coa_msm_ws_bytes(size_t n) {
+  const size_t np = 2 * n + 1;
+  const size_t nc = coa_msm_chunks_run(n, coa_msm_run(n));
+  return al(n * 32) + al(n * 16) + al(np * 96) + al((size_t)WA * np * 2) + al(COA_MSM_PREP_BLOCKS * 36) +
+         al((size_t)WA * nc * 128) + al((size_t)WA * 128) + al(16) + al((size_t)WA * nc * 512 * 128);
+}
+
+MsmWs coa_msm_ws_carve(void* base, size_t n) {
+  const size_t np = 2 * n + 1;
+  const size_t nc = coa_msm_chunks_run(n, coa_msm_run(n));
+  char* p = static_cast<char*>(base);
+  MsmWs w;
+  w.nchunks_cap = (uint32_t)nc;
+  w.k = reinterpret_cast<uint32_t*>(p);
+  p += al(n * 32);
+  w.z = reinterpret_cast<uint32_t*>(p);
+  p += al(n * 16);
+  w.pts = reinterpret_cast<uint32_t*>(p);
+  p += al(np * 96);
+  w.dig = reinterpret_cast<int16_t*>(p);
+  p += al((size_t)WA * np * 2);
+  w.zpart = reinterpret_cast<uint32_t*>(p);
+  p += al(COA_MSM_PREP_BLOCKS * 36);
+  w.part = reinterpret_cast<uint32_t*>(p);
+  p += al((size_t)WA * nc * 128);
+  w.wsum = reinterpret_cast<uint32_t*>(p);
+  p += al((size_t)WA * 128);
+  w.bad = reinterpret_cast<uint32_t*>(p);
+  p += al(16);
+  w.segs = reinterpret_cast<uint32_t*>(p);
+  return w;
+}
+
+// Sorted entries per lane: 128 (32,768 points per workgroup) once that still
+// gives >= 512 bucket workgroups (two per CU), else fewer (down to 16) so
+// small batches fill the 256 CUs.  COA_MSM_RUN overrides (A/B runs).
+uint32_t coa_msm_run(size_t n) {
+  const char* e = getenv("COA_MSM_RUN");
+  if (e) {
+    const int r = atoi(e);
+    if (r == 16 || r == 32 || r == 64 || r == 128) return (uint32_t)r;
+  }
+  for (uint32_t run = MAXRUN; run > 16; run >>= 1) {
+    const size_t chunk = 256 * (size_t)run;
+    const size_t heavy = ((2 * n + chunk - 1) / chunk) * WR + ((n + chunk - 1) / chunk) * (WA - WR);
+    if (heavy >= 512) return run;
+  }
+  return 16;
+}
+
+uint32_t coa_msm_chunks(size_t n) { return coa_msm_chunks_run(n, coa_msm_run(n)); }
+
+hipError_t coa_launch_msm(const uint8_t* pks, const uint8_t* sigs, uint32_t n, const MsmWs& ws, uint8_t* verdict,
+                          hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t np = 2 * n + 1;
+  const uint32_t run = coa_msm_run(n);
+  const uint32_t nc = coa_msm_chunks_run(n, run);
+  if (nc > ws.nchunks_cap) return hipErrorInvalidValue;  // COA_MSM_RUN changed since the workspace was sized
+  hipError_t e = hipMemsetAsync(ws.bad, 0, 4, s);
+  if (e != hipSuccess) return e;
+  uint32_t pb = (n + 255) / 256;
+  if (pb > COA_MSM_PREP_BLOCKS) pb = COA_MSM_PREP_BLOCKS;
+  hipLaunchKernelGGL(k_msm_prep, dim3(pb), dim3(256), 0, s, pks, sigs, ws.k, ws.z, n, np, ws.pts, ws.dig, ws.zpart,
+                     ws.bad);
+  hipLaunchKernelGGL(k_msm_bpoint, dim3(1), dim3(256), 0, s, ws.zpart, pb, n, np, ws.pts, ws.dig);
+  const uint32_t g8 = (nc * WA + 7) & ~7u;
+  hipLaunchKernelGGL(k_msm_bucket, dim3(g8), dim3(256), 0, s, ws.pts, ws.dig, n, np, run, nc, ws.segs,
+                     ws.part);
+  hipLaunchKernelGGL(k_msm_wsum, dim3(WA), dim3(256), 0, s, ws.part, nc, ws.wsum);
+  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, ws.wsum, ws.bad, verdict);
+  return hipGetLastError();
+}

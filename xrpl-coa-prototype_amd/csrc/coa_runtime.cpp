@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "coa_batch.h"
+#include "coa_msm.h"
 #include "coa_committee.h"
 #include "coa_halved.h"
 #include "coa_kernels.h"
@@ -100,13 +101,14 @@ struct Dev {
   DevBuf msgs, pks, sigs, kbuf, rec, verdicts, scratch, aux, rbuf, seeds, offs, data, out, idx, zs, terms, flags;
   // committee key cache (f2): sorted keys, flags, one comb of -A per key
   DevBuf ckeys, kflags, ktabs, kwtabs, cert, cscr;
+  DevBuf msm;  // Pippenger workspace (one large verify_batch group)
   bool kwide = false;  // kwtabs holds the committee's wide combs
   uint32_t nkeys = 0;
   PinBuf pin;
   std::mutex mu;
   std::vector<DevBuf*> all() {
     return {&msgs,  &pks,  &sigs, &kbuf, &rec, &verdicts, &scratch, &aux,  &rbuf,   &seeds, &offs,
-            &data,  &out,  &idx,  &zs,   &terms, &flags,  &ckeys,   &kflags, &ktabs, &kwtabs, &cert, &cscr};
+            &data,  &out,  &idx,  &zs,   &terms, &flags,  &ckeys,   &kflags, &ktabs, &kwtabs, &cert, &cscr, &msm};
   }
 };
 
@@ -339,8 +341,84 @@ uint64_t os_entropy_seed() {
   return s;
 }
 
+// Groups of at least msm_min() signatures take the Pippenger path
+// (coa_msm.hip); COA_MSM_MIN overrides (0 = never).
+size_t msm_min() {
+  const char* e = getenv("COA_MSM_MIN");
+  return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)16384;
+}
+
+// One group through the Pippenger kernels, device buffers resident.
+// d_zs: caller weights (16 B per signature) or NULL = derive from seed.
+int enqueue_msm(Dev& d, const uint8_t* d_msg, const uint8_t* d_pks, const uint8_t* d_sigs, size_t n,
+                const uint8_t* d_zs, uint64_t seed, uint32_t group, uint8_t* d_verdict, void* ws_base,
+                hipStream_t s) {
+  const MsmWs ws = coa_msm_ws_carve(ws_base, n);
+  HIP_TRY(coa_launch_hram(d_msg, 32, 0, nullptr, d_pks, d_sigs, (uint32_t)n, ws.k, s));
+  if (d_zs) HIP_TRY(hipMemcpyAsync(ws.z, d_zs, n * 16, hipMemcpyDeviceToDevice, s));
+  else HIP_TRY(coa_launch_batch_z(ws.k, d_sigs, nullptr, group, (uint32_t)n, seed, ws.z, s));
+  HIP_TRY(coa_launch_msm(d_pks, d_sigs, (uint32_t)n, ws, d_verdict, s));
+  return COA_OK;
+}
+
+// Host-pointer form for one group on device d (lock held by the caller).
+int msm_group(Dev& d, const uint8_t* msg, const uint8_t* pks, const uint8_t* sigs, size_t n, const uint8_t* zs_in,
+              uint64_t seed, uint32_t group, uint8_t* verdict_out) {
+  hipStream_t s = d.stream;
+  HIP_TRY(d.msgs.ensure(32));
+  HIP_TRY(d.pks.ensure(n * 32 + 32));
+  HIP_TRY(d.sigs.ensure(n * 64 + 64));
+  HIP_TRY(d.verdicts.ensure(16));
+  HIP_TRY(d.msm.ensure(coa_msm_ws_bytes(n)));
+  if (zs_in) HIP_TRY(d.zs.ensure(n * 16 + 16));
+  HIP_TRY(hipMemcpyAsync(d.msgs.p, msg, 32, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d.pks.p, pks, n * 32, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d.sigs.p, sigs, n * 64, hipMemcpyHostToDevice, s));
+  if (zs_in) HIP_TRY(hipMemcpyAsync(d.zs.p, zs_in, n * 16, hipMemcpyHostToDevice, s));
+  const int rc = enqueue_msm(d, d.msgs.as<uint8_t>(), d.pks.as<uint8_t>(), d.sigs.as<uint8_t>(), n,
+                             zs_in ? d.zs.as<uint8_t>() : nullptr, seed, group, d.verdicts.as<uint8_t>(), d.msm.p, s);
+  if (rc != COA_OK) return rc;
+  HIP_TRY(hipMemcpyAsync(verdict_out, d.verdicts.p, 1, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return COA_OK;
+}
+
 int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, const uint64_t* group_offsets,
-                      size_t n_groups, const uint8_t* zs_in, uint64_t seed, uint8_t* verdicts_out) {
+                      size_t n_groups, const uint8_t* zs_in, uint64_t seed, uint8_t* verdicts_out,
+                      uint32_t gbase = 0);
+
+// Large groups one by one through the Pippenger path (devices round-robin),
+// runs of small groups through the per-vote path.
+int batch_groups_split(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, const uint64_t* group_offsets,
+                       size_t n_groups, const uint8_t* zs_in, uint64_t seed, uint8_t* verdicts_out, size_t mmin) {
+  size_t g = 0, nlarge = 0;
+  while (g < n_groups) {
+    size_t e = g;
+    while (e < n_groups && group_offsets[e + 1] - group_offsets[e] < mmin) e++;
+    if (e > g) {
+      const uint64_t v0 = group_offsets[g];
+      std::vector<uint64_t> offs(e - g + 1);
+      for (size_t k = 0; k <= e - g; k++) offs[k] = group_offsets[g + k] - v0;
+      const int rc = batch_groups_impl(msgs + g * 32, pks + v0 * 32, sigs + v0 * 64, offs.data(), e - g,
+                                       zs_in ? zs_in + v0 * 16 : nullptr, seed, verdicts_out + g, (uint32_t)g);
+      if (rc != COA_OK) return rc;
+      g = e;
+      continue;
+    }
+    const uint64_t v0 = group_offsets[g], nv = group_offsets[g + 1] - v0;
+    Dev& d = *g_devs[nlarge++ % g_devs.size()];
+    std::lock_guard<std::mutex> l(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    const int rc = msm_group(d, msgs + g * 32, pks + v0 * 32, sigs + v0 * 64, nv, zs_in ? zs_in + v0 * 16 : nullptr,
+                             seed, (uint32_t)g, verdicts_out + g);
+    if (rc != COA_OK) return rc;
+    g++;
+  }
+  return COA_OK;
+}
+
+int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, const uint64_t* group_offsets,
+                      size_t n_groups, const uint8_t* zs_in, uint64_t seed, uint8_t* verdicts_out, uint32_t gbase) {
   if (n_groups == 0) return COA_OK;
   if (!msgs || !group_offsets || !verdicts_out) return fail(COA_EINVAL, "null argument");
   if (group_offsets[0] != 0) return fail(COA_EINVAL, "group_offsets[0] must be 0");
@@ -350,6 +428,12 @@ int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* si
   if (total && (!pks || !sigs)) return fail(COA_EINVAL, "null pks/sigs");
   if (check_n(total) != COA_OK) return COA_EINVAL;
   const uint64_t eff_seed = zs_in ? 0 : (seed ? seed : os_entropy_seed());
+  const size_t mmin = msm_min();
+  if (mmin) {
+    for (size_t g = 0; g < n_groups; g++)
+      if (group_offsets[g + 1] - group_offsets[g] >= mmin)
+        return batch_groups_split(msgs, pks, sigs, group_offsets, n_groups, zs_in, eff_seed, verdicts_out, mmin);
+  }
   // shard by group index
   return for_shards(n_groups, [&](Dev& d, size_t glo, size_t ghi) -> int {
     const size_t vlo = group_offsets[glo], vhi = group_offsets[ghi];
@@ -388,9 +472,9 @@ int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* si
     } else {
       // z derivation binds the global group index: restore it for the hash
       std::vector<uint32_t> gabs(group_of.size());
-      for (size_t i = 0; i < group_of.size(); i++) gabs[i] = group_of[i] + (uint32_t)glo;
+      for (size_t i = 0; i < group_of.size(); i++) gabs[i] = group_of[i] + (uint32_t)glo + gbase;
       HIP_TRY(hipMemcpyAsync(d.idx.p, gabs.data(), gabs.size() * 4, hipMemcpyHostToDevice, s));
-      HIP_TRY(coa_launch_batch_z(d.kbuf.as<uint32_t>(), d.sigs.as<uint8_t>(), d.idx.as<uint32_t>(), (uint32_t)nv,
+      HIP_TRY(coa_launch_batch_z(d.kbuf.as<uint32_t>(), d.sigs.as<uint8_t>(), d.idx.as<uint32_t>(), 0, (uint32_t)nv,
                                  eff_seed, d.zs.as<uint32_t>(), s));
       HIP_TRY(hipStreamSynchronize(s));  // gabs lifetime
     }
@@ -788,6 +872,33 @@ int coa_ed25519_verify_batch_groups_z(const uint8_t* msgs, const uint8_t* pks, c
   if (!zs && n_groups && group_offsets && group_offsets[n_groups]) return fail(COA_EINVAL, "null zs");
   static const uint8_t zero16[16] = {0};
   return batch_groups_impl(msgs, pks, sigs, group_offsets, n_groups, zs ? zs : zero16, 0, group_verdicts_out);
+}
+
+size_t coa_verify_batch_workspace_bytes(size_t n) { return coa_msm_ws_bytes(n); }
+
+int coa_ed25519_verify_batch_device(int device, const uint8_t* d_msg, const uint8_t* d_pks, const uint8_t* d_sigs,
+                                    size_t n, const uint8_t* d_zs, uint64_t rng_seed, uint8_t* d_verdict,
+                                    void* workspace, void* stream) {
+  int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  if (!d_msg || !d_verdict || (n && (!d_pks || !d_sigs))) return fail(COA_EINVAL, "null argument");
+  if (check_n(n) != COA_OK) return COA_EINVAL;
+  Dev* d = dev_by_id(device);
+  if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  if (n == 0) {  // empty batch: the equation is [0]B = O, Ok (as dalek)
+    HIP_TRY(hipMemsetAsync(d_verdict, 0, 1, s));
+    return COA_OK;
+  }
+  const uint64_t seed = d_zs ? 0 : (rng_seed ? rng_seed : os_entropy_seed());
+  if (workspace) return enqueue_msm(*d, d_msg, d_pks, d_sigs, n, d_zs, seed, 0, d_verdict, workspace, s);
+  std::lock_guard<std::mutex> l(d->mu);
+  HIP_TRY(d->msm.ensure(coa_msm_ws_bytes(n)));
+  rc = enqueue_msm(*d, d_msg, d_pks, d_sigs, n, d_zs, seed, 0, d_verdict, d->msm.p, s);
+  if (rc != COA_OK) return rc;
+  HIP_TRY(hipStreamSynchronize(s));
+  return COA_OK;
 }
 
 int coa_ed25519_verify_batch(const uint8_t msg[32], const uint8_t* pks, const uint8_t* sigs, size_t n,
