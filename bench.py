@@ -23,6 +23,8 @@ Also reported:
   cpu_baseline  the C restatement of dalek's algorithms (oracle/, "port")
                 on this host's cores, rank 0 at N=1 only, on a bounded sample.
   secondary     (rank 0, N=1) one C5 shard (2^21 triples) per verify call;
+                verify_batch through the Pippenger kernels (one 2^21-signature
+                group; one certificate's 67 votes, p50 beside the CPU);
                 C4 worker-batch SHA-512 GB/s; C3 and C1
                 Certificate::verify -- certificates/s for a round resident in
                 HBM and p50/p99 latency of one certificate through the
@@ -209,6 +211,96 @@ def c5_shard(local, dev, stream, n=1 << 21, steps=3):
             "ms_per_call": round(ms, 3), "verifications_per_s": round(n / (ms * 1e-3), 1),
             "frac": round(ALG_INT32_OPS_PER_VERIFY * n / (ms * 1e-3) / 1e12 / PEAK_INT32_TOPS, 4),
             "verdicts_ok": ok}
+
+
+def batch_alg_int32_ops(n):
+    """SURVEY.md 8(d) W_batch(n): 2n decompressions (276 field ops each),
+    Pippenger with c = 5 over 2n + 1 (+32) points (9 field ops per addition,
+    51 windows) and 253 doublings (8 each), x 200 INT32 ops per field op."""
+    return (2 * n * 276 + 9 * 51 * (2 * n + 1 + 32) + 8 * 253) * INT32_OPS_PER_FIELD_OP
+
+
+def verify_batch_config(local, dev, stream, n_large=1 << 21, n_cert=67, samples=300, cpu_samples=30):
+    """Signature::verify_batch (crypto/src/lib.rs:206-219) through the
+    Pippenger kernels (csrc/coa_msm.hip), uncached keys:
+      large_group       ONE batch equation over n_large signatures resident in
+                        HBM (coa_ed25519_verify_batch_device), HIP events;
+                        frac against the VALU peak with SURVEY 8(d)'s W_batch
+      single_group      one certificate's 67 votes through the host-pointer
+                        C ABI (coa_ed25519_verify_batch: H2D + kernels + D2H),
+                        p50/p99, beside the C restatement of dalek's
+                        verify_batch (Straus, as dalek below 190 points) on
+                        one core."""
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coa_crypto
+    import coa_oracle
+    import workloads
+
+    coa_oracle.build()
+    out = {}
+    n = n_large
+    m = torch.from_numpy(np.tile(workloads.messages(1), (n, 1))).to(dev)
+    seeds = torch.from_numpy(workloads.key_seeds(n)).to(dev)
+    pks = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    sigs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    coa_crypto.sign_many_device(local, seeds, m, pks, sigs, stream=stream)
+    msg = m[0].contiguous()
+    del seeds, m
+    verdict = torch.ones(1, dtype=torch.uint8, device=dev)
+    ws = torch.empty(coa_crypto.verify_batch_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    coa_crypto.verify_batch_device(local, msg, pks, sigs, verdict, rng_seed=11, workspace=ws, stream=stream)
+    torch.cuda.synchronize()
+    steps = 3
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        coa_crypto.verify_batch_device(local, msg, pks, sigs, verdict, rng_seed=11, workspace=ws, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    out["large_group"] = {
+        "workload": f"one verify_batch group of {n:,} signatures (one message), HBM-resident, Pippenger",
+        "ms_per_call": round(ms, 3), "signatures_per_s": round(n / (ms * 1e-3), 1),
+        "alg_int32_ops": batch_alg_int32_ops(n),
+        "frac": round(batch_alg_int32_ops(n) / (ms * 1e-3) / 1e12 / PEAK_INT32_TOPS, 4),
+        "verdict_ok": int(verdict.item()) == 0}
+    del pks, sigs, ws, verdict
+    torch.cuda.empty_cache()
+
+    # one certificate's votes, host pointers (the Rust shim's call)
+    mh = workloads.messages(1)
+    seeds_h = workloads.key_seeds(n_cert, start=1000)
+    pk_h, sg_h = coa_crypto.sign_many(seeds_h, np.tile(mh, (n_cert, 1)))
+    offs = np.array([0, n_cert], np.uint64)
+    lat = []
+    for i in range(samples + 20):
+        t0 = time.perf_counter()
+        v = coa_crypto.verify_batch_groups(mh, pk_h, sg_h, offs, rng_seed=0)
+        lat.append(time.perf_counter() - t0)
+        assert int(v[0]) == 0
+    lat = np.array(lat[20:]) * 1e3
+    rng = np.random.default_rng(5)
+    zs = [int.from_bytes(rng.bytes(16), "little") for _ in range(n_cert)]
+    pl, sl = [bytes(r) for r in pk_h], [bytes(r) for r in sg_h]
+    cl = []
+    for _ in range(cpu_samples):
+        t0 = time.perf_counter()
+        ok = coa_oracle.verify_batch(bytes(mh[0]), pl, sl, zs)
+        cl.append(time.perf_counter() - t0)
+        assert ok
+    cpu_p50 = float(np.percentile(np.array(cl) * 1e3, 50))
+    out["single_group"] = {
+        "workload": f"verify_batch of one certificate's {n_cert} votes, host pointers in, verdict out",
+        "path": "Pippenger (a one-group call routes there at any size)",
+        "p50_ms": round(float(np.percentile(lat, 50)), 3), "p99_ms": round(float(np.percentile(lat, 99)), 3),
+        "samples": samples,
+        "cpu_baseline": {"p50_ms": round(cpu_p50, 3), "cores": 1, "kind": "port",
+                         "sample": f"{cpu_samples} calls of the C restatement of dalek verify_batch, single thread"},
+        "p50_vs_cpu": round(cpu_p50 / float(np.percentile(lat, 50)), 2)}
+    return out
 
 
 def c4_sha512(local, dev, stream, counts, steps, cpu_threads):
@@ -455,6 +547,7 @@ def main():
         torch.cuda.empty_cache()
         secondary = {
             "c5_shard": c5_shard(local, dev, stream),
+            "verify_batch": verify_batch_config(local, dev, stream),
             "c4_sha512": c4_sha512(local, dev, stream, [int(x) for x in args.c4_batches.split(",") if x], 2,
                                    threads),
             "c3_certificate_verify": certificate_config(args.c3_certs, 1000, threads, dev, stream),

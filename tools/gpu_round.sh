@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 STEPS="${1:-tests,smoke,bench,prof}"
 run() { echo "== $1" ; }
 if [[ $STEPS == *tests* ]]; then
-  run tests && timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 \
+  run tests && timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 \
     || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
   tail -3 gpurun_out/pytest_gpu.log
 fi

@@ -13,9 +13,9 @@
 // R_i, 29 for the 253-bit scalars of A_i and B.
 //
 // Kernels:
-//   k_msm_prep    one lane per signature: encoding checks, decompression of
-//                 A_i and R_i to Niels form, z h mod l, digits, block partial
-//                 sums of z s (288-bit integers)
+//   k_msm_prep    two lanes per signature (A_i on one, R_i on the other):
+//                 encoding checks, decompression to Niels form, z h mod l,
+//                 digits, block partial sums of z s (288-bit integers)
 //   k_msm_bpoint  one workgroup: b = -(sum z s) mod l, B and its digits
 //   k_msm_bucket  one workgroup per (chunk of 256·run points, window):
 //                 LDS counting sort of the chunk's points by |digit|; every
@@ -191,47 +191,62 @@ __global__ void __launch_bounds__(256) k_msm_prep(const uint8_t* __restrict__ pk
   __shared__ uint32_t red[9 * 256];
   uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    uint32_t aw[8], rw[8], sw[8], hw[8], z[8];
-    const uint32_t* pk = reinterpret_cast<const uint32_t*>(pks + (uint64_t)i * 32);
-    const uint32_t* sg = reinterpret_cast<const uint32_t*>(sigs + (uint64_t)i * 64);
+  // Two lanes per signature: lane 2i decompresses A_i and recodes z_i h_i,
+  // lane 2i+1 decompresses R_i, checks s_i and recodes z_i.  The two
+  // decompressions (the long dependent chains) run side by side, so a small
+  // batch waits for one of them, not both.
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < 2 * n; j += stride) {
+    const uint32_t i = j >> 1;
+    const bool is_r = (j & 1) != 0;
+    uint32_t enc[8], z[8];
+    const uint32_t* src = is_r ? reinterpret_cast<const uint32_t*>(sigs + (uint64_t)i * 64)
+                               : reinterpret_cast<const uint32_t*>(pks + (uint64_t)i * 32);
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      aw[j] = pk[j];
-      rw[j] = sg[j];
-      sw[j] = sg[8 + j];
-      hw[j] = kbuf[(uint64_t)i * 8 + j];
-      z[j] = j < 4 ? zs[(uint64_t)i * 4 + j] : 0;
+    for (int w = 0; w < 8; w++) {
+      enc[w] = src[w];
+      z[w] = w < 4 ? zs[(uint64_t)i * 4 + w] : 0;
     }
-    bool ok = sc_is_canonical(sw);
     ge_p3 P;
-    ok = ge_decompress(P, aw) && ok;
-    niels_store(pts + (uint64_t)(n + i) * 24, P);
-    ok = ge_decompress(P, rw) && ok;
-    niels_store(pts + (uint64_t)i * 24, P);
-    if (!ok) atomicOr(bad, 1u);
-    sc a, zsv;
-    sc_mul(a, z, hw);
-    sc_mul(zsv, z, sw);
-    if (!ok) {
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        a.v[j] = 0;
-        z[j] = 0;
-        zsv.v[j] = 0;
-      }
-    }
+    bool ok = ge_decompress(P, enc);
+    niels_store(pts + (uint64_t)(is_r ? i : n + i) * 24, P);
     int d[WA];
-    recode<WR>(d, z);
+    if (is_r) {
+      uint32_t sw[8];
+      const uint32_t* sg = reinterpret_cast<const uint32_t*>(sigs + (uint64_t)i * 64);
 #pragma unroll
-    for (int w = 0; w < WR; w++) dig[(uint64_t)w * np + i] = (int16_t)d[w];
-    recode<WA>(d, a.v);
+      for (int w = 0; w < 8; w++) sw[w] = sg[8 + w];
+      ok = sc_is_canonical(sw) && ok;
+      sc zsv;
+      sc_mul(zsv, z, sw);
+      if (!ok) {
 #pragma unroll
-    for (int w = 0; w < WA; w++) dig[(uint64_t)w * np + n + i] = (int16_t)d[w];
-    uint32_t cy = 0;
+        for (int w = 0; w < 8; w++) {
+          z[w] = 0;
+          zsv.v[w] = 0;
+        }
+      }
+      recode<WR>(d, z);
 #pragma unroll
-    for (int j = 0; j < 8; j++) acc[j] = addc32(acc[j], zsv.v[j], cy, cy);
-    acc[8] += cy;
+      for (int w = 0; w < WR; w++) dig[(uint64_t)w * np + i] = (int16_t)d[w];
+      uint32_t cy = 0;
+#pragma unroll
+      for (int w = 0; w < 8; w++) acc[w] = addc32(acc[w], zsv.v[w], cy, cy);
+      acc[8] += cy;
+    } else {
+      uint32_t hw[8];
+#pragma unroll
+      for (int w = 0; w < 8; w++) hw[w] = kbuf[(uint64_t)i * 8 + w];
+      sc a;
+      sc_mul(a, z, hw);
+      if (!ok) {
+#pragma unroll
+        for (int w = 0; w < 8; w++) a.v[w] = 0;
+      }
+      recode<WA>(d, a.v);
+#pragma unroll
+      for (int w = 0; w < WA; w++) dig[(uint64_t)w * np + n + i] = (int16_t)d[w];
+    }
+    if (!ok) atomicOr(bad, 1u);
   }
   // block partial of sum z s (288-bit, no reduction)
   const int t = threadIdx.x;
@@ -640,7 +655,7 @@ hipError_t coa_launch_msm(const uint8_t* pks, const uint8_t* sigs, uint32_t n, c
   if (nc > ws.nchunks_cap) return hipErrorInvalidValue;  // COA_MSM_RUN changed since the workspace was sized
   hipError_t e = hipMemsetAsync(ws.bad, 0, 4, s);
   if (e != hipSuccess) return e;
-  uint32_t pb = (n + 255) / 256;
+  uint32_t pb = (2 * n + 255) / 256;
   if (pb > COA_MSM_PREP_BLOCKS) pb = COA_MSM_PREP_BLOCKS;
   hipLaunchKernelGGL(k_msm_prep, dim3(pb), dim3(256), 0, s, pks, sigs, ws.k, ws.z, n, np, ws.pts, ws.dig, ws.zpart,
                      ws.bad);
