@@ -77,6 +77,7 @@ def lib():
         "coa_shutdown": ([], ctypes.c_int),
         "coa_device_count": ([], ctypes.c_int),
         "coa_self_test": ([ctypes.c_int, P64], ctypes.c_int),
+        "coa_fe_rows_check_device": ([ctypes.c_int, vp, sz, vp, vp], ctypes.c_int),
         "coa_last_error": ([], ctypes.c_char_p),
         "coa_version": ([], ctypes.c_char_p),
         "coa_ed25519_verify_strict": ([P8, P8, P8], ctypes.c_int),
@@ -410,6 +411,15 @@ def _handle(device, stream):
     if stream is None:
         stream = torch.cuda.current_stream(device)
     return stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+
+
+def fe_rows_check_device(device, values, out, stream=None):
+    """Row-parallel field arithmetic self-test: values uint8 [n, 32] on the
+    device, out int32 [n] on the device (0 = every row-parallel result equals
+    the one-lane result for that input)."""
+    n = values.shape[0]
+    assert values.is_contiguous() and tuple(values.shape) == (n, 32) and out.numel() >= n
+    _check(lib().coa_fe_rows_check_device(device, values.data_ptr(), n, out.data_ptr(), _handle(device, stream)))
 
 
 def challenge_many_device(device, msgs, pks, sigs, k_out, stream=None):

@@ -63,3 +63,9 @@ hipError_t coa_launch_key_wcombs(const uint32_t* tabs, uint32_t nk, uint32_t* wt
 // variant only; may be null for lanes_per_sig == 64).
 size_t coa_cert_scratch_bytes(uint64_t jobs);
 hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr, hipStream_t s);
+
+// Row-parallel field arithmetic (coa_fe_wave.h) against coa_fe.h, one wave per
+// input x_i (32 LE bytes, any value < 2^256): out[i] bit0 pow_p58, bit1
+// invert, bit2 x_i * x_{i+1}, bit3 decompression of x_i as an encoding
+// (verdict and coordinates) differ.
+hipError_t coa_launch_fe_rows_check(const uint8_t* in, uint32_t n, uint32_t* out, hipStream_t s);

@@ -40,11 +40,14 @@
 //                      set of signatures (64 serial mixed additions each), P
 //                      compared with R's encoding after one inversion shared
 //                      by the lane's signatures; one lane per header digest
-//   k_cert_verify_lat  latency: one 128-thread workgroup per signature --
+//   k_cert_verify_lat  latency: one 192-thread workgroup per signature --
 //                      wave 0 hashes Certificate::digest and k, takes one
-//                      comb term per lane, sums the 64 terms by a 6-level
-//                      xor butterfly and tests P for small order, while
-//                      wave 1 decompresses R; the two meet in LDS.  One
+//                      term of [k](-A)'s comb per lane (32 lanes) and sums
+//                      them by a 5-level xor butterfly; wave 2 does the same
+//                      for [s]B meanwhile (it needs no hash); wave 1
+//                      decompresses R on DPP rows (coa_fe_wave.h).  The
+//                      three meet in LDS: P = both halves, small-order test,
+//                      compare with R.  One
 //                      workgroup per header digest: its lanes expand every
 //                      block's message schedule into LDS, then one wave
 //                      runs the rounds (coa_sha512.h, compress_kw).
@@ -489,7 +492,7 @@ __global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a, uint32_t* __
 // Blocks [0, nc): header digests (wave 0 of each).  Blocks [nc, 2nc + nv):
 // one signature job each.
 #define KW_CHUNK 64  // blocks of schedule per LDS pass (40 KiB)
-__global__ void __launch_bounds__(128) k_cert_verify_lat(CertArgs a) {
+__global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
   const uint32_t wave = coa_sha::uni(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   if (blockIdx.x < a.nc) {  // header digest: schedule in parallel, rounds on wave 0
@@ -526,6 +529,7 @@ __global__ void __launch_bounds__(128) k_cert_verify_lat(CertArgs a) {
     return;
   }
   __shared__ uint32_t r_lds[17];  // R.X, R.Y, decompress ok
+  __shared__ uint32_t s_lds[32];  // [s]B from wave 2
   const uint32_t job = blockIdx.x - a.nc;
   const bool hdr = job < a.nc;
   const uint32_t vi = job - a.nc;
@@ -535,9 +539,9 @@ __global__ void __launch_bounds__(128) k_cert_verify_lat(CertArgs a) {
   load8u(rw, sig);
   uint32_t bits = 0;
   ge_p3 P;
-  if (wave == 1) {  // R's decompression
+  if (wave == 1) {  // R's decompression, the power chain on the wave's DPP rows
     ge_p3 R;
-    const bool ok = ge_decompress(R, rw);
+    const bool ok = ge_decompress<true>(R, rw);
     if (lane == 0) {
 #pragma unroll
       for (int i = 0; i < 8; i++) {
@@ -547,57 +551,72 @@ __global__ void __launch_bounds__(128) k_cert_verify_lat(CertArgs a) {
       r_lds[16] = ok;
     }
   } else {
-    uint32_t pk[8], sw[8], msg[8];
-    load8u(pk, hdr ? a.origins + (uint64_t)c * 8 : a.vpks + (uint64_t)vi * 8);
-    load8u(sw, sig + 8);
-    load8u(msg, a.ids + (uint64_t)c * 8);
-    const int slot = key_lookup_u(a.keys, a.nk, pk);
-    if (slot < 0) {
-      bits = COA_CST_UNCACHED;
+    // one comb term per lane (lanes 0..31; the upper half sums a copy),
+    // [s]B on wave 2 from B's comb, [k](-A) on wave 0 from the key's comb
+    uint32_t dg[8];
+    const uint32_t* tab = a.comb;
+    int slot = 0;
+    uint32_t pre = 0;
+    if (wave == 2) {
+      load8u(dg, sig + 8);
     } else {
-      uint64_t st[8];
-      uint32_t h[16];
-      if (!hdr) {  // Certificate::digest on the scalar unit
-        uint32_t in[18];
-        const uint64_t rd = uni64(a.rounds[c]);
+      uint32_t pk[8], sw[8], msg[8];
+      load8u(pk, hdr ? a.origins + (uint64_t)c * 8 : a.vpks + (uint64_t)vi * 8);
+      load8u(sw, sig + 8);
+      load8u(msg, a.ids + (uint64_t)c * 8);
+      slot = key_lookup_u(a.keys, a.nk, pk);
+      if (slot < 0) {
+        bits = COA_CST_UNCACHED;
+        slot = 0;
+      } else {
+        uint64_t st[8];
+        uint32_t h[16];
+        if (!hdr) {  // Certificate::digest on the scalar unit
+          uint32_t in[18];
+          const uint64_t rd = uni64(a.rounds[c]);
 #pragma unroll
-        for (int i = 0; i < 8; i++) in[i] = msg[i];
-        in[8] = (uint32_t)rd;
-        in[9] = (uint32_t)(rd >> 32);
-        load8u(in + 10, a.origins + (uint64_t)c * 8);
-        coa_sha::hash_words<18>(st, in);
+          for (int i = 0; i < 8; i++) in[i] = msg[i];
+          in[8] = (uint32_t)rd;
+          in[9] = (uint32_t)(rd >> 32);
+          load8u(in + 10, a.origins + (uint64_t)c * 8);
+          coa_sha::hash_words<18>(st, in);
+          coa_sha::state_to_le_words(h, st);
+#pragma unroll
+          for (int i = 0; i < 8; i++) msg[i] = h[i];
+        }
+        uint32_t in[24];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          in[i] = rw[i];
+          in[8 + i] = pk[i];
+          in[16 + i] = msg[i];
+        }
+        coa_sha::hash_words<24>(st, in);
         coa_sha::state_to_le_words(h, st);
+        sc k;
+        sc_reduce512(k, h);
+        const uint32_t kf = coa_sha::uni(a.kflags[slot]);
+        const bool s_ok = sc_is_canonical(sw);
+        const bool a_ok = (kf & COA_KEY_DECOMPRESSES) != 0;
+        pre = (s_ok ? 0u : 1u) | (a_ok ? 0u : 2u) | ((kf & COA_KEY_SMALL_ORDER) ? 4u : 0u) |
+              ((kf & COA_KEY_TORSION_FREE) ? 0u : 8u);
 #pragma unroll
-        for (int i = 0; i < 8; i++) msg[i] = h[i];
+        for (int i = 0; i < 8; i++) dg[i] = k.v[i];
+        tab = a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS;
       }
-      uint32_t in[24];
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        in[i] = rw[i];
-        in[8 + i] = pk[i];
-        in[16 + i] = msg[i];
-      }
-      coa_sha::hash_words<24>(st, in);
-      coa_sha::state_to_le_words(h, st);
-      sc k;
-      sc_reduce512(k, h);
-      const uint32_t kf = coa_sha::uni(a.kflags[slot]);
-      const bool s_ok = sc_is_canonical(sw);
-      const bool a_ok = (kf & COA_KEY_DECOMPRESSES) != 0;
-      uint32_t dg[8];  // this lane's scalar: s for lanes < 32, k above
-#pragma unroll
-      for (int i = 0; i < 8; i++) dg[i] = lane < 32 ? sw[i] : k.v[i];
+    }
+    if (!(bits & COA_CST_UNCACHED)) {
       add_const_word(dg, 0x80808080u);
       const int j = lane & 31;
       const int e = (int)byte_of(dg, j) - 128;
       ge_niels q;
-      comb_select(q, lane < 32 ? a.comb : a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS, j, e);
+      comb_select(q, tab, j, e);
       ge_p1p1 t;
       ge_p3_identity(P);
       ge_madd(t, P, q);
       ge_p1p1_to_p3(P, t);
 #pragma unroll 1
-      for (int off = 32; off >= 1; off >>= 1) {
+      for (int off = 16; off >= 1; off >>= 1) {
         ge_p3 O;
         shfl_fe<64>(O.X, P.X, off);
         shfl_fe<64>(O.Y, P.Y, off);
@@ -608,18 +627,36 @@ __global__ void __launch_bounds__(128) k_cert_verify_lat(CertArgs a) {
         ge_add(t, P, oc);
         ge_p1p1_to_p3(P, t);
       }
-      // verify_strict's small-order test of R, taken on P: an accepting
-      // verdict needs R == P, and every other verdict is Err already
-      const bool small_p = hdr && ge_is_small_order(P);
-      bits = (s_ok ? 0u : 1u) | (a_ok ? 0u : 2u) | ((kf & COA_KEY_SMALL_ORDER) ? 4u : 0u) |
-             ((kf & COA_KEY_TORSION_FREE) ? 0u : 8u) | (small_p ? 16u : 0u);
-      bits <<= 8;  // pre-verdict flags, resolved after the hand-off
+      if (wave == 2 && lane == 0) {
+        const fe* f[4] = {&P.X, &P.Y, &P.Z, &P.T};
+#pragma unroll
+        for (int q4 = 0; q4 < 4; q4++)
+#pragma unroll
+          for (int i = 0; i < 8; i++) s_lds[q4 * 8 + i] = f[q4]->v[i];
+      }
+      bits = pre << 8;  // pre-verdict flags, resolved after the hand-off
     }
   }
   __syncthreads();
   if (wave == 0) {
     if (!(bits & COA_CST_UNCACHED)) {
-      const uint32_t pre = bits >> 8;
+      uint32_t pre = bits >> 8;
+      {  // P = [s]B + [k](-A)
+        ge_p3 S;
+        fe* f[4] = {&S.X, &S.Y, &S.Z, &S.T};
+#pragma unroll
+        for (int q4 = 0; q4 < 4; q4++)
+#pragma unroll
+          for (int i = 0; i < 8; i++) f[q4]->v[i] = s_lds[q4 * 8 + i];
+        ge_cached sc4;
+        ge_p3_to_cached(sc4, S);
+        ge_p1p1 t;
+        ge_add(t, P, sc4);
+        ge_p1p1_to_p3(P, t);
+      }
+      // verify_strict's small-order test of R, taken on P: an accepting
+      // verdict needs R == P, and every other verdict is Err already
+      if (hdr && ge_is_small_order(P)) pre |= 16u;
       ge_p3 R;
 #pragma unroll
       for (int i = 0; i < 8; i++) {
@@ -717,11 +754,49 @@ hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr,
   a.hdr_blocks = (a.nc + 255) / 256;
   const uint64_t jobs = (uint64_t)a.nc + a.nv;
   if (lanes_per_sig == 64) {  // one workgroup per header digest and per signature
-    hipLaunchKernelGGL(k_cert_verify_lat, dim3((uint32_t)(a.nc + jobs)), dim3(128), 0, s, a);
+    hipLaunchKernelGGL(k_cert_verify_lat, dim3((uint32_t)(a.nc + jobs)), dim3(192), 0, s, a);
     return hipGetLastError();
   }
   const uint64_t lanes = cert_tp_lanes(jobs);
   const uint32_t jpl = (uint32_t)((jobs + lanes - 1) / lanes);
   hipLaunchKernelGGL(k_cert_verify, dim3((uint32_t)(a.hdr_blocks + lanes / 256)), dim3(256), 0, s, a, pscr, jpl);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// coa_fe_rows_check: the row-parallel chains against the one-lane ones.
+__global__ void __launch_bounds__(64) k_fe_rows_check(const uint8_t* __restrict__ in, uint32_t n,
+                                                      uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x;
+  uint32_t w[8], w2[8];
+  load8u(w, reinterpret_cast<const uint32_t*>(in + (uint64_t)i * 32));
+  load8u(w2, reinterpret_cast<const uint32_t*>(in + (uint64_t)((i + 1) % n) * 32));
+  fe x, y;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    x.v[k] = w[k];
+    y.v[k] = w2[k];
+  }
+  uint32_t bad = 0;
+  fe a, b;
+  fe_pow_p58_rows(a, x);
+  fe_pow_p58(b, x);
+  bad |= fe_eq(a, b) ? 0u : 1u;
+  fe_invert_rows(a, x);
+  fe_invert(b, x);
+  bad |= fe_eq(a, b) ? 0u : 2u;
+  fw::to_fe(a, fw::mul(fw::from_fe(x), fw::from_fe(y)));
+  fe_mul(b, x, y);
+  bad |= fe_eq(a, b) ? 0u : 4u;
+  ge_p3 P, Q;
+  const bool ok_r = ge_decompress<true>(P, w);
+  const bool ok_s = ge_decompress(Q, w);
+  if (ok_r != ok_s || (ok_s && !(fe_eq(P.X, Q.X) && fe_eq(P.Y, Q.Y) && fe_eq(P.T, Q.T)))) bad |= 8u;
+  if (threadIdx.x == 0) out[i] = bad;
+}
+
+hipError_t coa_launch_fe_rows_check(const uint8_t* in, uint32_t n, uint32_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fe_rows_check, dim3(n), dim3(64), 0, s, in, n, out);
   return hipGetLastError();
 }

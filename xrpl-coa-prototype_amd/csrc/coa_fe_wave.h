@@ -1,0 +1,173 @@
+// Row-parallel GF(2^255 - 19) arithmetic for latency-bound chains on gfx950.
+//
+// A lone wave issues one VALU instruction every ~5 cycles, so a field
+// squaring done by one lane (176 instructions, coa_fe.h) costs ~900 cycles
+// and the ~254 squarings of a decompression or inversion chain take ~90 us.
+// Here ONE field element is spread over a 16-lane DPP row: lane c of the row
+// holds limb c (32-bit, c < 8; lanes 8..15 hold 0), so a product is
+//   8 row broadcasts of b's limbs (DPP row_newbcast),
+//   7 row shifts of a (DPP row_shr, zero fill),
+//   8 multiply-accumulates per lane (lane c sums column c = sum_k a_{c-k} b_k),
+//   carry normalisation across lanes (row_shr:1 / :2, repeated while any
+//   carry is left), the fold of limbs 8..15 by 2^256 = 38 (mod p) (row_shl:8)
+//   and a second normalisation with limb 8's carry wrapped into limb 0,
+// about 60 instructions on the chain instead of 176-214.  The four rows of a
+// wave are independent: each row computes its own product (the Horner step of
+// k_msm_final runs four different products at once), or all four compute the
+// same one (decompression in the certificate latency kernel).
+//
+// Values are < 2^256 in 8 limbs, not canonical; fw::to_fe returns them in
+// the ordinary (replicated per lane) representation of coa_fe.h, where
+// fe_canon finishes.  Every lane of the wave must execute these functions
+// together (DPP reads other lanes).  Checked against coa_fe.h by
+// coa_fe_rows_check_device (tests/test_gpu_fe_rows.py).
+#pragma once
+#include "coa_fe.h"
+
+namespace fw {
+
+COA_DEV uint32_t row_lane() { return __lane_id() & 15u; }
+
+template <int K>
+COA_DEV uint32_t shr(uint32_t x) {  // lane c of the row gets lane c-K, 0 below the row
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x110 + K, 0xf, 0xf, true);
+}
+template <int K>
+COA_DEV uint32_t shl(uint32_t x) {  // lane c gets lane c+K, 0 past the row
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x100 + K, 0xf, 0xf, true);
+}
+template <int K>
+COA_DEV uint32_t bcast(uint32_t x) {  // every lane of the row gets the row's lane K
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + K, 0xf, 0xf, false);
+}
+
+// Carry propagation of per-lane column values n_c < 2^34 (lanes 0..15) into
+// 32-bit limbs; the value is < 2^512 so nothing leaves lane 15.  Two passes
+// leave carries of 0 or 1 that move on only through 0xffffffff limbs, so the
+// uniform branch to the rippling loop is almost never taken.
+COA_DEV uint32_t carry_step(uint64_t& n) {
+  const uint32_t lo = (uint32_t)n, hi = (uint32_t)(n >> 32);
+  n = (uint64_t)lo + shr<1>(hi);
+  return hi;
+}
+COA_DEV uint32_t norm16(uint64_t n) {
+  carry_step(n);
+  uint32_t hi = carry_step(n);
+#pragma unroll 1
+  while (__any(hi != 0u)) hi = carry_step(n);
+  return (uint32_t)n;
+}
+
+// Limbs l_0..l_15 (value < 2^512) -> 8 limbs of a value < 2^256, congruent mod p.
+// (selects, not branches: lane-dependent ternaries on 64-bit values would
+// become exec-mask branches)
+COA_DEV uint32_t wrap_step(uint64_t& m, uint32_t r) {
+  const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+  const uint32_t h7 = bcast<7>(hi);  // carry out of limb 7 = 2^256 * h7 = 38 * h7
+  const uint32_t sh = shr<1>(hi);
+  uint32_t add = r == 0 ? h7 * 38u : sh;
+  add = r < 8 ? add : 0u;
+  m = (uint64_t)lo + add;
+  return r < 8 ? hi : 0u;
+}
+COA_DEV uint32_t fold(uint32_t l) {
+  const uint32_t r = row_lane();
+  const uint32_t up = shl<8>(l);
+  const uint32_t lk = r < 8 ? l : 0u;  // lanes 8..15 drop out (up is 0 there)
+  uint64_t m = (uint64_t)up * 38u + lk;
+  wrap_step(m, r);
+  uint32_t hi = wrap_step(m, r);
+#pragma unroll 1
+  while (__any(hi != 0u)) hi = wrap_step(m, r);
+  return (uint32_t)m;
+}
+
+// a * b mod p (not canonical), one product per 16-lane row.
+COA_DEV uint32_t mul(uint32_t a, uint32_t b) {
+  uint32_t bk[8], ak[8];
+  bk[0] = bcast<0>(b);
+  bk[1] = bcast<1>(b);
+  bk[2] = bcast<2>(b);
+  bk[3] = bcast<3>(b);
+  bk[4] = bcast<4>(b);
+  bk[5] = bcast<5>(b);
+  bk[6] = bcast<6>(b);
+  bk[7] = bcast<7>(b);
+  ak[0] = a;
+  ak[1] = shr<1>(a);
+  ak[2] = shr<2>(a);
+  ak[3] = shr<3>(a);
+  ak[4] = shr<4>(a);
+  ak[5] = shr<5>(a);
+  ak[6] = shr<6>(a);
+  ak[7] = shr<7>(a);
+  uint64_t acc = 0, acc1 = 0;  // two independent chains of four
+  uint32_t c2 = 0, c21 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k += 2) {
+    mac(acc, c2, ak[k], bk[k]);
+    mac(acc1, c21, ak[k + 1], bk[k + 1]);
+  }
+  const uint64_t sum = acc + acc1;
+  c2 += c21 + (sum < acc ? 1u : 0u);
+  acc = sum;
+  // column c = w0 + 2^32 w1 + 2^64 w2: spread w1 to lane c+1, w2 to c+2
+  const uint64_t n = (uint64_t)(uint32_t)acc + shr<1>((uint32_t)(acc >> 32)) + shr<2>(c2);
+  return fold(norm16(n));
+}
+COA_DEV uint32_t sq(uint32_t a) { return mul(a, a); }
+COA_DEV uint32_t sqn(uint32_t a, int n) {
+#pragma unroll 1
+  for (int i = 0; i < n; i++) a = mul(a, a);
+  return a;
+}
+
+COA_DEV uint32_t from_fe(const fe& a) {  // this lane's limb of its own copy of a
+  const uint32_t r = row_lane();
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x = r == (uint32_t)i ? a.v[i] : x;
+  return x;
+}
+COA_DEV void to_fe(fe& r, uint32_t x) {  // every lane of the row gets the row's value
+  r.v[0] = bcast<0>(x);
+  r.v[1] = bcast<1>(x);
+  r.v[2] = bcast<2>(x);
+  r.v[3] = bcast<3>(x);
+  r.v[4] = bcast<4>(x);
+  r.v[5] = bcast<5>(x);
+  r.v[6] = bcast<6>(x);
+  r.v[7] = bcast<7>(x);
+}
+
+// z^(2^252 - 3) (FieldElement::pow_p58) and z^(p - 2), the chains of
+// coa_fe.h fe_pow_chain on rows.
+COA_DEV uint32_t pow_chain(uint32_t& z11, uint32_t z) {
+  const uint32_t z2 = sq(z);
+  const uint32_t z9 = mul(sqn(z2, 2), z);
+  z11 = mul(z9, z2);
+  const uint32_t z_5_0 = mul(sq(z11), z9);
+  const uint32_t z_10_0 = mul(sqn(z_5_0, 5), z_5_0);
+  const uint32_t z_20_0 = mul(sqn(z_10_0, 10), z_10_0);
+  const uint32_t z_40_0 = mul(sqn(z_20_0, 20), z_20_0);
+  const uint32_t z_50_0 = mul(sqn(z_40_0, 10), z_10_0);
+  const uint32_t z_100_0 = mul(sqn(z_50_0, 50), z_50_0);
+  const uint32_t z_200_0 = mul(sqn(z_100_0, 100), z_100_0);
+  return mul(sqn(z_200_0, 50), z_50_0);  // 2^250 - 1
+}
+COA_DEV uint32_t pow_p58(uint32_t z) {
+  uint32_t z11;
+  const uint32_t t = pow_chain(z11, z);
+  return mul(sqn(t, 2), z);
+}
+COA_DEV uint32_t invert(uint32_t z) {
+  uint32_t z11;
+  const uint32_t t = pow_chain(z11, z);
+  return mul(sqn(t, 5), z11);
+}
+
+}  // namespace fw
+
+// fe_pow_p58 / fe_invert with the chain on rows (replicated fe in and out).
+COA_DEV void fe_pow_p58_rows(fe& r, const fe& z) { fw::to_fe(r, fw::pow_p58(fw::from_fe(z))); }
+COA_DEV void fe_invert_rows(fe& r, const fe& z) { fw::to_fe(r, fw::invert(fw::from_fe(z))); }

@@ -16,6 +16,7 @@
 // in dalek.
 #pragma once
 #include "coa_fe.h"
+#include "coa_fe_wave.h"
 
 struct ge_p2 {
   fe X, Y, Z;
@@ -168,6 +169,9 @@ COA_DEV void ge_niels_cneg(ge_niels& q, bool neg) {
 
 // curve25519-dalek FieldElement::sqrt_ratio_i(u, v): (was_nonzero_square, r)
 // with r the non-negative root of u/v (or of i*u/v when u/v is a non-square).
+// Rows = true: the (p-5)/8 power on 16-lane DPP rows (coa_fe_wave.h); every
+// lane of the wave must then take part.
+template <bool Rows = false>
 COA_DEV bool fe_sqrt_ratio_i(fe& r, const fe& u, const fe& v) {
   fe v3, v7, t, check, nu, nui, i;
   fe_sq(v3, v);
@@ -175,7 +179,10 @@ COA_DEV bool fe_sqrt_ratio_i(fe& r, const fe& u, const fe& v) {
   fe_sq(v7, v3);
   fe_mul(v7, v7, v);  // v^7
   fe_mul(t, u, v7);
-  fe_pow_p58(t, t);   // (u v^7)^((p-5)/8)
+  if constexpr (Rows)
+    fe_pow_p58_rows(t, t);
+  else
+    fe_pow_p58(t, t);  // (u v^7)^((p-5)/8)
   fe_mul(r, u, v3);
   fe_mul(r, r, t);    // u v^3 (u v^7)^((p-5)/8)
   fe_sq(check, r);
@@ -196,6 +203,7 @@ COA_DEV bool fe_sqrt_ratio_i(fe& r, const fe& u, const fe& v) {
 // curve25519-dalek 3.x CompressedEdwardsY::decompress on the 8 little-endian
 // dwords of the encoding.  Accepts y in [p, 2^255) (means y - p) and
 // "negative zero" (x = 0 with the sign bit set), exactly as dalek does.
+template <bool Rows = false>
 COA_DEV bool ge_decompress(ge_p3& r, const uint32_t* w) {
   fe y, yy, u, v, x, one, d;
   fe_from_words(y, w);
@@ -205,7 +213,7 @@ COA_DEV bool ge_decompress(ge_p3& r, const uint32_t* w) {
   fe_sub(u, yy, one);   // u = y^2 - 1
   fe_mul(v, yy, d);
   fe_add(v, v, one);    // v = d y^2 + 1
-  const bool ok = fe_sqrt_ratio_i(x, u, v);
+  const bool ok = fe_sqrt_ratio_i<Rows>(x, u, v);
   fe_cneg(x, (w[7] >> 31) != 0);
   r.X = x;
   r.Y = y;

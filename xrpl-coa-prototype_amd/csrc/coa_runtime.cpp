@@ -768,6 +768,20 @@ int coa_self_test(int device, uint64_t* bad_entries) {
   return COA_OK;
 }
 
+int coa_fe_rows_check_device(int device, const uint8_t* d_in, size_t n, uint32_t* d_out, void* stream) {
+  const int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  if (n && (!d_in || !d_out)) return fail(COA_EINVAL, "null argument");
+  if (n > (1u << 24)) return fail(COA_EINVAL, "n too large");
+  Dev* d = dev_by_id(device);
+  if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  HIP_TRY(coa_launch_fe_rows_check(d_in, (uint32_t)n, d_out, s));
+  if (!stream) HIP_TRY(hipStreamSynchronize(s));
+  return COA_OK;
+}
+
 size_t coa_verify_workspace_bytes(size_t n) { return ws_bytes(n); }
 
 int coa_ed25519_verify_strict_many(const uint8_t* msgs, size_t msg_len, const uint8_t* pks, const uint8_t* sigs,
