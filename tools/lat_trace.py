@@ -1,0 +1,63 @@
+"""Phase timestamps (clock64) of the certificate latency kernel's first
+signature job, from a build with -DCOA_LAT_TRACE.
+
+  python tools/lat_trace.py build     (CPU: writes build/lat_trace/libcoa_verify.so)
+  python tools/lat_trace.py run       (GPU: one C1-sized certificate, prints per-wave marks)
+
+Marks per wave: 0 start, 1 hash/decompression done, 2 comb term loaded,
+3 butterfly done, 4 after the hand-off barrier, 5 verdict (wave 0)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "xrpl-coa-prototype_amd")
+OUT = os.path.join(ROOT, "build", "lat_trace")
+
+
+def build():
+    sys.path.insert(0, PKG)
+    import build as b
+
+    b.build()
+    os.makedirs(OUT, exist_ok=True)
+    obj = os.path.join(OUT, "coa_committee.o")
+    subprocess.run([b.HIPCC] + b.COMMON + ["-DCOA_LAT_TRACE", "-c", os.path.join(b.CSRC, "coa_committee.hip"), "-o", obj],
+                   check=True)
+    objs = [obj if s == "coa_committee.hip" else os.path.join(b.OBJDIR, s + ".o") for s in b.SOURCES]
+    subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", os.path.join(OUT, "libcoa_verify.so")]
+                   + objs, check=True)
+
+
+def run():
+    os.environ["COA_VERIFY_LIB"] = os.path.join(OUT, "libcoa_verify.so")
+    sys.path.insert(0, PKG)
+    import ctypes
+
+    import numpy as np
+    import torch  # noqa: F401
+
+    import certificates as C
+    import coa_crypto
+
+    coa_crypto.init(1)
+    committee, batch = C.synth_certificates(2, committee_size=4, n_payload=1, seed=3)
+    committee.register()
+    rounds = np.full(2, batch.round, np.uint64)
+    L = coa_crypto.lib()
+    f = L.coa_lat_trace
+    f.argtypes = [ctypes.c_void_p]
+    for rep in range(5):
+        coa_crypto.certificate_verify(batch.header_inputs[0], batch.ids[0], batch.authors[0], batch.header_sigs[0],
+                                      int(rounds[0]), batch.vote_pks[:3], batch.vote_sigs[:3])
+        buf = (ctypes.c_ulonglong * 24)()
+        f(ctypes.addressof(buf))
+        t = np.array(list(buf), np.int64).reshape(3, 8)
+        t0 = t[:, 0].min()
+        print(json.dumps({"rep": rep, "wave0": (t[0, :6] - t0).tolist(), "wave1": (t[1, :5] - t0).tolist(),
+                          "wave2": (t[2, :5] - t0).tolist()}), flush=True)
+
+
+if __name__ == "__main__":
+    {"build": build, "run": run}[sys.argv[1]]()

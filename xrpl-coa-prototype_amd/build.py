@@ -21,7 +21,7 @@ ARCH = "gfx950"
 SOURCES = ["coa_kernels.hip", "coa_halved.hip", "coa_batch.hip", "coa_committee.hip", "coa_msm.hip", "coa_runtime.cpp",
            "coa_queue.cpp", "coa_wire.cpp"]
 HEADERS = ["coa_fe.h", "coa_sc.h", "coa_ge.h", "coa_sha512.h", "coa_smul.h", "coa_kernels.h", "coa_batch.h", "coa_halved.h",
-           "coa_committee.h", "coa_msm.h"]
+           "coa_committee.h", "coa_msm.h", "coa_fe_wave.h"]
 COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include")]
 
 

@@ -492,6 +492,16 @@ __global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a, uint32_t* __
 // Blocks [0, nc): header digests (wave 0 of each).  Blocks [nc, 2nc + nv):
 // one signature job each.
 #define KW_CHUNK 64  // blocks of schedule per LDS pass (40 KiB)
+#ifdef COA_LAT_TRACE  // phase timestamps of the first signature job (tools/lat_trace.py)
+__device__ unsigned long long g_lat_trace[3][8];
+#define LAT_MARK(w, i) \
+  if (job == 0 && lane == 0) g_lat_trace[w][i] = clock64();
+extern "C" int coa_lat_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lat_trace), sizeof(g_lat_trace)) == hipSuccess ? 0 : -1;
+}
+#else
+#define LAT_MARK(w, i)
+#endif
 __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
   const uint32_t wave = coa_sha::uni(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
@@ -539,9 +549,11 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
   load8u(rw, sig);
   uint32_t bits = 0;
   ge_p3 P;
+  LAT_MARK(wave, 0)
   if (wave == 1) {  // R's decompression, the power chain on the wave's DPP rows
     ge_p3 R;
     const bool ok = ge_decompress<true>(R, rw);
+    LAT_MARK(1, 1)
     if (lane == 0) {
 #pragma unroll
       for (int i = 0; i < 8; i++) {
@@ -605,6 +617,7 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
         tab = a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS;
       }
     }
+    LAT_MARK(wave, 1)
     if (!(bits & COA_CST_UNCACHED)) {
       add_const_word(dg, 0x80808080u);
       const int j = lane & 31;
@@ -615,6 +628,7 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
       ge_p3_identity(P);
       ge_madd(t, P, q);
       ge_p1p1_to_p3(P, t);
+      LAT_MARK(wave, 2)
 #pragma unroll 1
       for (int off = 16; off >= 1; off >>= 1) {
         ge_p3 O;
@@ -627,6 +641,7 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
         ge_add(t, P, oc);
         ge_p1p1_to_p3(P, t);
       }
+      LAT_MARK(wave, 3)
       if (wave == 2 && lane == 0) {
         const fe* f[4] = {&P.X, &P.Y, &P.Z, &P.T};
 #pragma unroll
@@ -638,6 +653,7 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
     }
   }
   __syncthreads();
+  LAT_MARK(wave, 4)
   if (wave == 0) {
     if (!(bits & COA_CST_UNCACHED)) {
       uint32_t pre = bits >> 8;
@@ -677,6 +693,7 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
         bits = (eq && tfree) ? 0u : COA_CST_VOTES_INCONCLUSIVE;
       }
     }
+    LAT_MARK(0, 5)
     if (lane == 0 && bits) atomicOr(a.status + c, bits);
   }
 }

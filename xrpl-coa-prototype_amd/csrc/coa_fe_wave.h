@@ -112,8 +112,18 @@ COA_DEV uint32_t mul(uint32_t a, uint32_t b) {
   c2 += c21 + (sum < acc ? 1u : 0u);
   acc = sum;
   // column c = w0 + 2^32 w1 + 2^64 w2: spread w1 to lane c+1, w2 to c+2
+  // (n_c < 2^34), fold n_{c+8} by 38 into lane c (< 2^40), then the wrap
+  // passes of fold_carry bring every lane below 2^32
   const uint64_t n = (uint64_t)(uint32_t)acc + shr<1>((uint32_t)(acc >> 32)) + shr<2>(c2);
-  return fold(norm16(n));
+  const uint32_t r = row_lane();
+  const uint32_t up_lo = shl<8>((uint32_t)n), up_hi = shl<8>((uint32_t)(n >> 32));
+  uint64_t m = (uint64_t)up_lo * 38u + (r < 8 ? n : 0);
+  m += (uint64_t)(up_hi * 38u) << 32;
+  wrap_step(m, r);
+  uint32_t hi = wrap_step(m, r);
+#pragma unroll 1
+  while (__any(hi != 0u)) hi = wrap_step(m, r);
+  return (uint32_t)m;
 }
 COA_DEV uint32_t sq(uint32_t a) { return mul(a, a); }
 COA_DEV uint32_t sqn(uint32_t a, int n) {
