@@ -28,7 +28,8 @@
 //   k_msm_wsum    one workgroup per window: sum of the chunk partials
 //   k_msm_final   one wave: Horner over the windows (9 doublings each) with
 //                 the four squarings / three products of every doubling on
-//                 four lanes at once, identity test, encoding flag -> verdict
+//                 the wave's four DPP rows at once (coa_fe_wave.h), identity
+//                 test, encoding flag -> verdict
 #include "coa_msm.h"
 
 #include <cstdlib>
@@ -493,17 +494,23 @@ COA_DEV void fe_sel4(fe& r, int k, const fe& a, const fe& b, const fe& c, const 
   fe_cmov(r, c, k == 2);
   fe_cmov(r, d, k == 3);
 }
-// one product per lane: lane k gets x_k * y_k
-COA_DEV void mul4(fe& r0, fe& r1, fe& r2, fe& r3, int k, const fe& x0, const fe& y0, const fe& x1, const fe& y1,
+// four products at once, one per 16-lane DPP row (coa_fe_wave.h): row r
+// forms x_r * y_r with limb c on its lane c; every lane then reads the four
+// results (limb i of product r from lane 16 r + i).  The whole wave calls it.
+COA_DEV void mul4(fe& r0, fe& r1, fe& r2, fe& r3, int, const fe& x0, const fe& y0, const fe& x1, const fe& y1,
                   const fe& x2, const fe& y2, const fe& x3, const fe& y3) {
-  fe x, y, p;
-  fe_sel4(x, k, x0, x1, x2, x3);
-  fe_sel4(y, k, y0, y1, y2, y3);
-  fe_mul(p, x, y);
-  fe_bcast(r0, p, 0);
-  fe_bcast(r1, p, 1);
-  fe_bcast(r2, p, 2);
-  fe_bcast(r3, p, 3);
+  const int row = (int)(__lane_id() >> 4);
+  fe x, y;
+  fe_sel4(x, row, x0, x1, x2, x3);
+  fe_sel4(y, row, y0, y1, y2, y3);
+  const uint32_t p = fw::mul(fw::from_fe(x), fw::from_fe(y));
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r0.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)p, i);
+    r1.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)p, 16 + i);
+    r2.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)p, 32 + i);
+    r3.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)p, 48 + i);
+  }
 }
 // p1p1 of 2P from projective P (ge_p2_dbl with the four squarings spread)
 COA_DEV void dbl4(ge_p1p1& r, const ge_p2& p, int k) {
