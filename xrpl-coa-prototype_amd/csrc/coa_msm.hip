@@ -670,7 +670,9 @@ hipError_t coa_launch_msm(const uint8_t* pks, const uint8_t* sigs, uint32_t n, c
   const uint32_t g8 = (nc * WA + 7) & ~7u;
   hipLaunchKernelGGL(k_msm_bucket, dim3(g8), dim3(256), 0, s, ws.pts, ws.dig, n, np, run, nc, ws.segs,
                      ws.part);
-  hipLaunchKernelGGL(k_msm_wsum, dim3(WA), dim3(256), 0, s, ws.part, nc, ws.wsum);
-  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, ws.wsum, ws.bad, verdict);
+  // one chunk (small groups): its partials already are the window sums,
+  // laid out as wsum (window w at w * 32 words)
+  if (nc > 1) hipLaunchKernelGGL(k_msm_wsum, dim3(WA), dim3(256), 0, s, ws.part, nc, ws.wsum);
+  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, nc > 1 ? ws.wsum : ws.part, ws.bad, verdict);
   return hipGetLastError();
 }
