@@ -21,6 +21,8 @@
 //   k_halve          (k, s) -> (c, |d|, e, H, sign d)
 //   k_verify_halved  decompression + small-order checks + Q == O
 #include "coa_halved.h"
+
+#include <cstdlib>
 #include "coa_kernels.h"
 
 #include "coa_fe.h"
@@ -888,19 +890,27 @@ hipError_t coa_launch_check_wcomb(const uint32_t* wcomb, uint32_t* bad, hipStrea
   return hipGetLastError();
 }
 
+static uint32_t block_env(const char* name) {
+  const char* e = getenv(name);
+  const int b = e ? atoi(e) : COA_VERIFY_BLOCK;
+  return (b == 64 || b == 128 || b == 256) ? (uint32_t)b : (uint32_t)COA_VERIFY_BLOCK;
+}
+
 hipError_t coa_launch_verify_split(const uint8_t* pks, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
                                    const uint32_t* kbuf, uint32_t n, uint32_t* rec, uint8_t* flags,
                                    uint8_t* verdicts, uint32_t* scratch, uint32_t* ebp, const uint32_t* comb,
                                    const uint32_t* wcomb, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint32_t blocks = (n + COA_VERIFY_BLOCK - 1) / COA_VERIFY_BLOCK;
+  // workgroup sizes (A/B: COA_PRE_BLOCK / COA_MAIN_BLOCK = 64, 128 or 256)
+  static const uint32_t pre_b = block_env("COA_PRE_BLOCK"), main_b = block_env("COA_MAIN_BLOCK");
+  const uint32_t blocks = (n + pre_b - 1) / pre_b;
   const int aligned = ((msg_len & 3) == 0) && (((uintptr_t)msgs & 3) == 0);
-  hipLaunchKernelGGL(k_pre_halve<2>, dim3(2 * blocks), dim3(COA_VERIFY_BLOCK), 0, s, pks, sigs, msgs, msg_len, aligned,
-                     kbuf, n, rec, flags, scratch, ebp, comb, wcomb, blocks);
+  hipLaunchKernelGGL(k_pre_halve<2>, dim3(2 * blocks), dim3(pre_b), 0, s, pks, sigs, msgs, msg_len, aligned, kbuf, n,
+                     rec, flags, scratch, ebp, comb, wcomb, blocks);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_verify_main<2>, dim3(blocks), dim3(COA_VERIFY_BLOCK), 0, s, rec, flags, n, verdicts, scratch,
-                     ebp, comb, wcomb);
+  hipLaunchKernelGGL(k_verify_main<2>, dim3((n + main_b - 1) / main_b), dim3(main_b), 0, s, rec, flags, n, verdicts,
+                     scratch, ebp, comb, wcomb);
   return hipGetLastError();
 }
 
