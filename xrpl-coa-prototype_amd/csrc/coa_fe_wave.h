@@ -65,7 +65,7 @@ COA_DEV uint32_t wrap_step(uint64_t& m, uint32_t r) {
   const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
   const uint32_t h7 = bcast<7>(hi);  // carry out of limb 7 = 2^256 * h7 = 38 * h7
   const uint32_t sh = shr<1>(hi);
-  uint32_t add = r == 0 ? h7 * 38u : sh;
+  uint32_t add = r == 0 ? __umul24(h7, 38u) : sh;  // h7 < 2^9: the full-rate 24-bit multiply
   add = r < 8 ? add : 0u;
   m = (uint64_t)lo + add;
   return r < 8 ? hi : 0u;
@@ -101,16 +101,30 @@ COA_DEV uint32_t mul(uint32_t a, uint32_t b) {
   ak[5] = shr<5>(a);
   ak[6] = shr<6>(a);
   ak[7] = shr<7>(a);
-  uint64_t acc = 0, acc1 = 0;  // two independent chains of four
-  uint32_t c2 = 0, c21 = 0;
-#pragma unroll
-  for (int k = 0; k < 8; k += 2) {
-    mac(acc, c2, ak[k], bk[k]);
-    mac(acc1, c21, ak[k + 1], bk[k + 1]);
-  }
-  const uint64_t sum = acc + acc1;
-  c2 += c21 + (sum < acc ? 1u : 0u);
-  acc = sum;
+  // the whole column in one asm statement (hipcc pads each statement with an
+  // s_nop before the next VALU that reads its outputs)
+  uint64_t acc = 0;
+  uint32_t c2 = 0;
+  asm("v_mad_u64_u32 %0, vcc, %2, %10, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %3, %11, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %4, %12, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %5, %13, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %6, %14, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %7, %15, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %8, %16, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %9, %17, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(c2)
+      : "v"(ak[0]), "v"(ak[1]), "v"(ak[2]), "v"(ak[3]), "v"(ak[4]), "v"(ak[5]), "v"(ak[6]), "v"(ak[7]), "v"(bk[0]),
+        "v"(bk[1]), "v"(bk[2]), "v"(bk[3]), "v"(bk[4]), "v"(bk[5]), "v"(bk[6]), "v"(bk[7])
+      : "vcc");
   // column c = w0 + 2^32 w1 + 2^64 w2: spread w1 to lane c+1, w2 to c+2
   // (n_c < 2^34), fold n_{c+8} by 38 into lane c (< 2^40), then the wrap
   // passes of fold_carry bring every lane below 2^32
@@ -118,7 +132,7 @@ COA_DEV uint32_t mul(uint32_t a, uint32_t b) {
   const uint32_t r = row_lane();
   const uint32_t up_lo = shl<8>((uint32_t)n), up_hi = shl<8>((uint32_t)(n >> 32));
   uint64_t m = (uint64_t)up_lo * 38u + (r < 8 ? n : 0);
-  m += (uint64_t)(up_hi * 38u) << 32;
+  m += (uint64_t)__umul24(up_hi, 38u) << 32;  // up_hi <= 3
   wrap_step(m, r);
   uint32_t hi = wrap_step(m, r);
 #pragma unroll 1
