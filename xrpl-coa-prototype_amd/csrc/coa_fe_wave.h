@@ -8,9 +8,10 @@
 //   8 row broadcasts of b's limbs (DPP row_newbcast),
 //   7 row shifts of a (DPP row_shr, zero fill),
 //   8 multiply-accumulates per lane (lane c sums column c = sum_k a_{c-k} b_k),
-//   carry normalisation across lanes (row_shr:1 / :2, repeated while any
-//   carry is left), the fold of limbs 8..15 by 2^256 = 38 (mod p) (row_shl:8)
-//   and a second normalisation with limb 8's carry wrapped into limb 0,
+//   the spread of each column's upper words to the next lanes (row_shr:1 /
+//   :2), the fold of limbs 8..15 by 2^256 = 38 (mod p) (row_shl:8), and two
+//   carry passes with limb 7's carry wrapped into limb 0 (a uniform branch
+//   to a rippling loop only while a carry is left),
 // about 60 instructions on the chain instead of 176-214.  The four rows of a
 // wave are independent: each row computes its own product (the Horner step of
 // k_msm_final runs four different products at once), or all four compute the
@@ -41,45 +42,41 @@ COA_DEV uint32_t bcast(uint32_t x) {  // every lane of the row gets the row's la
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + K, 0xf, 0xf, false);
 }
 
-// Carry propagation of per-lane column values n_c < 2^34 (lanes 0..15) into
-// 32-bit limbs; the value is < 2^512 so nothing leaves lane 15.  Two passes
-// leave carries of 0 or 1 that move on only through 0xffffffff limbs, so the
-// uniform branch to the rippling loop is almost never taken.
-COA_DEV uint32_t carry_step(uint64_t& n) {
-  const uint32_t lo = (uint32_t)n, hi = (uint32_t)(n >> 32);
-  n = (uint64_t)lo + shr<1>(hi);
-  return hi;
-}
-COA_DEV uint32_t norm16(uint64_t n) {
-  carry_step(n);
-  uint32_t hi = carry_step(n);
-#pragma unroll 1
-  while (__any(hi != 0u)) hi = carry_step(n);
-  return (uint32_t)n;
-}
-
-// Limbs l_0..l_15 (value < 2^512) -> 8 limbs of a value < 2^256, congruent mod p.
-// (selects, not branches: lane-dependent ternaries on 64-bit values would
-// become exec-mask branches)
+// One carry pass over the row's 8 limbs of per-lane 64-bit values: lane c
+// keeps its low word plus lane c-1's high word; limb 7's high word re-enters
+// limb 0 times 38 (2^256 = 38 mod p).  Lanes 8..15 stay 0.  (Selects, not
+// branches: lane-dependent ternaries on 64-bit values would become exec-mask
+// branches.)
 COA_DEV uint32_t wrap_step(uint64_t& m, uint32_t r) {
   const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
-  const uint32_t h7 = bcast<7>(hi);  // carry out of limb 7 = 2^256 * h7 = 38 * h7
+  const uint32_t h7 = bcast<7>(hi);
   const uint32_t sh = shr<1>(hi);
   uint32_t add = r == 0 ? __umul24(h7, 38u) : sh;  // h7 < 2^9: the full-rate 24-bit multiply
   add = r < 8 ? add : 0u;
   m = (uint64_t)lo + add;
   return r < 8 ? hi : 0u;
 }
-COA_DEV uint32_t fold(uint32_t l) {
+// Per-lane values m_c < 2^40 on lanes 0..7 (0 above) -> 32-bit limbs of a
+// congruent value < 2^256.  Two passes leave carries of 0 or 1 that move on
+// only through 0xffffffff limbs, so the uniform branch to the rippling loop
+// is almost never taken.
+COA_DEV uint32_t normalize(uint64_t m) {
   const uint32_t r = row_lane();
-  const uint32_t up = shl<8>(l);
-  const uint32_t lk = r < 8 ? l : 0u;  // lanes 8..15 drop out (up is 0 there)
-  uint64_t m = (uint64_t)up * 38u + lk;
   wrap_step(m, r);
   uint32_t hi = wrap_step(m, r);
 #pragma unroll 1
   while (__any(hi != 0u)) hi = wrap_step(m, r);
   return (uint32_t)m;
+}
+
+// a + b and a - b mod p (not canonical).  The difference adds 4p in
+// unnormalised limbs (limb 0: 2^33 - 76, limbs 1..7: 2^33 - 2), so no lane
+// goes negative.
+COA_DEV uint32_t add(uint32_t a, uint32_t b) { return normalize((uint64_t)a + b); }
+COA_DEV uint32_t sub(uint32_t a, uint32_t b) {
+  const uint32_t r = row_lane();
+  const uint64_t four_p = r == 0 ? 0x1ffffffb4ull : (r < 8 ? 0x1fffffffeull : 0ull);
+  return normalize((uint64_t)a + four_p - b);
 }
 
 // a * b mod p (not canonical), one product per 16-lane row.
@@ -133,11 +130,7 @@ COA_DEV uint32_t mul(uint32_t a, uint32_t b) {
   const uint32_t up_lo = shl<8>((uint32_t)n), up_hi = shl<8>((uint32_t)(n >> 32));
   uint64_t m = (uint64_t)up_lo * 38u + (r < 8 ? n : 0);
   m += (uint64_t)__umul24(up_hi, 38u) << 32;  // up_hi <= 3
-  wrap_step(m, r);
-  uint32_t hi = wrap_step(m, r);
-#pragma unroll 1
-  while (__any(hi != 0u)) hi = wrap_step(m, r);
-  return (uint32_t)m;
+  return normalize(m);
 }
 COA_DEV uint32_t sq(uint32_t a) { return mul(a, a); }
 COA_DEV uint32_t sqn(uint32_t a, int n) {

@@ -26,10 +26,10 @@
 //                 after it; sum_j j·B_j by a 256-lane suffix scan plus a
 //                 reduction (wave shuffles, LDS across the four waves)
 //   k_msm_wsum    one workgroup per window: sum of the chunk partials
-//   k_msm_final   one wave: Horner over the windows (9 doublings each) with
-//                 the four squarings / three products of every doubling on
-//                 the wave's four DPP rows at once (coa_fe_wave.h), identity
-//                 test, encoding flag -> verdict
+//   k_msm_final   one wave: Horner over the windows (9 doublings each) in
+//                 row form (coa_fe_wave.h): each step's four products on the
+//                 wave's four DPP rows at once, additions on the rows too;
+//                 identity test, encoding flag -> verdict
 #include "coa_msm.h"
 
 #include <cstdlib>
@@ -492,65 +492,70 @@ __global__ void __launch_bounds__(256) k_msm_wsum(const uint32_t* __restrict__ p
 
 // ------------------------------------------------------ Horner + verdict
 namespace {
-// Lanes 0..3 each compute one field product; every lane then reads all four
-// results (v_readlane), so the accumulator stays replicated across the wave.
-COA_DEV void fe_bcast(fe& r, const fe& v, int lane) {
-#pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)v.v[i], lane);
+// k_msm_final in row form (coa_fe_wave.h): every coordinate is one uint32 per
+// lane, each 16-lane row holding the whole element (limb c on lane c).  A
+// step's four products run on the four rows at once, row r on operand pair
+// r (a per-lane select), and every row then reads all four results back
+// (ds_bpermute).  Additions and subtractions stay on the rows.
+namespace rp {
+struct P2 {
+  uint32_t X, Y, Z;
+};
+struct P1 {
+  uint32_t X, Y, Z, T;
+};
+struct Ca {
+  uint32_t ypx, ymx, Z, t2d;
+};
+COA_DEV uint32_t pick(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint32_t r = __lane_id() >> 4;
+  return r == 0 ? a : (r == 1 ? b : (r == 2 ? c : d));
 }
-COA_DEV void fe_sel4(fe& r, int k, const fe& a, const fe& b, const fe& c, const fe& d) {
-  r = a;
-  fe_cmov(r, b, k == 1);
-  fe_cmov(r, c, k == 2);
-  fe_cmov(r, d, k == 3);
+template <int R>
+COA_DEV uint32_t from_row(uint32_t p) {
+  return (uint32_t)__shfl((int)p, (int)((R << 4) | (__lane_id() & 15u)), 64);
 }
-// four products at once, one per 16-lane DPP row (coa_fe_wave.h): row r
-// forms x_r * y_r with limb c on its lane c; every lane then reads the four
-// results (limb i of product r from lane 16 r + i).  The whole wave calls it.
-COA_DEV void mul4(fe& r0, fe& r1, fe& r2, fe& r3, int, const fe& x0, const fe& y0, const fe& x1, const fe& y1,
-                  const fe& x2, const fe& y2, const fe& x3, const fe& y3) {
-  const int row = (int)(__lane_id() >> 4);
-  fe x, y;
-  fe_sel4(x, row, x0, x1, x2, x3);
-  fe_sel4(y, row, y0, y1, y2, y3);
-  const uint32_t p = fw::mul(fw::from_fe(x), fw::from_fe(y));
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    r0.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)p, i);
-    r1.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)p, 16 + i);
-    r2.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)p, 32 + i);
-    r3.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)p, 48 + i);
-  }
+// 2P (p1p1) from projective P: ge_p2_dbl with its four squarings on the rows
+COA_DEV void dbl(P1& r, const P2& p) {
+  const uint32_t s = fw::add(p.X, p.Y);
+  const uint32_t x = pick(p.X, p.Y, p.Z, s);
+  const uint32_t q = fw::mul(x, x);
+  const uint32_t xx = from_row<0>(q), yy = from_row<1>(q), zz = from_row<2>(q), aa = from_row<3>(q);
+  const uint32_t zz2 = fw::add(zz, zz);
+  r.Y = fw::add(yy, xx);
+  r.Z = fw::sub(yy, xx);
+  r.X = fw::sub(aa, r.Y);
+  r.T = fw::sub(zz2, r.Z);
 }
-// p1p1 of 2P from projective P (ge_p2_dbl with the four squarings spread)
-COA_DEV void dbl4(ge_p1p1& r, const ge_p2& p, int k) {
-  fe s, xx, yy, zz, aa;
-  fe_add(s, p.X, p.Y);
-  mul4(xx, yy, zz, aa, k, p.X, p.X, p.Y, p.Y, p.Z, p.Z, s, s);
-  fe_add(zz, zz, zz);
-  fe_add(r.Y, yy, xx);
-  fe_sub(r.Z, yy, xx);
-  fe_sub(r.X, aa, r.Y);
-  fe_sub(r.T, zz, r.Z);
+COA_DEV void to_p2(P2& r, const P1& p) {
+  const uint32_t q = fw::mul(pick(p.X, p.Y, p.Z, p.Z), pick(p.T, p.Z, p.T, p.T));
+  r.X = from_row<0>(q);
+  r.Y = from_row<1>(q);
+  r.Z = from_row<2>(q);
 }
-COA_DEV void to_p3_4(ge_p3& r, const ge_p1p1& p, int k) {
-  mul4(r.X, r.Y, r.Z, r.T, k, p.X, p.T, p.Y, p.Z, p.Z, p.T, p.X, p.Y);
+COA_DEV void to_p3(P1& r, const P1& p) {
+  const uint32_t q = fw::mul(pick(p.X, p.Y, p.Z, p.X), pick(p.T, p.Z, p.T, p.Y));
+  r.X = from_row<0>(q);
+  r.Y = from_row<1>(q);
+  r.Z = from_row<2>(q);
+  r.T = from_row<3>(q);
 }
-COA_DEV void to_p2_4(ge_p2& r, const ge_p1p1& p, int k) {
-  fe unused;
-  mul4(r.X, r.Y, r.Z, unused, k, p.X, p.T, p.Y, p.Z, p.Z, p.T, p.Z, p.T);
+// p (extended) + q (cached) -> p1p1, as ge_add
+COA_DEV void add(P1& r, const P1& p, const Ca& c) {
+  const uint32_t ypx = fw::add(p.Y, p.X), ymx = fw::sub(p.Y, p.X);
+  const uint32_t q = fw::mul(pick(ypx, ymx, c.t2d, p.Z), pick(c.ypx, c.ymx, p.T, c.Z));
+  const uint32_t b = from_row<0>(q), a = from_row<1>(q), cc = from_row<2>(q), zz = from_row<3>(q);
+  const uint32_t zz2 = fw::add(zz, zz);
+  r.X = fw::sub(b, a);
+  r.Y = fw::add(b, a);
+  r.Z = fw::add(zz2, cc);
+  r.T = fw::sub(zz2, cc);
 }
-COA_DEV void add4(ge_p1p1& r, const ge_p3& p, const ge_cached& q, int k) {
-  fe ypx, ymx, a, b, c, zz;
-  fe_add(ypx, p.Y, p.X);
-  fe_sub(ymx, p.Y, p.X);
-  mul4(b, a, c, zz, k, ypx, q.YplusX, ymx, q.YminusX, q.T2d, p.T, p.Z, q.Z);
-  fe_add(zz, zz, zz);
-  fe_sub(r.X, b, a);
-  fe_add(r.Y, b, a);
-  fe_add(r.Z, zz, c);
-  fe_sub(r.T, zz, c);
+COA_DEV uint32_t ld(const uint32_t* base) {  // this lane's limb (0 on lanes 8..15 of the row)
+  const uint32_t c = __lane_id() & 15u;
+  return c < 8 ? base[c] : 0u;
 }
+}  // namespace rp
 }  // namespace
 
 __global__ void __launch_bounds__(64) k_msm_final(const uint32_t* __restrict__ wsum, const uint32_t* __restrict__ bad,
@@ -569,32 +574,28 @@ __global__ void __launch_bounds__(64) k_msm_final(const uint32_t* __restrict__ w
       for (int i = 0; i < 8; i++) cw[t * 32 + q * 8 + i] = f[q]->v[i];
   }
   __syncthreads();
-  const int k = t & 3;
-  ge_p3 top;
-  gbl_get(top, wsum + (uint64_t)(WA - 1) * 32);
-  ge_p2 acc;
-  ge_p3_to_p2(acc, top);
-  ge_p1p1 r;
+  const uint32_t* top = wsum + (uint64_t)(WA - 1) * 32;
+  rp::P2 acc = {rp::ld(top), rp::ld(top + 8), rp::ld(top + 16)};
+  rp::P1 r, a3;
 #pragma unroll 1
   for (int w = WA - 2; w >= 0; w--) {
 #pragma unroll 1
     for (int j = 0; j < COA_MSM_C - 1; j++) {
-      dbl4(r, acc, k);
-      to_p2_4(acc, r, k);
+      rp::dbl(r, acc);
+      rp::to_p2(acc, r);
     }
-    dbl4(r, acc, k);
-    ge_p3 a3;
-    to_p3_4(a3, r, k);
-    ge_cached c;
-    fe* f[4] = {&c.YplusX, &c.YminusX, &c.Z, &c.T2d};
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-#pragma unroll
-      for (int i = 0; i < 8; i++) f[q]->v[i] = cw[w * 32 + q * 8 + i];
-    add4(r, a3, c, k);
-    to_p2_4(acc, r, k);
+    rp::dbl(r, acc);
+    rp::to_p3(a3, r);
+    const uint32_t* q = cw + w * 32;
+    const rp::Ca c = {rp::ld(q), rp::ld(q + 8), rp::ld(q + 16), rp::ld(q + 24)};
+    rp::add(r, a3, c);
+    rp::to_p2(acc, r);
   }
-  if (t == 0) verdict[0] = (ge_p2_is_identity(acc) && bad[0] == 0) ? 0 : 1;
+  ge_p2 res;
+  fw::to_fe(res.X, acc.X);
+  fw::to_fe(res.Y, acc.Y);
+  fw::to_fe(res.Z, acc.Z);
+  if (t == 0) verdict[0] = (ge_p2_is_identity(res) && bad[0] == 0) ? 0 : 1;
 }
 
 // ----------------------------------------------------------------- host
