@@ -59,7 +59,8 @@ int coa_self_test(int device, uint64_t* bad_entries);
 /* Self-test of the row-parallel field arithmetic (no reference counterpart):
  * for each of the n 32-byte values d_in[i] (device memory, any value below
  * 2^256) compares, on the device, the 16-lane-row versions of z^((p-5)/8),
- * z^(p-2), z * d_in[i+1] and decompression (of d_in[i] as an encoding) with
+ * z^(p-2), z * d_in[i+1], z + d_in[i+1], z - d_in[i+1] and decompression (of
+ * d_in[i] as an encoding) with
  * the one-lane versions.  d_out[i] (uint32) gets a bit per mismatch: 0 = agree.
  * stream NULL = the engine's stream (the call then waits). */
 int coa_fe_rows_check_device(int device, const uint8_t* d_in, size_t n, uint32_t* d_out, void* stream);

@@ -1,6 +1,6 @@
 """Row-parallel field arithmetic (csrc/coa_fe_wave.h: one GF(2^255-19)
 element over a 16-lane DPP row) against the one-lane arithmetic of
-coa_fe.h, on the device: z^((p-5)/8), z^(p-2), products and whole
+coa_fe.h, on the device: z^((p-5)/8), z^(p-2), products, sums, differences and whole
 decompressions (curve25519-dalek's sqrt_ratio_i chain), over random values,
 carry-heavy limb patterns and the encodings the adversarial suite uses."""
 import numpy as np

@@ -67,5 +67,5 @@ hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr,
 // Row-parallel field arithmetic (coa_fe_wave.h) against coa_fe.h, one wave per
 // input x_i (32 LE bytes, any value < 2^256): out[i] bit0 pow_p58, bit1
 // invert, bit2 x_i * x_{i+1}, bit3 decompression of x_i as an encoding
-// (verdict and coordinates) differ.
+// (verdict and coordinates), bit4 x_i + x_{i+1}, bit5 x_i - x_{i+1} differ.
 hipError_t coa_launch_fe_rows_check(const uint8_t* in, uint32_t n, uint32_t* out, hipStream_t s);

@@ -805,6 +805,12 @@ __global__ void __launch_bounds__(64) k_fe_rows_check(const uint8_t* __restrict_
   fw::to_fe(a, fw::mul(fw::from_fe(x), fw::from_fe(y)));
   fe_mul(b, x, y);
   bad |= fe_eq(a, b) ? 0u : 4u;
+  fw::to_fe(a, fw::add(fw::from_fe(x), fw::from_fe(y)));
+  fe_add(b, x, y);
+  bad |= fe_eq(a, b) ? 0u : 16u;
+  fw::to_fe(a, fw::sub(fw::from_fe(x), fw::from_fe(y)));
+  fe_sub(b, x, y);
+  bad |= fe_eq(a, b) ? 0u : 32u;
   ge_p3 P, Q;
   const bool ok_r = ge_decompress<true>(P, w);
   const bool ok_s = ge_decompress(Q, w);
