@@ -496,7 +496,7 @@ namespace {
 // lane, each 16-lane row holding the whole element (limb c on lane c).  A
 // step's four products run on the four rows at once, row r on operand pair
 // r (a per-lane select), and every row then reads all four results back
-// (ds_bpermute).  Additions and subtractions stay on the rows.
+// (three lane-swap instructions, rows4).  Additions and subtractions stay on the rows.
 namespace rp {
 struct P2 {
   uint32_t X, Y, Z;
@@ -511,16 +511,25 @@ COA_DEV uint32_t pick(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   const uint32_t r = __lane_id() >> 4;
   return r == 0 ? a : (r == 1 ? b : (r == 2 ? c : d));
 }
-template <int R>
-COA_DEV uint32_t from_row(uint32_t p) {
-  return (uint32_t)__shfl((int)p, (int)((R << 4) | (__lane_id() & 15u)), 64);
+// Row r's value to every row, for all four rows at once: v_permlane32_swap
+// of q with itself gives (r0 r1 r0 r1) and (r2 r3 r2 r3); v_permlane16_swap of
+// each with itself splits it into two broadcasts (tools/probe_permlane.hip
+// checked the lane mapping on gfx950).  Three VALU instructions, no LDS.
+COA_DEV void rows4(uint32_t q, uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_t& r3) {
+  const auto h = __builtin_amdgcn_permlane32_swap(q, q, false, false);
+  const auto lo = __builtin_amdgcn_permlane16_swap(h[0], h[0], false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(h[1], h[1], false, false);
+  r0 = lo[0];
+  r1 = lo[1];
+  r2 = hi[0];
+  r3 = hi[1];
 }
 // 2P (p1p1) from projective P: ge_p2_dbl with its four squarings on the rows
 COA_DEV void dbl(P1& r, const P2& p) {
   const uint32_t s = fw::add(p.X, p.Y);
   const uint32_t x = pick(p.X, p.Y, p.Z, s);
-  const uint32_t q = fw::mul(x, x);
-  const uint32_t xx = from_row<0>(q), yy = from_row<1>(q), zz = from_row<2>(q), aa = from_row<3>(q);
+  uint32_t xx, yy, zz, aa;
+  rows4(fw::mul(x, x), xx, yy, zz, aa);
   const uint32_t zz2 = fw::add(zz, zz);
   r.Y = fw::add(yy, xx);
   r.Z = fw::sub(yy, xx);
@@ -528,23 +537,17 @@ COA_DEV void dbl(P1& r, const P2& p) {
   r.T = fw::sub(zz2, r.Z);
 }
 COA_DEV void to_p2(P2& r, const P1& p) {
-  const uint32_t q = fw::mul(pick(p.X, p.Y, p.Z, p.Z), pick(p.T, p.Z, p.T, p.T));
-  r.X = from_row<0>(q);
-  r.Y = from_row<1>(q);
-  r.Z = from_row<2>(q);
+  uint32_t unused;
+  rows4(fw::mul(pick(p.X, p.Y, p.Z, p.Z), pick(p.T, p.Z, p.T, p.T)), r.X, r.Y, r.Z, unused);
 }
 COA_DEV void to_p3(P1& r, const P1& p) {
-  const uint32_t q = fw::mul(pick(p.X, p.Y, p.Z, p.X), pick(p.T, p.Z, p.T, p.Y));
-  r.X = from_row<0>(q);
-  r.Y = from_row<1>(q);
-  r.Z = from_row<2>(q);
-  r.T = from_row<3>(q);
+  rows4(fw::mul(pick(p.X, p.Y, p.Z, p.X), pick(p.T, p.Z, p.T, p.Y)), r.X, r.Y, r.Z, r.T);
 }
 // p (extended) + q (cached) -> p1p1, as ge_add
 COA_DEV void add(P1& r, const P1& p, const Ca& c) {
   const uint32_t ypx = fw::add(p.Y, p.X), ymx = fw::sub(p.Y, p.X);
-  const uint32_t q = fw::mul(pick(ypx, ymx, c.t2d, p.Z), pick(c.ypx, c.ymx, p.T, c.Z));
-  const uint32_t b = from_row<0>(q), a = from_row<1>(q), cc = from_row<2>(q), zz = from_row<3>(q);
+  uint32_t b, a, cc, zz;
+  rows4(fw::mul(pick(ypx, ymx, c.t2d, p.Z), pick(c.ypx, c.ymx, p.T, c.Z)), b, a, cc, zz);
   const uint32_t zz2 = fw::add(zz, zz);
   r.X = fw::sub(b, a);
   r.Y = fw::add(b, a);
