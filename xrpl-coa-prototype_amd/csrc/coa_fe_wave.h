@@ -19,8 +19,9 @@
 //
 // Values are < 2^256 in 8 limbs, not canonical; fw::to_fe returns them in
 // the ordinary (replicated per lane) representation of coa_fe.h, where
-// fe_canon finishes.  Every lane of the wave must execute these functions
-// together (DPP reads other lanes).  Checked against coa_fe.h by
+// fe_canon finishes.  All 16 lanes of a row must execute these functions
+// together (DPP reads the row's other lanes); rows are independent, and a
+// whole row may sit out (k_msm_prep's last rows).  Checked against coa_fe.h by
 // coa_fe_rows_check_device (tests/test_gpu_fe_rows.py).
 #pragma once
 #include "coa_fe.h"
