@@ -169,32 +169,41 @@ COA_DEV void ge_niels_cneg(ge_niels& q, bool neg) {
 
 // curve25519-dalek FieldElement::sqrt_ratio_i(u, v): (was_nonzero_square, r)
 // with r the non-negative root of u/v (or of i*u/v when u/v is a non-square).
-// Rows = true: the (p-5)/8 power on 16-lane DPP rows (coa_fe_wave.h); every
-// lane of the wave must then take part.
+// Rows = true: every product on 16-lane DPP rows (coa_fe_wave.h); all lanes
+// of a row must then take part.
 template <bool Rows = false>
 COA_DEV bool fe_sqrt_ratio_i(fe& r, const fe& u, const fe& v) {
-  fe v3, v7, t, check, nu, nui, i;
-  fe_sq(v3, v);
-  fe_mul(v3, v3, v);  // v^3
-  fe_sq(v7, v3);
-  fe_mul(v7, v7, v);  // v^7
-  fe_mul(t, u, v7);
-  if constexpr (Rows)
-    fe_pow_p58_rows(t, t);
-  else
-    fe_pow_p58(t, t);  // (u v^7)^((p-5)/8)
-  fe_mul(r, u, v3);
-  fe_mul(r, r, t);    // u v^3 (u v^7)^((p-5)/8)
-  fe_sq(check, r);
-  fe_mul(check, check, v);
+  fe check, nu, nui, i, ri;
   fe_const_sqrtm1(i);
   fe_neg(nu, u);
-  fe_mul(nui, nu, i);
+  if constexpr (Rows) {  // every product on the rows; back to lanes for the tests
+    const uint32_t fu = fw::from_fe(u), fv = fw::from_fe(v), fi = fw::from_fe(i);
+    const uint32_t v3 = fw::mul(fw::sq(fv), fv);
+    const uint32_t v7 = fw::mul(fw::sq(v3), fv);
+    const uint32_t t = fw::pow_p58(fw::mul(fu, v7));
+    const uint32_t rr = fw::mul(fw::mul(fu, v3), t);
+    fw::to_fe(r, rr);
+    fw::to_fe(check, fw::mul(fw::sq(rr), fv));
+    fw::to_fe(ri, fw::mul(rr, fi));
+    fw::to_fe(nui, fw::mul(fw::from_fe(nu), fi));
+  } else {
+    fe v3, v7, t;
+    fe_sq(v3, v);
+    fe_mul(v3, v3, v);  // v^3
+    fe_sq(v7, v3);
+    fe_mul(v7, v7, v);  // v^7
+    fe_mul(t, u, v7);
+    fe_pow_p58(t, t);   // (u v^7)^((p-5)/8)
+    fe_mul(r, u, v3);
+    fe_mul(r, r, t);    // u v^3 (u v^7)^((p-5)/8)
+    fe_sq(check, r);
+    fe_mul(check, check, v);
+    fe_mul(nui, nu, i);
+    fe_mul(ri, r, i);
+  }
   const bool correct = fe_eq(check, u);
   const bool flipped = fe_eq(check, nu);
   const bool flipped_i = fe_eq(check, nui);
-  fe ri;
-  fe_mul(ri, r, i);
   fe_cmov(r, ri, flipped || flipped_i);
   fe_cneg(r, fe_isneg(r) != 0);
   return correct || flipped;
