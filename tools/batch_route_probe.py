@@ -6,7 +6,8 @@ copy.
 
 usage: python tools/batch_route_probe.py [n ...]   (default 1024 .. 262144)
 An argument GxV times G groups of V signatures each (one message per group)
-through the per-vote path only, e.g. 10000x67 (a C3 round with uncached keys).
+through the per-vote path (or, with PROBE_GROUPS_MSM_MIN=16384, the default
+routing), e.g. 10000x67 (a C3 round with uncached keys).
 Prints one JSON line per size."""
 import json
 import os
@@ -42,7 +43,7 @@ def groups(dev, ng, nv):
     torch.cuda.synchronize()
     pk, sg = pk.cpu().numpy(), sg.cpu().numpy()
     offs = np.arange(ng + 1, dtype=np.uint64) * nv
-    os.environ["COA_MSM_MIN"] = "0"
+    os.environ["COA_MSM_MIN"] = os.environ.get("PROBE_GROUPS_MSM_MIN", "0")
     coa_crypto.verify_batch_groups(gm, pk, sg, offs, rng_seed=7)
     reps = 5
     t0 = time.perf_counter()

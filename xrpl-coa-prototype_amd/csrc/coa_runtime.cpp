@@ -342,7 +342,7 @@ uint64_t os_entropy_seed() {
 }
 
 // Groups of at least msm_min() signatures take the Pippenger path
-// (coa_msm.hip), and so does the group of a one-group call; COA_MSM_MIN
+// (coa_msm.hip), and so do the groups of a call with at most two; COA_MSM_MIN
 // overrides (0 = never).
 size_t msm_min() {
   const char* e = getenv("COA_MSM_MIN");
@@ -429,12 +429,13 @@ int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* si
   if (total && (!pks || !sigs)) return fail(COA_EINVAL, "null pks/sigs");
   if (check_n(total) != COA_OK) return COA_EINVAL;
   const uint64_t eff_seed = zs_in ? 0 : (seed ? seed : os_entropy_seed());
-  // A lone group takes the Pippenger path at any size: one group through the
-  // per-vote path waits for one lane's whole joint scalar multiplication
-  // (~1.3 ms), the Pippenger kernels spread it over the chip (0.75 ms at 67
-  // votes, tools/batch_route_probe.py).
+  // One or two groups take the Pippenger path at any size: the per-vote path
+  // waits for one lane's whole joint scalar multiplication (~1.4 ms however
+  // few groups), the Pippenger kernels spread a group over the chip (~0.5 ms
+  // at 67 votes, tools/batch_route_probe.py); from three groups one per-vote
+  // launch is faster than the groups one after another.
   size_t mmin = msm_min();
-  if (mmin && n_groups == 1) mmin = 1;
+  if (mmin && n_groups <= 2) mmin = 1;
   if (mmin) {
     for (size_t g = 0; g < n_groups; g++)
       if (group_offsets[g + 1] - group_offsets[g] >= mmin)
