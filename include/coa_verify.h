@@ -133,8 +133,9 @@ int coa_ed25519_verify_batch_groups_z(const uint8_t* msgs, const uint8_t* pks, c
 
 /* Pippenger form of the call above for ONE group whose buffers are resident
  * in the HBM of `device` (dalek's verify_batch switches to Pippenger above
- * 190 points; the host-pointer entries above route groups of at least
- * COA_MSM_MIN signatures, default 16384, here as well).
+ * 190 points; the host-pointer entries above route here the groups of a
+ * call with one or two groups, and groups of at least COA_MSM_MIN
+ * signatures, default 16384).
  *   d_msg        32 bytes, the digest every signature signs
  *   d_pks        n * 32, d_sigs n * 64
  *   d_zs         n * 16 explicit weights (parity tests) or NULL = derived
