@@ -142,12 +142,14 @@ int coa_ed25519_verify_batch_groups_z(const uint8_t* msgs, const uint8_t* pks, c
  *                from rng_seed (0 = fresh OS entropy)
  *   *d_verdict   0 Ok / 1 Err, same rules as coa_ed25519_verify_batch
  * `workspace` NULL = engine-owned (the call then waits for the stream), else
- * at least coa_verify_batch_workspace_bytes(n) bytes on `device` (the call
- * only enqueues). */
+ * `workspace_bytes` bytes on `device`, at least
+ * coa_verify_batch_workspace_bytes(n) evaluated under the same environment
+ * (COA_MSM_RUN changes the layout); a smaller buffer is refused with
+ * COA_EINVAL.  With a workspace the call only enqueues. */
 size_t coa_verify_batch_workspace_bytes(size_t n);
 int coa_ed25519_verify_batch_device(int device, const uint8_t* d_msg, const uint8_t* d_pks, const uint8_t* d_sigs,
                                     size_t n, const uint8_t* d_zs, uint64_t rng_seed, uint8_t* d_verdict,
-                                    void* workspace, void* stream);
+                                    void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------ Digest
  * Replaces Sha512::digest at worker/src/processor.rs:38 (500 KB batch

@@ -1,0 +1,115 @@
+"""C3 at its stated size (BASELINE.json configs[2]): one round
+of 10,000 certificates of a committee of 100 (67 votes each, 3,336-byte
+headers), with injected failures of every crypto kind, through the engine's
+Certificate::verify crypto (coa_certificate_verify_many: fused kernel over the
+registered committee, exact fallbacks for keys outside it) and compared status
+bit for status bit with the C restatement of dalek run the reference's way,
+per certificate (oracle/coa_oracle.c: Header::digest == id,
+Signature::verify(id, author), verify_batch(Certificate::digest, votes) --
+primary/src/messages.rs:48-84,189-234)."""
+import concurrent.futures
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import coa_oracle as co
+
+pytestmark = pytest.mark.gpu
+
+L_ORDER = 2 ** 252 + 27742317777372353535851937790883648493
+SMALL_ORDER_R = bytes.fromhex("c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a")
+OFF_CURVE = (2).to_bytes(32, "little")
+KINDS = ("header_byte", "header_sig_flip", "header_sig_small_R", "vote_sig_flip", "vote_s_plus_l",
+         "vote_small_R", "vote_foreign_key_valid", "vote_wrong_member_key", "vote_off_curve_key",
+         "author_outside_committee_valid")
+
+
+def _oracle_bits(hin, hid, author, hsig, round_, vpks, vsigs, zs):
+    """COA_CERT_* bits the reference's own checks would produce, each check
+    run independently (the engine reports all three)."""
+    bits = 0
+    if co.sha512(hin)[:32] != bytes(hid):
+        bits |= 1
+    if not co.verify_strict(bytes(hid), bytes(author), bytes(hsig)):
+        bits |= 2
+    d = co.sha512(bytes(hid) + struct.pack("<Q", round_) + bytes(author))[:32]
+    if not co.verify_batch(d, [bytes(p) for p in vpks], [bytes(s) for s in vsigs], zs):
+        bits |= 4
+    return bits
+
+
+@pytest.mark.timeout(600)
+def test_c3_round_full_size_with_injected_failures(engine):
+    import certificates as C
+    import workloads
+
+    n = 10_000
+    committee, b = C.synth_certificates(n, committee_size=100, n_payload=32, seed=3)
+    assert committee.register() == 100
+    hin = list(b.header_inputs)
+    ids, authors, hsigs = b.ids.copy(), b.authors.copy(), b.header_sigs.copy()
+    vpks, vsigs = b.vote_pks.copy(), b.vote_sigs.copy()
+    rng = np.random.default_rng(0xC3)
+    victims = rng.permutation(n)[:300]
+    kind_of = {}
+    for j, c in enumerate(victims):
+        c = int(c)
+        k = j % len(KINDS)
+        kind_of[c] = k
+        lo = int(b.offsets[c])
+        v = lo + int(rng.integers(0, 67))
+        if k == 0:
+            h = bytearray(hin[c]); h[100 + j % 3000] ^= 0x10; hin[c] = bytes(h)
+        elif k == 1:
+            hsigs[c, 40] ^= 1
+        elif k == 2:
+            hsigs[c, :32] = np.frombuffer(SMALL_ORDER_R, np.uint8)
+        elif k == 3:
+            vsigs[v, 5] ^= 0x80
+        elif k == 4:
+            s = int.from_bytes(bytes(vsigs[v, 32:]), "little") + L_ORDER
+            vsigs[v, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
+        elif k == 5:
+            vsigs[v, :32] = np.frombuffer(SMALL_ORDER_R, np.uint8)
+        elif k == 6:  # a valid signature by a key outside the committee: Ok crypto (uncached kernels)
+            p, s = engine.sign_many(workloads.key_seeds(1, start=10 ** 6 + c), b.cert_digests[c:c + 1])
+            vpks[v], vsigs[v] = p[0], s[0]
+        elif k == 7:  # another member's key under this vote's signature
+            vpks[v] = vpks[lo + (v - lo + 1) % 67]
+        elif k == 8:
+            vpks[v] = np.frombuffer(OFF_CURVE, np.uint8)
+        else:  # header re-authored by a key outside the committee, every signature valid
+            seed = workloads.key_seeds(1, start=2 * 10 ** 6 + c)
+            apk = engine.public_keys(seed)[0]
+            h = bytes(apk) + hin[c][32:]
+            hin[c] = h
+            ids[c] = engine.sha512_many([h])[0, :32]
+            authors[c] = apk
+            _, hs = engine.sign_many(seed, ids[c:c + 1])
+            hsigs[c] = hs[0]
+            cd = engine.sha512_many([bytes(ids[c]) + struct.pack("<Q", b.round) + bytes(apk)])[0, :32]
+            vseeds = workloads.key_seeds(100)[(c + np.arange(67)) % 100]
+            p, s = engine.sign_many(vseeds, np.tile(cd, (67, 1)))
+            vpks[lo:lo + 67], vsigs[lo:lo + 67] = p, s
+    rounds = np.full(n, b.round, np.uint64)
+    got = engine.certificate_verify_many(hin, ids, authors, hsigs, rounds, vpks, vsigs, b.offsets, rng_seed=17)
+
+    zr = np.random.default_rng(1)
+
+    def one(c):
+        lo, hi = int(b.offsets[c]), int(b.offsets[c + 1])
+        zs = [int.from_bytes(zr.bytes(16), "little") for _ in range(hi - lo)]
+        return _oracle_bits(hin[c], ids[c], authors[c], hsigs[c], b.round, vpks[lo:hi], vsigs[lo:hi], zs)
+
+    with concurrent.futures.ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+        exp = np.array(list(ex.map(one, range(n))), np.uint8)
+    mism = np.nonzero(got != exp)[0]
+    assert mism.size == 0, [(int(c), kind_of.get(int(c)), int(got[c]), int(exp[c])) for c in mism[:20]]
+    # every injected kind had its intended effect, untouched certificates are Ok
+    want = {0: 1, 1: 2, 2: 2, 3: 4, 4: 4, 5: 4, 6: 0, 7: 4, 8: 4, 9: 0}
+    for c, k in kind_of.items():
+        assert got[c] == want[k], (c, KINDS[k], int(got[c]))
+    untouched = np.setdiff1d(np.arange(n), victims)
+    assert (got[untouched] == 0).all()

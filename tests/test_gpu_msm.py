@@ -209,3 +209,6 @@ def test_device_entry_resident(engine):
     engine.verify_batch_device(0, msg, pk[:0], sg[:0], out, rng_seed=1)  # empty batch: Ok
     torch.cuda.synchronize()
     assert int(out[0]) == 0
+    # a workspace smaller than verify_batch_workspace_bytes(n) is refused
+    with pytest.raises(engine.EngineError):
+        engine.verify_batch_device(0, msg, pk, sg, out, rng_seed=1, workspace=ws[:4096])

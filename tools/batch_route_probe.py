@@ -6,8 +6,8 @@ copy.
 
 usage: python tools/batch_route_probe.py [n ...]   (default 1024 .. 262144)
 An argument GxV times G groups of V signatures each (one message per group)
-through the per-vote path (or, with PROBE_GROUPS_MSM_MIN=16384, the default
-routing), e.g. 10000x67 (a C3 round with uncached keys).
+under both routings (COA_MSM_MIN=0: per-vote; unset: the default), e.g. 2x67
+or 10000x67 (a C3 round with uncached keys).
 Prints one JSON line per size."""
 import json
 import os
@@ -33,6 +33,11 @@ def timed(msg, pk, sg, offs, reps):
 
 
 def groups(dev, ng, nv):
+    """G groups of V signatures each, timed under both routings: COA_MSM_MIN=0
+    (every group through one per-vote launch) and the default routing (calls
+    with one or two groups, and groups >= 16,384, take the Pippenger path).
+    Each row records the route and the COA_MSM_MIN it ran under, and checks
+    that a corrupted copy (one flipped s bit in the last group) is rejected."""
     n = ng * nv
     gm = messages(ng)
     m = torch.from_numpy(np.repeat(gm, nv, axis=0)).to(dev)
@@ -42,17 +47,31 @@ def groups(dev, ng, nv):
     coa_crypto.sign_many_device(0, seeds, m, pk, sg)
     torch.cuda.synchronize()
     pk, sg = pk.cpu().numpy(), sg.cpu().numpy()
+    bad = sg.copy()
+    bad[n - 1, 40] ^= 1
     offs = np.arange(ng + 1, dtype=np.uint64) * nv
-    os.environ["COA_MSM_MIN"] = os.environ.get("PROBE_GROUPS_MSM_MIN", "0")
-    coa_crypto.verify_batch_groups(gm, pk, sg, offs, rng_seed=7)
-    reps = 5
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        v = coa_crypto.verify_batch_groups(gm, pk, sg, offs, rng_seed=7)
-    ms = (time.perf_counter() - t0) / reps * 1e3
-    print(json.dumps({"groups": ng, "votes_per_group": nv, "per_vote": {"ms": round(ms, 4),
-                      "groups_per_s": round(ng / ms * 1e3, 1), "sig_per_s": round(n / ms * 1e3, 1),
-                      "valid_ok": int(v.sum()) == 0}}), flush=True)
+    row = {"groups": ng, "votes_per_group": nv}
+    for mmin in ("0", None):
+        if mmin is None:
+            os.environ.pop("COA_MSM_MIN", None)
+            route = "pippenger" if (ng <= 2 or nv >= 16384) else "per_vote"
+            label = "default"
+        else:
+            os.environ["COA_MSM_MIN"] = mmin
+            route, label = "per_vote", "msm_min_0"
+        coa_crypto.verify_batch_groups(gm, pk, sg, offs, rng_seed=7)
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            v = coa_crypto.verify_batch_groups(gm, pk, sg, offs, rng_seed=7)
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        vb = coa_crypto.verify_batch_groups(gm, pk, bad, offs, rng_seed=7)
+        row[label] = {"route": route, "COA_MSM_MIN": mmin if mmin is not None else "unset (16384)",
+                      "ms": round(ms, 4), "groups_per_s": round(ng / ms * 1e3, 1),
+                      "sig_per_s": round(n / ms * 1e3, 1), "valid_ok": int(v.sum()) == 0,
+                      "corrupt_rejected": int(vb[-1]) == 1 and int(vb[:-1].sum()) == 0}
+    os.environ.pop("COA_MSM_MIN", None)
+    print(json.dumps(row), flush=True)
 
 
 def main():

@@ -52,7 +52,7 @@ def build(verbose=False):
     objs = [o for o, _ in results]
     rebuilt = any(b for _, b in results)
     if rebuilt or not os.path.exists(LIB) or os.path.getmtime(LIB) < _newest(objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")

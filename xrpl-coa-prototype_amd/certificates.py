@@ -260,7 +260,8 @@ class CertificateBatch:
         self.vote_pks = vote_pks                # uint8 [nv, 32]
         self.vote_sigs = vote_sigs              # uint8 [nv, 64]
         self.offsets = offsets                  # uint64 [n + 1]
-        self.voter_idx = voter_idx              # int [nv] committee index of each voter
+        self.voter_idx = voter_idx              # int [nv] key-seed index of each voter (synthesis only;
+                                                # the checks read vote_pks)
         self.author_idx = author_idx            # int [n]
 
     def __len__(self):
@@ -318,6 +319,32 @@ def synth_certificates(n_certs, committee_size=100, n_votes=None, n_payload=32, 
                                        author_idx, round_)
 
 
+def _quorum_errors(batch, committee):
+    """Certificate::verify's vote checks (primary/src/messages.rs:196-211) over
+    a CertificateBatch, read from the vote keys themselves (not from the
+    synthetic voter_idx): a key outside the committee (stake 0,
+    UnknownAuthority), a key voting twice (AuthorityReuse) or less than
+    2N/3 + 1 of stake (CertificateRequiresQuorum) marks the certificate.
+    Returns uint8 [n]: 1 = one of those errors."""
+    n = len(batch)
+    err = np.zeros(n, np.uint8)
+    nv = int(batch.offsets[-1]) if n else 0
+    if nv == 0:
+        return np.ones(n, np.uint8) if committee.quorum_threshold() > 0 else err
+    keys = np.ascontiguousarray(batch.vote_pks[:nv], dtype=np.uint8).view(np.dtype((np.void, 32))).reshape(-1)
+    uniq, inv = np.unique(keys, return_inverse=True)
+    ustake = np.array([committee.stake(PublicKey(bytes(u))) for u in uniq], np.int64)
+    vstake = ustake[inv]
+    q = committee.quorum_threshold()
+    for i in range(n):
+        lo, hi = int(batch.offsets[i]), int(batch.offsets[i + 1])
+        k = inv[lo:hi]
+        st = vstake[lo:hi]
+        if (st <= 0).any() or len(np.unique(k)) != len(k) or int(st.sum()) < q:
+            err[i] = 1
+    return err
+
+
 def verify_certificate_batch(batch, committee, rng_seed=0):
     """Certificate::verify over a CertificateBatch: one fused engine call
     (coa_certificate_verify_many) + vectorised protocol checks.
@@ -329,14 +356,7 @@ def verify_certificate_batch(batch, committee, rng_seed=0):
     err = (st != 0).astype(np.uint8)
     stake = np.array([committee.stake(PublicKey(bytes(p))) for p in batch.authors])
     err |= (stake <= 0).astype(np.uint8)                                        # UnknownAuthority
-    # quorum: distinct voters with stake, total >= 2N/3 + 1
-    keys = committee.authorities()
-    kstake = np.array([committee.stake(k) for k in keys])
-    for i in range(n):
-        lo, hi = int(batch.offsets[i]), int(batch.offsets[i + 1])
-        v = batch.voter_idx[lo:hi]
-        if len(np.unique(v)) != len(v) or kstake[v].sum() < committee.quorum_threshold():
-            err[i] = 1
+    err |= _quorum_errors(batch, committee)                                     # votes: stake, reuse, quorum
     return err
 
 
@@ -349,13 +369,7 @@ def verify_certificate_batch_stepwise(batch, committee, rng_seed=0):
     stake = np.array([committee.stake(PublicKey(bytes(p))) for p in batch.authors])
     err |= (stake <= 0).astype(np.uint8)
     err |= coa_crypto.verify_strict_many(batch.ids, batch.authors, batch.header_sigs)
-    keys = committee.authorities()
-    kstake = np.array([committee.stake(k) for k in keys])
-    for i in range(n):
-        lo, hi = int(batch.offsets[i]), int(batch.offsets[i + 1])
-        v = batch.voter_idx[lo:hi]
-        if len(np.unique(v)) != len(v) or kstake[v].sum() < committee.quorum_threshold():
-            err[i] = 1
+    err |= _quorum_errors(batch, committee)
     cin = [bytes(batch.ids[c]) + struct.pack("<Q", batch.round) + bytes(batch.authors[c]) for c in range(n)]
     cd = coa_crypto.sha512_many(cin)[:, :32]
     gv = coa_crypto.verify_batch_groups(cd, batch.vote_pks, batch.vote_sigs, batch.offsets, rng_seed=rng_seed)

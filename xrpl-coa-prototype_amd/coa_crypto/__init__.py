@@ -90,7 +90,7 @@ def lib():
         "coa_ed25519_verify_batch_groups": ([P8, P8, P8, P64, sz, P8, ctypes.c_uint64], ctypes.c_int),
         "coa_ed25519_verify_batch_groups_z": ([P8, P8, P8, P64, sz, P8, P8], ctypes.c_int),
         "coa_verify_batch_workspace_bytes": ([sz], sz),
-        "coa_ed25519_verify_batch_device": ([ctypes.c_int, vp, vp, vp, sz, vp, ctypes.c_uint64, vp, vp, vp],
+        "coa_ed25519_verify_batch_device": ([ctypes.c_int, vp, vp, vp, sz, vp, ctypes.c_uint64, vp, vp, sz, vp],
                                             ctypes.c_int),
         "coa_sha512_many": ([P8, P64, sz, P8], ctypes.c_int),
         "coa_sha512_trunc32_many": ([P8, P64, sz, P8], ctypes.c_int),
@@ -273,13 +273,19 @@ def init(n_gpus=0):
 
 
 def init_devices(ids):
-    """Open exactly these HIP devices (bench.py: each rank its own GPU)."""
+    """Open exactly these HIP devices (bench.py: each rank its own GPU).  A
+    device listed k times gets k contexts, i.e. k index-range shards."""
     arr = (ctypes.c_int * len(ids))(*ids)
     return _check(lib().coa_init_devices(arr, len(ids)))
 
 
 def device_count():
     return _check(lib().coa_device_count())
+
+
+def shutdown():
+    """Release every context (the next call re-initialises lazily)."""
+    return _check(lib().coa_shutdown())
 
 
 def self_test(device=0):
@@ -386,8 +392,9 @@ def verify_batch_device(device, msg, pks, sigs, verdict, zs=None, rng_seed=0, wo
     if zs is not None:
         assert tuple(zs.shape) == (n, 16)
     ws = workspace.data_ptr() if workspace is not None else None
+    wsb = workspace.numel() * workspace.element_size() if workspace is not None else 0
     _check(lib().coa_ed25519_verify_batch_device(device, msg.data_ptr(), pks.data_ptr(), sigs.data_ptr(), n, zp,
-                                                 rng_seed, verdict.data_ptr(), ws, handle))
+                                                 rng_seed, verdict.data_ptr(), ws, wsb, handle))
 
 
 def verify_strict_many_device(device, msgs, pks, sigs, verdicts, workspace=None, stream=None):

@@ -1,12 +1,15 @@
 // Host runtime behind include/coa_verify.h.
 //
 // * One context per GPU: a non-blocking HIP stream, the fixed-base B table
-//   (built on the device by k_build_btable at coa_init) and growable device
-//   buffers.  Each context has its own mutex; a call holds the mutexes of the
-//   devices it enqueues on until their streams drain.
+//   (built on the device by k_build_btable at coa_init), growable device
+//   buffers and its own host worker thread ("each GPU has its
+//   own host thread, context and streams").  Each context has its own mutex; a
+//   shard holds its context's mutex until the context's stream drains.
 // * Host-pointer "many" calls shard items by contiguous index range over the
-//   opened devices: no cross-GPU exchange, verdict bytes land
-//   in place in the caller's output slice.
+//   opened contexts: every shard runs on its context's worker
+//   thread, so the shards' copies, launches and waits proceed concurrently; no
+//   cross-GPU exchange, verdict bytes land in place in the caller's output
+//   slice.  A call with one shard runs on the caller's thread (no hop).
 // * Device-pointer calls enqueue on the caller's stream and return.
 // * No CPU fallback anywhere: without a usable GPU, calls fail with
 //   COA_ENODEVICE.
@@ -16,12 +19,18 @@
 
 #include <algorithm>
 #include <array>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <future>
 #include <memory>
 #include <mutex>
 #include <random>
 #include <string>
+#include <thread>
+#include <utility>
 #include <vector>
 
 #include "coa_batch.h"
@@ -92,8 +101,65 @@ struct PinBuf {
   }
 };
 
+// True on a context worker thread: nested sharded calls then run inline
+// (a worker never waits for its own queue).
+thread_local bool t_in_worker = false;
+
+// Result of a task run on another thread: return code + that thread's error.
+using TaskResult = std::pair<int, std::string>;
+
+// One host thread per device context, running submitted tasks in order.
+class Worker {
+ public:
+  Worker() : th_([this] { loop(); }) {}
+  ~Worker() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  std::future<TaskResult> submit(std::function<int()> f) {
+    auto task = std::make_shared<std::packaged_task<TaskResult()>>([f = std::move(f)] {
+      g_err.clear();
+      const int rc = f();
+      return TaskResult(rc, rc == COA_OK ? std::string() : g_err);
+    });
+    std::future<TaskResult> fut = task->get_future();
+    {
+      std::lock_guard<std::mutex> l(m_);
+      q_.emplace_back([task] { (*task)(); });
+    }
+    cv_.notify_one();
+    return fut;
+  }
+
+ private:
+  void loop() {
+    t_in_worker = true;
+    for (;;) {
+      std::function<void()> job;
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        job = std::move(q_.front());
+        q_.pop_front();
+      }
+      job();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  bool stop_ = false;
+  std::thread th_;  // last: starts after the members above exist
+};
+
 struct Dev {
   int id = 0;
+  std::unique_ptr<Worker> worker;
   hipStream_t stream = nullptr;
   uint32_t* btab = nullptr;  // 128 x (j+1)B, radix-256 fixed-base table (12 KiB)
   uint32_t* comb = nullptr;  // 32 x 128 x (v+1)256^j B comb for k_verify_halved (384 KiB)
@@ -161,6 +227,7 @@ int open_device(int d) {
     }
   }
   HIP_TRY(hipStreamSynchronize(dev->stream));
+  dev->worker = std::make_unique<Worker>();
   g_devs.push_back(std::move(dev));
   return COA_OK;
 }
@@ -174,9 +241,11 @@ int init_locked(const int* ids, int n) {
     return fail(COA_ENODEVICE, "no HIP device available (this engine has no CPU fallback)");
   std::vector<int> want;
   if (ids) {
+    // a device listed k times gets k contexts (k index-range shards on one
+    // GPU: rehearses an N-GPU split, e.g. tests/test_gpu_c5.py)
     for (int i = 0; i < n; i++) {
       if (ids[i] < 0 || ids[i] >= count) return fail(COA_EINVAL, "device id out of range");
-      if (std::find(want.begin(), want.end(), ids[i]) == want.end()) want.push_back(ids[i]);
+      want.push_back(ids[i]);
     }
     if (want.empty()) return fail(COA_EINVAL, "empty device list");
   } else {
@@ -310,28 +379,53 @@ int check_n(size_t n) {
   return COA_OK;
 }
 
-// Run `body` for every shard with the device lock held, then drain every
-// used stream.  body(Dev&, lo, hi) enqueues work and returns COA_OK or an error.
+// Runs tasks that each own one context: concurrently on the contexts' worker
+// threads, or inline on this thread when they all use one context (no thread
+// hop on the latency path) or when this is already a worker.  Returns the
+// first failure (its message in this thread's coa_last_error).
+int run_tasks(std::vector<std::pair<Dev*, std::function<int()>>>& tasks) {
+  bool one_ctx = true;
+  for (auto& t : tasks) one_ctx = one_ctx && t.first == tasks[0].first;
+  if (one_ctx || t_in_worker) {
+    for (auto& t : tasks) {
+      const int rc = t.second();
+      if (rc != COA_OK) return rc;
+    }
+    return COA_OK;
+  }
+  std::vector<std::future<TaskResult>> futs;
+  futs.reserve(tasks.size());
+  for (auto& t : tasks) futs.push_back(t.first->worker->submit(t.second));
+  int rc = COA_OK;
+  std::string msg;
+  for (auto& f : futs) {
+    TaskResult r = f.get();  // wait for every task: they reference the caller's buffers
+    if (r.first != COA_OK && rc == COA_OK) {
+      rc = r.first;
+      msg = r.second;
+    }
+  }
+  if (rc != COA_OK) g_err = msg;
+  return rc;
+}
+
+// Run `body` for every shard with its context's lock held, then drain the
+// context's stream.  body(Dev&, lo, hi) enqueues work and returns COA_OK or an
+// error.  The shards run concurrently, one per context worker.
 template <class F>
 int for_shards(size_t n, F body) {
-  std::vector<Range> rs = shard(n);
-  std::vector<std::unique_lock<std::mutex>> locks;
-  int rc = COA_OK;
-  for (auto& r : rs) {
-    locks.emplace_back(r.dev->mu);
-    if (hipSetDevice(r.dev->id) != hipSuccess) {
-      rc = fail(COA_EHIP, "hipSetDevice failed");
-      break;
-    }
-    rc = body(*r.dev, r.lo, r.hi);
-    if (rc != COA_OK) break;
+  std::vector<std::pair<Dev*, std::function<int()>>> tasks;
+  for (const Range& r : shard(n)) {
+    tasks.emplace_back(r.dev, [r, &body]() -> int {
+      std::lock_guard<std::mutex> l(r.dev->mu);
+      if (hipSetDevice(r.dev->id) != hipSuccess) return fail(COA_EHIP, "hipSetDevice failed");
+      int rc = body(*r.dev, r.lo, r.hi);
+      const hipError_t e = hipStreamSynchronize(r.dev->stream);
+      if (e != hipSuccess && rc == COA_OK) rc = fail(COA_EHIP, std::string("stream sync: ") + hipGetErrorString(e));
+      return rc;
+    });
   }
-  for (auto& r : rs) {
-    (void)hipSetDevice(r.dev->id);
-    hipError_t e = hipStreamSynchronize(r.dev->stream);
-    if (e != hipSuccess && rc == COA_OK) rc = fail(COA_EHIP, std::string("stream sync: ") + hipGetErrorString(e));
-  }
-  return rc;
+  return run_tasks(tasks);
 }
 
 uint64_t os_entropy_seed() {
@@ -388,34 +482,73 @@ int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* si
                       size_t n_groups, const uint8_t* zs_in, uint64_t seed, uint8_t* verdicts_out,
                       uint32_t gbase = 0);
 
-// Large groups one by one through the Pippenger path (devices round-robin),
-// runs of small groups through the per-vote path.
+// Large groups through the Pippenger path, dealt round-robin to the contexts
+// and run concurrently on their workers; runs of small groups through the
+// per-vote path (sharded over the contexts) meanwhile.
+// gbase: the global index of this call's first group (the z_i hash binds it).
 int batch_groups_split(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, const uint64_t* group_offsets,
-                       size_t n_groups, const uint8_t* zs_in, uint64_t seed, uint8_t* verdicts_out, size_t mmin) {
-  size_t g = 0, nlarge = 0;
-  while (g < n_groups) {
+                       size_t n_groups, const uint8_t* zs_in, uint64_t seed, uint8_t* verdicts_out, size_t mmin,
+                       uint32_t gbase) {
+  std::vector<std::vector<size_t>> large(g_devs.size());
+  std::vector<std::pair<size_t, size_t>> small_runs;
+  size_t nlarge = 0;
+  for (size_t g = 0; g < n_groups;) {
     size_t e = g;
     while (e < n_groups && group_offsets[e + 1] - group_offsets[e] < mmin) e++;
     if (e > g) {
-      const uint64_t v0 = group_offsets[g];
-      std::vector<uint64_t> offs(e - g + 1);
-      for (size_t k = 0; k <= e - g; k++) offs[k] = group_offsets[g + k] - v0;
-      const int rc = batch_groups_impl(msgs + g * 32, pks + v0 * 32, sigs + v0 * 64, offs.data(), e - g,
-                                       zs_in ? zs_in + v0 * 16 : nullptr, seed, verdicts_out + g, (uint32_t)g);
-      if (rc != COA_OK) return rc;
+      small_runs.emplace_back(g, e);
       g = e;
-      continue;
+    } else {
+      large[nlarge++ % g_devs.size()].push_back(g++);
     }
-    const uint64_t v0 = group_offsets[g], nv = group_offsets[g + 1] - v0;
-    Dev& d = *g_devs[nlarge++ % g_devs.size()];
-    std::lock_guard<std::mutex> l(d.mu);
-    HIP_TRY(hipSetDevice(d.id));
-    const int rc = msm_group(d, msgs + g * 32, pks + v0 * 32, sigs + v0 * 64, nv, zs_in ? zs_in + v0 * 16 : nullptr,
-                             seed, (uint32_t)g, verdicts_out + g);
-    if (rc != COA_OK) return rc;
-    g++;
   }
-  return COA_OK;
+  std::vector<std::pair<Dev*, std::function<int()>>> tasks;
+  for (size_t di = 0; di < g_devs.size(); di++) {
+    if (large[di].empty()) continue;
+    Dev* d = g_devs[di].get();
+    const std::vector<size_t>* mine = &large[di];
+    tasks.emplace_back(d, [=]() -> int {
+      std::lock_guard<std::mutex> l(d->mu);
+      HIP_TRY(hipSetDevice(d->id));
+      for (size_t g : *mine) {
+        const uint64_t v0 = group_offsets[g], nv = group_offsets[g + 1] - v0;
+        const int rc = msm_group(*d, msgs + g * 32, pks + v0 * 32, sigs + v0 * 64, nv,
+                                 zs_in ? zs_in + v0 * 16 : nullptr, seed, gbase + (uint32_t)g, verdicts_out + g);
+        if (rc != COA_OK) return rc;
+      }
+      return COA_OK;
+    });
+  }
+  // the large groups go to the workers first when there are several
+  // contexts; with one context (or inside a worker) everything runs here
+  bool one_ctx = g_devs.size() == 1 || t_in_worker;
+  std::vector<std::future<TaskResult>> futs;
+  if (!one_ctx)
+    for (auto& t : tasks) futs.push_back(t.first->worker->submit(t.second));
+  int rc = COA_OK;
+  for (auto& r : small_runs) {
+    const size_t g = r.first, e = r.second;
+    const uint64_t v0 = group_offsets[g];
+    std::vector<uint64_t> offs(e - g + 1);
+    for (size_t k = 0; k <= e - g; k++) offs[k] = group_offsets[g + k] - v0;
+    rc = batch_groups_impl(msgs + g * 32, pks + v0 * 32, sigs + v0 * 64, offs.data(), e - g,
+                           zs_in ? zs_in + v0 * 16 : nullptr, seed, verdicts_out + g, gbase + (uint32_t)g);
+    if (rc != COA_OK) break;
+  }
+  std::string msg = rc != COA_OK ? g_err : std::string();
+  if (one_ctx) {
+    if (rc == COA_OK) rc = run_tasks(tasks);
+    return rc;
+  }
+  for (auto& f : futs) {
+    TaskResult t = f.get();
+    if (t.first != COA_OK && rc == COA_OK) {
+      rc = t.first;
+      msg = t.second;
+    }
+  }
+  if (rc != COA_OK) g_err = msg;
+  return rc;
 }
 
 int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, const uint64_t* group_offsets,
@@ -439,7 +572,8 @@ int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* si
   if (mmin) {
     for (size_t g = 0; g < n_groups; g++)
       if (group_offsets[g + 1] - group_offsets[g] >= mmin)
-        return batch_groups_split(msgs, pks, sigs, group_offsets, n_groups, zs_in, eff_seed, verdicts_out, mmin);
+        return batch_groups_split(msgs, pks, sigs, group_offsets, n_groups, zs_in, eff_seed, verdicts_out, mmin,
+                                  gbase);
   }
   // shard by group index
   return for_shards(n_groups, [&](Dev& d, size_t glo, size_t ghi) -> int {
@@ -899,7 +1033,7 @@ size_t coa_verify_batch_workspace_bytes(size_t n) { return coa_msm_ws_bytes(n); 
 
 int coa_ed25519_verify_batch_device(int device, const uint8_t* d_msg, const uint8_t* d_pks, const uint8_t* d_sigs,
                                     size_t n, const uint8_t* d_zs, uint64_t rng_seed, uint8_t* d_verdict,
-                                    void* workspace, void* stream) {
+                                    void* workspace, size_t workspace_bytes, void* stream) {
   int rc = ensure_init();
   if (rc != COA_OK) return rc;
   if (!d_msg || !d_verdict || (n && (!d_pks || !d_sigs))) return fail(COA_EINVAL, "null argument");
@@ -913,7 +1047,13 @@ int coa_ed25519_verify_batch_device(int device, const uint8_t* d_msg, const uint
     return COA_OK;
   }
   const uint64_t seed = d_zs ? 0 : (rng_seed ? rng_seed : os_entropy_seed());
-  if (workspace) return enqueue_msm(*d, d_msg, d_pks, d_sigs, n, d_zs, seed, 0, d_verdict, workspace, s);
+  if (workspace) {
+    // the chunk count (and so the layout) depends on the bucket run length of
+    // this call: refuse a buffer sized for another one
+    if (workspace_bytes < coa_msm_ws_bytes(n))
+      return fail(COA_EINVAL, "workspace smaller than coa_verify_batch_workspace_bytes(n)");
+    return enqueue_msm(*d, d_msg, d_pks, d_sigs, n, d_zs, seed, 0, d_verdict, workspace, s);
+  }
   std::lock_guard<std::mutex> l(d->mu);
   HIP_TRY(d->msm.ensure(coa_msm_ws_bytes(n)));
   rc = enqueue_msm(*d, d_msg, d_pks, d_sigs, n, d_zs, seed, 0, d_verdict, d->msm.p, s);
@@ -1058,35 +1198,43 @@ int coa_committee_register(const uint8_t* pks, size_t n) {
   std::sort(keys.begin(), keys.end());
   keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
   const size_t nk = keys.size();
+  // every context builds its own copy, concurrently on the context workers
+  std::vector<std::pair<Dev*, std::function<int()>>> tasks;
   for (auto& dp : g_devs) {
-    Dev& d = *dp;
-    std::lock_guard<std::mutex> l(d.mu);
-    HIP_TRY(hipSetDevice(d.id));
-    d.nkeys = 0;
-    if (nk == 0) continue;
-    HIP_TRY(d.ckeys.ensure(nk * 32));
-    HIP_TRY(d.kflags.ensure(nk * 4));
-    HIP_TRY(d.ktabs.ensure(nk * (size_t)COA_KEY_TAB_DWORDS * 4));
-    HIP_TRY(hipMemcpyAsync(d.ckeys.p, keys.data(), nk * 32, hipMemcpyHostToDevice, d.stream));
-    HIP_TRY(coa_launch_key_flags(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.kflags.as<uint32_t>(), d.stream));
-    HIP_TRY(coa_launch_key_tables(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.ktabs.as<uint32_t>(), d.stream));
-    // wide combs (48 MiB per key) when the committee fits the budget
-    // (speed only: without the memory the radix-256 key combs serve)
-    d.kwide = false;
-    if ((double)nk * COA_KWCOMB_DWORDS * 4 <= key_wcomb_budget()) {
-      if (d.kwtabs.ensure(nk * (size_t)COA_KWCOMB_DWORDS * 4, true) == hipSuccess) {
-        HIP_TRY(coa_launch_key_wcombs(d.ktabs.as<uint32_t>(), (uint32_t)nk, d.kwtabs.as<uint32_t>(), d.stream));
-        d.kwide = true;
+    Dev* dv = dp.get();
+    tasks.emplace_back(dv, [dv, nk, &keys]() -> int {
+      Dev& d = *dv;
+      std::lock_guard<std::mutex> l(d.mu);
+      HIP_TRY(hipSetDevice(d.id));
+      d.nkeys = 0;
+      if (nk == 0) return COA_OK;
+      HIP_TRY(d.ckeys.ensure(nk * 32));
+      HIP_TRY(d.kflags.ensure(nk * 4));
+      HIP_TRY(d.ktabs.ensure(nk * (size_t)COA_KEY_TAB_DWORDS * 4));
+      HIP_TRY(hipMemcpyAsync(d.ckeys.p, keys.data(), nk * 32, hipMemcpyHostToDevice, d.stream));
+      HIP_TRY(coa_launch_key_flags(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.kflags.as<uint32_t>(), d.stream));
+      HIP_TRY(coa_launch_key_tables(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.ktabs.as<uint32_t>(), d.stream));
+      // wide combs (48 MiB per key) when the committee fits the budget
+      // (speed only: without the memory the radix-256 key combs serve)
+      d.kwide = false;
+      if ((double)nk * COA_KWCOMB_DWORDS * 4 <= key_wcomb_budget()) {
+        if (d.kwtabs.ensure(nk * (size_t)COA_KWCOMB_DWORDS * 4, true) == hipSuccess) {
+          HIP_TRY(coa_launch_key_wcombs(d.ktabs.as<uint32_t>(), (uint32_t)nk, d.kwtabs.as<uint32_t>(), d.stream));
+          d.kwide = true;
+        } else {
+          d.kwtabs.release();
+          (void)hipGetLastError();
+        }
       } else {
-        d.kwtabs.release();
-        (void)hipGetLastError();
+        d.kwtabs.release();  // a smaller committee's tables are not kept
       }
-    } else {
-      d.kwtabs.release();  // a smaller committee's tables are not kept
-    }
-    HIP_TRY(hipStreamSynchronize(d.stream));
-    d.nkeys = (uint32_t)nk;
+      HIP_TRY(hipStreamSynchronize(d.stream));
+      d.nkeys = (uint32_t)nk;
+      return COA_OK;
+    });
   }
+  rc = run_tasks(tasks);
+  if (rc != COA_OK) return rc;
   return (int)nk;
 }
 
