@@ -741,6 +741,7 @@ out:
 }
 
 /* ---------------------------------------------------- multithreaded driver */
+#define COA_ORACLE_MAX_THREADS 4096
 typedef struct {
   const uint8_t *msgs, *pks, *sigs;
   size_t msg_len, lo, hi;
@@ -759,14 +760,70 @@ void coa_oracle_verify_strict_many(const uint8_t* msgs, size_t msg_len, const ui
                                    size_t n, uint8_t* out, int nthreads) {
   ensure_init();
   if (nthreads < 1) nthreads = 1;
-  pthread_t th[256];
-  job_t jobs[256];
-  if (nthreads > 256) nthreads = 256;
+  if (nthreads > COA_ORACLE_MAX_THREADS) nthreads = COA_ORACLE_MAX_THREADS;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  job_t* jobs = (job_t*)malloc(sizeof(job_t) * nthreads);
   for (int t = 0; t < nthreads; t++) {
     jobs[t] = (job_t){msgs, pks, sigs, msg_len, n * t / nthreads, n * (t + 1) / nthreads, out};
     pthread_create(&th[t], NULL, verify_worker, &jobs[t]);
   }
   for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(th);
+  free(jobs);
+}
+
+/* ------------------------------------- Certificate::verify crypto, many
+   Certificate::verify (primary/src/messages.rs:189-215) as the reference runs
+   it, one certificate per call of the loop, with the three crypto checks
+   evaluated independently (bit 1: SHA-512(header bytes)[..32] != id,
+   messages.rs:49-51 / 70-84; bit 2: verify_strict(id, author, header sig),
+   :64-66; bit 4: verify_batch(Certificate::digest, votes) with the given
+   16-byte weights, :214 / 226-234).  Certificates are dealt to nthreads
+   pthreads in contiguous ranges (CPU baseline: all host cores). */
+typedef struct {
+  const uint8_t *hdata, *ids, *origins, *hsigs, *vpks, *vsigs, *zs;
+  const uint64_t *hoff, *rounds, *voff;
+  size_t lo, hi;
+  uint8_t* out;
+} certjob_t;
+
+static uint8_t cert_one(const certjob_t* j, size_t c) {
+  uint8_t bits = 0, h[64], m[72];
+  coa_oracle_sha512(j->hdata + j->hoff[c], j->hoff[c + 1] - j->hoff[c], h);
+  if (memcmp(h, j->ids + 32 * c, 32) != 0) bits |= 1;
+  if (coa_oracle_verify_strict(j->ids + 32 * c, 32, j->origins + 32 * c, j->hsigs + 64 * c)) bits |= 2;
+  memcpy(m, j->ids + 32 * c, 32);
+  for (int b = 0; b < 8; b++) m[32 + b] = (uint8_t)(j->rounds[c] >> (8 * b));
+  memcpy(m + 40, j->origins + 32 * c, 32);
+  coa_oracle_sha512(m, 72, h);
+  const uint64_t v0 = j->voff[c], nv = j->voff[c + 1] - v0;
+  if (coa_oracle_verify_batch(h, 32, j->vpks + 32 * v0, j->vsigs + 64 * v0, nv, j->zs + 16 * v0)) bits |= 4;
+  return bits;
+}
+
+static void* cert_worker(void* p) {
+  certjob_t* j = (certjob_t*)p;
+  for (size_t c = j->lo; c < j->hi; c++) j->out[c] = cert_one(j, c);
+  return NULL;
+}
+
+void coa_oracle_certificate_verify_many(const uint8_t* hdata, const uint64_t* hoff, const uint8_t* ids,
+                                        const uint8_t* origins, const uint8_t* hsigs, const uint64_t* rounds,
+                                        const uint8_t* vpks, const uint8_t* vsigs, const uint64_t* voff,
+                                        const uint8_t* zs, size_t n, uint8_t* out, int nthreads) {
+  ensure_init();
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > COA_ORACLE_MAX_THREADS) nthreads = COA_ORACLE_MAX_THREADS;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  certjob_t* jobs = (certjob_t*)malloc(sizeof(certjob_t) * nthreads);
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = (certjob_t){hdata, ids, origins, hsigs, vpks, vsigs, zs, hoff, rounds, voff,
+                          n * t / nthreads, n * (t + 1) / nthreads, out};
+    pthread_create(&th[t], NULL, cert_worker, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(th);
+  free(jobs);
 }
 
 #ifdef COA_COUNT
@@ -793,12 +850,14 @@ static void* sha_worker(void* p) {
 
 void coa_oracle_sha512_many_mt(const uint8_t* data, const uint64_t* off, size_t n, uint8_t* out64, int nthreads) {
   if (nthreads < 1) nthreads = 1;
-  if (nthreads > 256) nthreads = 256;
-  pthread_t th[256];
-  shajob_t jobs[256];
+  if (nthreads > COA_ORACLE_MAX_THREADS) nthreads = COA_ORACLE_MAX_THREADS;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  shajob_t* jobs = (shajob_t*)malloc(sizeof(shajob_t) * nthreads);
   for (int t = 0; t < nthreads; t++) {
     jobs[t] = (shajob_t){data, off, n * t / nthreads, n * (t + 1) / nthreads, out64};
     pthread_create(&th[t], NULL, sha_worker, &jobs[t]);
   }
   for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(th);
+  free(jobs);
 }

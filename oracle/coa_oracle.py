@@ -38,6 +38,8 @@ def lib(count=False):
         L.coa_oracle_sha512.restype = None
         L.coa_oracle_sha512_many_mt.argtypes = [P8, ctypes.c_void_p, sz, P8, ctypes.c_int]
         L.coa_oracle_sha512_many_mt.restype = None
+        L.coa_oracle_certificate_verify_many.argtypes = [P8, P8, P8, P8, P8, P8, P8, P8, P8, P8, sz, P8, ctypes.c_int]
+        L.coa_oracle_certificate_verify_many.restype = None
         if count:
             L.coa_oracle_counts.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 2
             L.coa_oracle_reset_counts.argtypes = []
@@ -143,3 +145,22 @@ def certificate_verify(header_input, header_id, author, header_sig, round_, vote
         return False
     d = sha512(bytes(header_id) + _st.pack("<Q", round_) + bytes(author))[:32]
     return verify_batch(d, [bytes(p) for p in vote_pks], [bytes(s) for s in vote_sigs], zs)
+
+
+def certificate_verify_many(header_inputs, ids, origins, header_sigs, rounds, vote_pks, vote_sigs, vote_offsets, zs,
+                            nthreads=1):
+    """Certificate::verify crypto for n certificates on nthreads C threads:
+    uint8 [n] of bits 1 (header id), 2 (header signature), 4 (vote batch with
+    the given weights zs, uint8 [n_votes, 16]), each check independent."""
+    n = len(header_inputs)
+    hdata = np.frombuffer(b"".join(bytes(h) for h in header_inputs) + b"\0", np.uint8).copy()
+    hoff = np.zeros(n + 1, np.uint64)
+    hoff[1:] = np.cumsum([len(h) for h in header_inputs])
+    a = [np.ascontiguousarray(x, np.uint8) for x in (ids, origins, header_sigs)]
+    r = np.ascontiguousarray(np.broadcast_to(np.asarray(rounds, np.uint64), (n,)))
+    vp, vs, z = (np.ascontiguousarray(x, np.uint8) for x in (vote_pks, vote_sigs, zs))
+    voff = np.ascontiguousarray(vote_offsets, np.uint64)
+    out = np.zeros(max(n, 1), np.uint8)
+    lib().coa_oracle_certificate_verify_many(_p(hdata), _p(hoff), _p(a[0]), _p(a[1]), _p(a[2]), _p(r), _p(vp), _p(vs),
+                                             _p(voff), _p(z), n, _p(out), nthreads)
+    return out[:n]

@@ -81,3 +81,67 @@ def test_shard_ranges_cover(n, parts):
     if n >= parts:
         sizes = [hi - lo for _, lo, hi in rs]
         assert max(sizes) - min(sizes) <= 1
+
+
+def _bench_rank(rank, world, port, q):
+    """One rank of bench.py's timed region (bench.timed_steps): gloo barrier
+    on both sides, max-over-ranks elapsed.  Rank r's step verifies its own
+    contiguous slice with the CPU oracle (standing in for its GPU) and sleeps
+    r * 30 ms per step, so the max must be rank 1's time."""
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        import coa_oracle as co
+        import ed25519_ref as o
+        import workloads
+
+        n = 6
+        lo, hi = sharding.rank_slice(rank, world, n)
+        seeds, msgs = workloads.key_seeds(n, start=lo), workloads.messages(n, start=lo)
+        pks = np.frombuffer(b"".join(o.public_key(bytes(s)) for s in seeds), np.uint8).reshape(-1, 32).copy()
+        sigs = np.frombuffer(b"".join(o.sign(bytes(s), bytes(m)) for s, m in zip(seeds, msgs)),
+                             np.uint8).reshape(-1, 64).copy()
+        calls = []
+
+        def step(i):
+            v = co.verify_strict_many(msgs, pks, sigs, 1)
+            assert int(v.sum()) == 0
+            time.sleep(0.03 * rank)
+            calls.append(i)
+
+        t0 = time.perf_counter()
+        el = bench.timed_steps(step, 4, 2, world, dist, lambda: None)
+        own = time.perf_counter() - t0
+        q.put((rank, el, own, calls))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_timed_region_two_ranks():
+    """bench.py's own rank path (timed_steps) under world 2: warmup steps are
+    untimed (step(None)), exactly `steps` timed steps, the reported time is the
+    max over ranks and identical on both ranks, and it covers the slow rank's
+    sleeps."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, el0, _, calls0), (_, el1, _, calls1) = res
+    assert el0 == el1                   # one max, seen by every rank
+    assert el1 >= 4 * 0.03              # includes rank 1's four timed sleeps
+    assert calls0 == calls1 == [None, None, 0, 1, 2, 3]

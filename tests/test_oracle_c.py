@@ -85,3 +85,45 @@ def test_libsodium_second_reference_agrees_on_canonical_triples():
         pytest.skip("libsodium not present")
     assert (got[0] == co.verify_strict_many(msgs, pks, sg, 2)).all()
     assert int(got[0].sum()) == len(range(0, n, 3))
+
+
+def test_c_oracle_certificate_verify_many_matches_pieces():
+    """coa_oracle_certificate_verify_many (the C3 all-core CPU baseline and
+    the C3 parity checker) gives, per certificate, the bits of the three
+    single checks it is made of, on any thread count."""
+    rnd = random.Random(3)
+    seeds = [bytes([i + 1]) * 32 for i in range(5)]
+    pks = [o.public_key(s) for s in seeds]
+    hin, ids, origins, hsigs, vp, vs, offs, exp = [], [], [], [], [], [], [0], []
+    for c in range(6):
+        author = c % 5
+        h = pks[author] + struct.pack("<Q", 7) + bytes(rnd.getrandbits(8) for _ in range(40))
+        hid = o.sha512(h)[:32]
+        sig = o.sign(seeds[author], hid)
+        cd = o.sha512(hid + struct.pack("<Q", 7) + pks[author])[:32]
+        votes = [(pks[v], o.sign(seeds[v], cd)) for v in range(4)]
+        bits = 0
+        if c == 1:
+            h = h[:-1] + bytes([h[-1] ^ 1]); bits |= 1
+        if c == 2:
+            sig = sig[:40] + bytes([sig[40] ^ 1]) + sig[41:]; bits |= 2
+        if c == 3:
+            votes[2] = (votes[2][0], votes[2][1][:5] + bytes([votes[2][1][5] ^ 1]) + votes[2][1][6:]); bits |= 4
+        if c == 4:
+            votes[0] = (pks[4], votes[0][1]); bits |= 4
+        hin.append(h); ids.append(hid); origins.append(pks[author]); hsigs.append(sig)
+        vp += [p for p, _ in votes]; vs += [s for _, s in votes]; offs.append(offs[-1] + len(votes))
+        exp.append(bits)
+    n = len(hin)
+    zs = np.frombuffer(bytes(rnd.getrandbits(8) for _ in range(16 * len(vp))), np.uint8).reshape(-1, 16)
+    arr = lambda xs, w: np.frombuffer(b"".join(xs), np.uint8).reshape(-1, w)  # noqa: E731
+    for threads in (1, 3, 8):
+        got = co.certificate_verify_many(hin, arr(ids, 32), arr(origins, 32), arr(hsigs, 64), 7, arr(vp, 32),
+                                         arr(vs, 64), np.array(offs, np.uint64), zs, threads)
+        assert list(got) == exp
+    # and each certificate's bits agree with the one-certificate helper's verdict
+    for c in range(n):
+        lo, hi = offs[c], offs[c + 1]
+        ok = co.certificate_verify(hin[c], ids[c], origins[c], hsigs[c], 7, vp[lo:hi], vs[lo:hi],
+                                   [int.from_bytes(bytes(z), "little") for z in zs[lo:hi]])
+        assert ok == (exp[c] == 0)

@@ -39,11 +39,45 @@ if [[ $STEPS == *sq* ]]; then
       -- python3 bench.py --no-cpu-baseline --no-secondary --steps 3 --warmup 1 > gpurun_out/pmc_SQ.json 2> gpurun_out/pmc_SQ.err \
     || { tail -30 gpurun_out/pmc_SQ.err; exit 1; }
 fi
-if [[ $STEPS == *pmc* ]]; then
+if [[ $STEPS == *fullprof* ]]; then
+  # the driver's exact command (python bench.py, defaults) under the kernel trace
+  run fullprof && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/fullprof -o run --output-format csv \
+      -- python3 bench.py > gpurun_out/bench_fullprof.json 2> gpurun_out/fullprof.err \
+    || { tail -30 gpurun_out/fullprof.err; exit 1; }
+  python3 tools/kernel_trace_summary.py gpurun_out/fullprof gpurun_out/fullprof_by_grid.json | head -40
+fi
+if [[ $STEPS == *verifypmc* ]]; then
+  # three counter passes of the C2 verify call -> profiles JSON tied to this build
+  run "pmc SQ" && timeout -k 10 -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY -T -d gpurun_out/vp/pmc_SQ -o run --output-format csv \
+      -- python3 bench.py --no-cpu-baseline --no-secondary --steps 3 --warmup 1 > gpurun_out/vp_sq.json 2> gpurun_out/vp_sq.err \
+    || { tail -30 gpurun_out/vp_sq.err; exit 1; }
+  for c in FETCH_SIZE WRITE_SIZE; do
+    run "pmc $c" && timeout -k 10 -s KILL 240 rocprofv3 --pmc $c -T -d gpurun_out/vp/pmc_$c -o run --output-format csv \
+        -- python3 bench.py --no-cpu-baseline --no-secondary --steps 3 --warmup 1 > gpurun_out/vp_$c.json 2> gpurun_out/vp_$c.err \
+      || { tail -30 gpurun_out/vp_$c.err; exit 1; }
+  done
+  python3 tools/pmc_verify.py gpurun_out/vp 65536 gpurun_out/verify_pmc.json > /dev/null && echo "verify_pmc ok"
+fi
+if [[ $STEPS == *pmc* ]] && [[ $STEPS != *verifypmc* ]]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     run "pmc $c" && timeout -k 10 300 rocprofv3 --pmc $c -T -d gpurun_out/pmc_$c -o run --output-format csv \
         -- python3 bench.py --no-cpu-baseline --no-secondary --steps 3 --warmup 1 > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err \
       || { tail -30 gpurun_out/pmc_$c.err; exit 1; }
   done
   find gpurun_out -path "*pmc_*" -name "*.csv" | head
+fi
+if [[ $STEPS == *latprobe* ]]; then
+  run latprobe && timeout -k 10 300 python3 tools/lat_probe.py > gpurun_out/lat_probe.jsonl 2> gpurun_out/lat_probe.err \
+    || { tail -30 gpurun_out/lat_probe.err; exit 1; }
+  cat gpurun_out/lat_probe.jsonl
+fi
+if [[ $STEPS == *onlytests* ]]; then
+  run onlytests && timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread $TESTS > gpurun_out/pytest_sel.log 2>&1 \
+    || { tail -40 gpurun_out/pytest_sel.log; exit 1; }
+  tail -15 gpurun_out/pytest_sel.log
+fi
+if [[ $STEPS == *vlat* ]]; then
+  run vlat && timeout -k 10 120 python3 tools/vlat_trace.py run > gpurun_out/vlat_trace.jsonl 2> gpurun_out/vlat_trace.err \
+    || { tail -30 gpurun_out/vlat_trace.err; exit 1; }
+  cat gpurun_out/vlat_trace.jsonl
 fi

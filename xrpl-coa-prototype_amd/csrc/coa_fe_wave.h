@@ -58,27 +58,30 @@ COA_DEV uint32_t wrap_step(uint64_t& m, uint32_t r) {
   return r < 8 ? hi : 0u;
 }
 // Per-lane values m_c < 2^40 on lanes 0..7 (0 above) -> 32-bit limbs of a
-// congruent value < 2^256.  Two passes leave carries of 0 or 1 that move on
-// only through 0xffffffff limbs, so the uniform branch to the rippling loop
-// is almost never taken.
+// congruent value < 2^256.  One pass leaves every lane below 2^32 + 2^14
+// (the carry from the lane below, or 38 times limb 7's), so a lane still has
+// a high word only when its low word was within 2^14 of 2^32: the uniform
+// branch to the rippling passes is almost never taken.
 COA_DEV uint32_t normalize(uint64_t m) {
   const uint32_t r = row_lane();
   wrap_step(m, r);
-  uint32_t hi = wrap_step(m, r);
 #pragma unroll 1
-  while (__any(hi != 0u)) hi = wrap_step(m, r);
+  while (__any((uint32_t)(m >> 32) != 0u)) wrap_step(m, r);
   return (uint32_t)m;
+}
+// 4p and 8p in unnormalised limbs (limb 0: 4p_0 = 2^33 - 76, limbs 1..7:
+// 2^33 - 2; doubled for 8p; 0 on lanes 8..15): added before a subtraction so
+// no lane goes negative
+COA_DEV uint64_t four_p() {
+  const uint32_t r = row_lane();
+  return r == 0 ? 0x1ffffffb4ull : (r < 8 ? 0x1fffffffeull : 0ull);
 }
 
 // a + b and a - b mod p (not canonical).  The difference adds 4p in
 // unnormalised limbs (limb 0: 2^33 - 76, limbs 1..7: 2^33 - 2), so no lane
 // goes negative.
 COA_DEV uint32_t add(uint32_t a, uint32_t b) { return normalize((uint64_t)a + b); }
-COA_DEV uint32_t sub(uint32_t a, uint32_t b) {
-  const uint32_t r = row_lane();
-  const uint64_t four_p = r == 0 ? 0x1ffffffb4ull : (r < 8 ? 0x1fffffffeull : 0ull);
-  return normalize((uint64_t)a + four_p - b);
-}
+COA_DEV uint32_t sub(uint32_t a, uint32_t b) { return normalize((uint64_t)a + four_p() - b); }
 
 // a * b mod p (not canonical), one product per 16-lane row.
 COA_DEV uint32_t mul(uint32_t a, uint32_t b) {

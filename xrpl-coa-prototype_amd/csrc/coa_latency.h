@@ -1,0 +1,21 @@
+// Internal launch wrapper of the single-signature latency kernel
+// (coa_latency.hip): crypto::Signature::verify (crypto/src/lib.rs:200-204)
+// for the few-at-a-time callers -- Header::verify and Vote::verify verify one
+// message at a time (primary/src/messages.rs:64-66,139-141).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct LatArgs {
+  const uint32_t* in;      // [n][32] dwords: msg (8) | pk (8) | R (8) | s (8)
+  uint32_t n;
+  uint8_t* verdicts;       // [n] 0 Ok / 1 Err
+  const uint32_t* keys;    // registered committee keys (sorted), or null
+  const uint32_t* kflags;  // [nk]
+  const uint32_t* ktabs;   // [nk] radix-256 combs of -A (coa_committee.h)
+  uint32_t nk;
+  const uint32_t* comb;    // radix-256 comb of B (coa_halved.h)
+};
+
+// One 256-thread workgroup (four waves) per signature.
+hipError_t coa_launch_verify_lat(const LatArgs& a, hipStream_t s);

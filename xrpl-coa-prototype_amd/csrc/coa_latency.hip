@@ -1,0 +1,365 @@
+// Single-signature latency kernel for gfx950: crypto::Signature::verify ==
+// ed25519-dalek 1.0.1 verify_strict (crypto/src/lib.rs:200-204), for callers
+// that verify one message at a time -- Header::verify and Vote::verify
+// (primary/src/messages.rs:64-66,139-141, from Core::process_header /
+// process_vote, primary/src/core.rs:306-336).
+//
+// The throughput kernels (coa_halved.hip) give each signature ONE lane, so a
+// lone signature waits for a whole one-lane verification (~0.9 ms).  Here one
+// 256-thread workgroup (four waves, four SIMDs) works on one signature and
+// the latency-bound chains run on 16-lane DPP rows (coa_fe_wave.h,
+// coa_ge_rows.h):
+//
+//   key registered (coa_committee_register; committee keys are fixed per
+//   config::Committee):
+//     wave 0  k = SHA-512(R || A || M) mod l, then [k](-A) from the key's
+//             radix-256 comb: one term per lane, summed by a 5-level butterfly
+//     wave 2  [s]B from B's comb the same way (needs no hash, runs meanwhile)
+//     wave 1  R's decompression, the power chain on the rows
+//     then wave 0: P = [s]B + [k](-A), verify_strict's small-order test of R
+//     taken on P (an accepting verdict needs R == P), P == R projectively.
+//   key not registered (the halved-scalar check of coa_halved.hip):
+//     wave 0  k, the halving (c, d) with c == d k (mod 8l), e = d s mod l
+//     wave 3  A's decompression (rows), small-order test, table j(-A), j <= 8
+//     wave 1  the same for R
+//     then, in parallel: wave 3 [c](-A) and wave 1 [|d|](-/+R) by signed
+//     radix-16 Horner chains on the rows, wave 2 [e]B from B's comb; wave 0
+//     sums the three and tests Q == O.
+// Both verdicts are dalek's bit for bit: the cached one by the same argument
+// as k_cert_verify_lat's header job, the uncached one by the halving argument
+// of coa_halved.hip (Q == [d]P exactly, d odd).
+#include "coa_latency.h"
+
+#include "coa_fe.h"
+#include "coa_ge.h"
+#include "coa_ge_rows.h"
+#include "coa_halve.h"
+#include "coa_halved.h"
+#include "coa_committee.h"
+#include "coa_keycache.h"
+#include "coa_sc.h"
+#include "coa_sha512.h"
+#include "coa_smul.h"
+
+namespace {
+using namespace coa_kc;
+
+// one comb term per lane (lanes 0..31; the upper half sums a copy) of the
+// radix-256 comb `tab` for the 8-dword scalar dg, summed by an xor butterfly:
+// every lane ends with sum_j tab[j][byte j of dg] (signed digits)
+COA_DEV void comb_butterfly(ge_p3& P, uint32_t* dg, const uint32_t* tab, uint32_t lane) {
+  add_const_word(dg, 0x80808080u);
+  const int j = lane & 31;
+  const int e = (int)byte_of(dg, j) - 128;
+  ge_niels q;
+  comb_select(q, tab, j, e);
+  ge_p1p1 t;
+  ge_p3_identity(P);
+  ge_madd(t, P, q);
+  ge_p1p1_to_p3(P, t);
+#pragma unroll 1
+  for (int off = 16; off >= 1; off >>= 1) {
+    ge_p3 O;
+    shfl_fe<64>(O.X, P.X, off);
+    shfl_fe<64>(O.Y, P.Y, off);
+    shfl_fe<64>(O.Z, P.Z, off);
+    shfl_fe<64>(O.T, P.T, off);
+    ge_cached oc;
+    ge_p3_to_cached(oc, O);
+    ge_add(t, P, oc);
+    ge_p1p1_to_p3(P, t);
+  }
+}
+
+COA_DEV void lds_put_p3(uint32_t* d, const ge_p3& P) {
+  const fe* f[4] = {&P.X, &P.Y, &P.Z, &P.T};
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+#pragma unroll
+    for (int i = 0; i < 8; i++) d[q * 8 + i] = f[q]->v[i];
+}
+COA_DEV void lds_get_p3(ge_p3& P, const uint32_t* d) {
+  fe* f[4] = {&P.X, &P.Y, &P.Z, &P.T};
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+#pragma unroll
+    for (int i = 0; i < 8; i++) f[q]->v[i] = d[q * 8 + i];
+}
+
+// row-form table entry: 4 coordinates x 8 limbs in LDS (row 0 writes)
+COA_DEV void tab_put(uint32_t* e, const rp::Ca& c) {
+  const uint32_t l = __lane_id();
+  if (l < 8) {
+    e[l] = c.ypx;
+    e[8 + l] = c.ymx;
+    e[16 + l] = c.Z;
+    e[24 + l] = c.t2d;
+  }
+}
+// entry |d| - 1 of the table (identity for d = 0), negated for d < 0
+COA_DEV void tab_get(rp::Ca& c, const uint32_t* tab, int d) {
+  const int m = d < 0 ? -d : d;
+  const uint32_t l = __lane_id() & 15u;
+  if (m == 0) {
+    const uint32_t one = l == 0 ? 1u : 0u;
+    c.ypx = one;
+    c.ymx = one;
+    c.Z = one;
+    c.t2d = 0;
+    return;
+  }
+  const uint32_t* e = tab + (m - 1) * 32;
+  const uint32_t ypx = l < 8 ? e[l] : 0u, ymx = l < 8 ? e[8 + l] : 0u;
+  c.Z = l < 8 ? e[16 + l] : 0u;
+  const uint32_t t2d = l < 8 ? e[24 + l] : 0u;
+  if (d < 0) {  // -(x, y) = (-x, y): swap Y+X and Y-X, negate 2dT
+    c.ypx = ymx;
+    c.ymx = ypx;
+    c.t2d = fw::sub(0u, t2d);
+  } else {
+    c.ypx = ypx;
+    c.ymx = ymx;
+    c.t2d = t2d;
+  }
+}
+
+// tab[j - 1] = j * (-Q), j = 1..8, in cached form (row arithmetic)
+COA_DEV void build_table(uint32_t* tab, const ge_p3& Q) {
+  rp::P1 base, cur;
+  rp::L1 t;
+  rp::from_p3(base, Q);
+  rp::neg(cur, base);
+  rp::Ca c1, cj;
+  rp::to_cached(c1, cur);
+  tab_put(tab, c1);
+#pragma unroll 1
+  for (int j = 1; j < 8; j++) {
+    rp::add(t, cur, c1);
+    rp::to_p3(cur, t);
+    rp::to_cached(cj, cur);
+    tab_put(tab + j * 32, cj);
+  }
+}
+
+// sum_pos digit_pos 16^pos * table point, digits = nibble pos of rec minus 8
+// (negated when neg), by a signed radix-16 Horner chain on the rows
+COA_DEV void horner(ge_p3& out, const uint32_t* tab, const uint32_t* rec, int H, bool neg) {
+  rp::P1 acc3;
+  rp::L1 t;
+  rp::P2 acc2;
+  rp::identity(acc3);
+  rp::Ca q;
+#pragma unroll 1
+  for (int pos = H - 1; pos >= 0; pos--) {
+    int d = (int)((word_sel(rec, pos >> 3) >> (4 * (pos & 7))) & 15u) - 8;
+    if (neg) d = -d;
+    if (pos != H - 1) {
+#pragma unroll 1
+      for (int k = 0; k < 3; k++) {
+        rp::dbl(t, acc2);
+        rp::to_p2(acc2, t);
+      }
+      rp::dbl(t, acc2);
+      rp::to_p3(acc3, t);
+    }
+    tab_get(q, tab, d);
+    rp::add(t, acc3, q);
+    if (pos != 0) rp::to_p2(acc2, t);
+  }
+  rp::to_p3(acc3, t);
+  rp::to_ge_p3(out, acc3);
+}
+
+}  // namespace
+
+#ifdef COA_VLAT_TRACE  // phase timestamps of item 0 per wave (tools/vlat_trace.py)
+__device__ unsigned long long g_vlat_trace[4][8];
+#define VMARK(i) \
+  if (item == 0 && lane == 0) g_vlat_trace[wave][i] = clock64();
+extern "C" int coa_vlat_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vlat_trace), sizeof(g_vlat_trace)) == hipSuccess ? 0 : -1;
+}
+#else
+#define VMARK(i)
+#endif
+
+__global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
+  __shared__ uint32_t sh_rec[24];      // c' | d' | e (wave 0, uncached path)
+  __shared__ uint32_t sh_meta[4];      // H, d < 0, s < l
+  __shared__ uint32_t sh_ok[4];        // per wave: decompression ok and not small order
+  __shared__ uint32_t sh_pt[3][32];    // points handed to wave 0
+  __shared__ uint32_t sh_tab[2][8 * 32];  // j(-A), j(-R) in cached form (uncached path)
+  __shared__ uint32_t sh_r[17];        // R (X, Y) and its decompression verdict (cached path)
+  const uint32_t wave = coa_sha::uni(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t item = blockIdx.x;
+  const uint32_t* in = a.in + (uint64_t)item * 32;
+  uint32_t msg[8], pk[8], rw[8], sw[8];
+  load8u(msg, in);
+  load8u(pk, in + 8);
+  load8u(rw, in + 16);
+  load8u(sw, in + 24);
+  VMARK(0)
+  const int slot = a.nk ? key_lookup_u(a.keys, a.nk, pk) : -1;
+
+  if (slot >= 0) {  // ------------------------------------------ cached key
+    ge_p3 P;
+    uint32_t pre = 0;
+    if (wave == 1) {
+      ge_p3 R;
+      const bool ok = ge_decompress<true>(R, rw);
+      if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          sh_r[i] = R.X.v[i];
+          sh_r[8 + i] = R.Y.v[i];
+        }
+        sh_r[16] = ok;
+      }
+    } else if (wave == 2) {
+      uint32_t dg[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) dg[i] = sw[i];
+      comb_butterfly(P, dg, a.comb, lane);
+      if (lane == 0) lds_put_p3(sh_pt[0], P);
+    } else if (wave == 0) {
+      uint64_t st[8];
+      uint32_t h[16], w[24];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        w[i] = rw[i];
+        w[8 + i] = pk[i];
+        w[16 + i] = msg[i];
+      }
+      coa_sha::hash_words<24>(st, w);
+      coa_sha::state_to_le_words(h, st);
+      sc k;
+      sc_reduce512(k, h);
+      const uint32_t kf = coa_sha::uni(a.kflags[slot]);
+      pre = (sc_is_canonical(sw) ? 0u : 1u) | ((kf & COA_KEY_DECOMPRESSES) ? 0u : 2u) |
+            ((kf & COA_KEY_SMALL_ORDER) ? 4u : 0u);
+      comb_butterfly(P, k.v, a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS, lane);
+    }
+    VMARK(1)
+    __syncthreads();
+    VMARK(2)
+    if (wave == 0) {
+      ge_p3 S;
+      lds_get_p3(S, sh_pt[0]);
+      ge_cached sc4;
+      ge_p3_to_cached(sc4, S);
+      ge_p1p1 t;
+      ge_add(t, P, sc4);
+      ge_p1p1_to_p3(P, t);
+      // verify_strict's small-order test of R, taken on P: an accepting
+      // verdict needs R == P, and every other verdict is Err already
+      const bool small_r = ge_is_small_order(P);
+      ge_p3 R;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        R.X.v[i] = sh_r[i];
+        R.Y.v[i] = sh_r[8 + i];
+      }
+      fe_set(R.Z, 1);
+      ge_p2 P2;
+      ge_p3_to_p2(P2, P);
+      const bool ok = pre == 0 && sh_r[16] != 0 && !small_r && ge_p2_eq_p3(P2, R);
+      if (lane == 0) a.verdicts[item] = ok ? 0 : 1;
+      VMARK(3)
+    }
+    return;
+  }
+
+  // ------------------------------------------------------ uncached key
+  if (wave == 0) {
+    uint64_t st[8];
+    uint32_t h[16], w[24];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      w[i] = rw[i];
+      w[8 + i] = pk[i];
+      w[16 + i] = msg[i];
+    }
+    coa_sha::hash_words<24>(st, w);
+    coa_sha::state_to_le_words(h, st);
+    sc k;
+    sc_reduce512(k, h);
+    uint32_t c[8], d[8];
+    int cost;
+    bool neg;
+    coa_halve::halve(c, d, cost, neg, k.v);
+    sc e;
+    sc_mul(e, d, sw);  // s may be non-canonical here; the verdict rejects it
+    if (neg) {
+      sc en;
+      sc_neg(en, e.v);
+      e = en;
+    }
+    add_const_word(c, 0x88888888u);
+    add_const_word(d, 0x88888888u);
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        sh_rec[i] = c[i];
+        sh_rec[8 + i] = d[i];
+        sh_rec[16 + i] = e.v[i];
+      }
+      sh_meta[0] = (uint32_t)((cost + 2 + 3) / 4);  // c, |d| < 2^(4H - 2)
+      sh_meta[1] = neg;
+      sh_meta[2] = sc_is_canonical(sw);
+    }
+  } else if (wave == 1 || wave == 3) {
+    ge_p3 Q;
+    const bool dec = ge_decompress<true>(Q, wave == 3 ? pk : rw);
+    const bool ok = dec && !ge_is_small_order(Q);
+    build_table(sh_tab[wave == 3 ? 0 : 1], Q);
+    if (lane == 0) sh_ok[wave] = ok;
+  }
+  VMARK(1)
+  __syncthreads();
+  VMARK(2)
+  const int H = (int)coa_sha::uni(sh_meta[0]);
+  const bool dneg = coa_sha::uni(sh_meta[1]) != 0;
+  if (wave == 1 || wave == 3) {
+    uint32_t rec[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) rec[i] = coa_sha::uni(sh_rec[(wave == 3 ? 0 : 8) + i]);
+    ge_p3 T;
+    horner(T, sh_tab[wave == 3 ? 0 : 1], rec, H, wave == 1 && dneg);
+    if (lane == 0) lds_put_p3(sh_pt[wave == 3 ? 0 : 1], T);
+  } else if (wave == 2) {
+    uint32_t e[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) e[i] = coa_sha::uni(sh_rec[16 + i]);
+    ge_p3 E;
+    comb_butterfly(E, e, a.comb, lane);
+    if (lane == 0) lds_put_p3(sh_pt[2], E);
+  }
+  VMARK(3)
+  __syncthreads();
+  VMARK(4)
+  if (wave == 0) {
+    ge_p3 Q, T;
+    ge_cached c;
+    ge_p1p1 t;
+    lds_get_p3(Q, sh_pt[2]);
+#pragma unroll 1
+    for (int i = 0; i < 2; i++) {
+      lds_get_p3(T, sh_pt[i]);
+      ge_p3_to_cached(c, T);
+      ge_add(t, Q, c);
+      ge_p1p1_to_p3(Q, t);
+    }
+    ge_p2 q2;
+    ge_p3_to_p2(q2, Q);
+    const bool ok = sh_meta[2] != 0 && sh_ok[1] != 0 && sh_ok[3] != 0 && ge_p2_is_identity(q2);
+    if (lane == 0) a.verdicts[item] = ok ? 0 : 1;
+    VMARK(5)
+  }
+}
+
+hipError_t coa_launch_verify_lat(const LatArgs& a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_verify_lat, dim3(a.n), dim3(256), 0, s, a);
+  return hipGetLastError();
+}

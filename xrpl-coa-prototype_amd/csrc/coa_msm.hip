@@ -36,6 +36,7 @@
 
 #include "coa_fe.h"
 #include "coa_ge.h"
+#include "coa_ge_rows.h"
 #include "coa_sc.h"
 
 namespace {
@@ -491,75 +492,6 @@ __global__ void __launch_bounds__(256) k_msm_wsum(const uint32_t* __restrict__ p
 }
 
 // ------------------------------------------------------ Horner + verdict
-namespace {
-// k_msm_final in row form (coa_fe_wave.h): every coordinate is one uint32 per
-// lane, each 16-lane row holding the whole element (limb c on lane c).  A
-// step's four products run on the four rows at once, row r on operand pair
-// r (a per-lane select), and every row then reads all four results back
-// (three lane-swap instructions, rows4).  Additions and subtractions stay on the rows.
-namespace rp {
-struct P2 {
-  uint32_t X, Y, Z;
-};
-struct P1 {
-  uint32_t X, Y, Z, T;
-};
-struct Ca {
-  uint32_t ypx, ymx, Z, t2d;
-};
-COA_DEV uint32_t pick(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  const uint32_t r = __lane_id() >> 4;
-  return r == 0 ? a : (r == 1 ? b : (r == 2 ? c : d));
-}
-// Row r's value to every row, for all four rows at once: v_permlane32_swap
-// of q with itself gives (r0 r1 r0 r1) and (r2 r3 r2 r3); v_permlane16_swap of
-// each with itself splits it into two broadcasts (tools/probe_permlane.hip
-// checked the lane mapping on gfx950).  Three VALU instructions, no LDS.
-COA_DEV void rows4(uint32_t q, uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_t& r3) {
-  const auto h = __builtin_amdgcn_permlane32_swap(q, q, false, false);
-  const auto lo = __builtin_amdgcn_permlane16_swap(h[0], h[0], false, false);
-  const auto hi = __builtin_amdgcn_permlane16_swap(h[1], h[1], false, false);
-  r0 = lo[0];
-  r1 = lo[1];
-  r2 = hi[0];
-  r3 = hi[1];
-}
-// 2P (p1p1) from projective P: ge_p2_dbl with its four squarings on the rows
-COA_DEV void dbl(P1& r, const P2& p) {
-  const uint32_t s = fw::add(p.X, p.Y);
-  const uint32_t x = pick(p.X, p.Y, p.Z, s);
-  uint32_t xx, yy, zz, aa;
-  rows4(fw::mul(x, x), xx, yy, zz, aa);
-  const uint32_t zz2 = fw::add(zz, zz);
-  r.Y = fw::add(yy, xx);
-  r.Z = fw::sub(yy, xx);
-  r.X = fw::sub(aa, r.Y);
-  r.T = fw::sub(zz2, r.Z);
-}
-COA_DEV void to_p2(P2& r, const P1& p) {
-  uint32_t unused;
-  rows4(fw::mul(pick(p.X, p.Y, p.Z, p.Z), pick(p.T, p.Z, p.T, p.T)), r.X, r.Y, r.Z, unused);
-}
-COA_DEV void to_p3(P1& r, const P1& p) {
-  rows4(fw::mul(pick(p.X, p.Y, p.Z, p.X), pick(p.T, p.Z, p.T, p.Y)), r.X, r.Y, r.Z, r.T);
-}
-// p (extended) + q (cached) -> p1p1, as ge_add
-COA_DEV void add(P1& r, const P1& p, const Ca& c) {
-  const uint32_t ypx = fw::add(p.Y, p.X), ymx = fw::sub(p.Y, p.X);
-  uint32_t b, a, cc, zz;
-  rows4(fw::mul(pick(ypx, ymx, c.t2d, p.Z), pick(c.ypx, c.ymx, p.T, c.Z)), b, a, cc, zz);
-  const uint32_t zz2 = fw::add(zz, zz);
-  r.X = fw::sub(b, a);
-  r.Y = fw::add(b, a);
-  r.Z = fw::add(zz2, cc);
-  r.T = fw::sub(zz2, cc);
-}
-COA_DEV uint32_t ld(const uint32_t* base) {  // this lane's limb (0 on lanes 8..15 of the row)
-  const uint32_t c = __lane_id() & 15u;
-  return c < 8 ? base[c] : 0u;
-}
-}  // namespace rp
-}  // namespace
 
 __global__ void __launch_bounds__(64) k_msm_final(const uint32_t* __restrict__ wsum, const uint32_t* __restrict__ bad,
                                                   uint8_t* __restrict__ verdict) {
@@ -579,7 +511,8 @@ __global__ void __launch_bounds__(64) k_msm_final(const uint32_t* __restrict__ w
   __syncthreads();
   const uint32_t* top = wsum + (uint64_t)(WA - 1) * 32;
   rp::P2 acc = {rp::ld(top), rp::ld(top + 8), rp::ld(top + 16)};
-  rp::P1 r, a3;
+  rp::L1 r;
+  rp::P1 a3;
 #pragma unroll 1
   for (int w = WA - 2; w >= 0; w--) {
 #pragma unroll 1

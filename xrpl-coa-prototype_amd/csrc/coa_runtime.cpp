@@ -38,6 +38,7 @@
 #include "coa_committee.h"
 #include "coa_halved.h"
 #include "coa_kernels.h"
+#include "coa_latency.h"
 
 namespace {
 
@@ -168,13 +169,14 @@ struct Dev {
   // committee key cache (f2): sorted keys, flags, one comb of -A per key
   DevBuf ckeys, kflags, ktabs, kwtabs, cert, cscr;
   DevBuf msm;  // Pippenger workspace (one large verify_batch group)
+  DevBuf lat;  // single-signature latency path: inputs + verdicts
   bool kwide = false;  // kwtabs holds the committee's wide combs
   uint32_t nkeys = 0;
   PinBuf pin;
   std::mutex mu;
   std::vector<DevBuf*> all() {
     return {&msgs,  &pks,  &sigs, &kbuf, &rec, &verdicts, &scratch, &aux,  &rbuf,   &seeds, &offs,
-            &data,  &out,  &idx,  &zs,   &terms, &flags,  &ckeys,   &kflags, &ktabs, &kwtabs, &cert, &cscr, &msm};
+            &data,  &out,  &idx,  &zs,   &terms, &flags,  &ckeys,   &kflags, &ktabs, &kwtabs, &cert, &cscr, &msm, &lat};
   }
 };
 
@@ -372,6 +374,46 @@ int enqueue_verify(Dev& d, const uint8_t* d_msgs, size_t msg_len, const uint8_t*
     return enqueue_split(d, d_msgs ? d_msgs : d_pks, msg_len, nullptr, d_pks, d_sigs, n, d_verdicts, w, s);
   HIP_TRY(coa_launch_hram(d_msgs, (uint32_t)msg_len, msg_len, nullptr, d_pks, d_sigs, (uint32_t)n, w.k, s));
   return enqueue_verify_prehashed(d, d_pks, d_sigs, n, d_verdicts, w.k, w, s);
+}
+
+// Calls of at most lat_max() signatures with 32-byte messages take the
+// single-signature latency kernel (coa_latency.hip, one workgroup per
+// signature: faster than the split kernels up to ~2k signatures,
+// tools/lat_probe.py); COA_LAT_MAX overrides (0 = never).
+size_t lat_max() {
+  const char* e = getenv("COA_LAT_MAX");
+  return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)2048;
+}
+
+// n <= lat_max() triples with 32-byte messages through k_verify_lat on device
+// d (its lock held, device set): one pinned staging buffer, one H2D, one
+// launch, one D2H.
+int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, size_t n, uint8_t* out) {
+  const size_t in_bytes = n * 128, vofs = align_up(in_bytes, 256);
+  HIP_TRY(d.pin.ensure(vofs + n));
+  HIP_TRY(d.lat.ensure(vofs + n));
+  uint8_t* h = static_cast<uint8_t*>(d.pin.p);
+  for (size_t i = 0; i < n; i++) {
+    std::memcpy(h + i * 128, msgs + i * 32, 32);
+    std::memcpy(h + i * 128 + 32, pks + i * 32, 32);
+    std::memcpy(h + i * 128 + 64, sigs + i * 64, 64);
+  }
+  hipStream_t s = d.stream;
+  HIP_TRY(hipMemcpyAsync(d.lat.p, h, in_bytes, hipMemcpyHostToDevice, s));
+  LatArgs a;
+  a.in = d.lat.as<uint32_t>();
+  a.n = (uint32_t)n;
+  a.verdicts = d.lat.as<uint8_t>() + vofs;
+  a.keys = d.ckeys.as<uint32_t>();
+  a.kflags = d.kflags.as<uint32_t>();
+  a.ktabs = d.ktabs.as<uint32_t>();
+  a.nk = d.nkeys;
+  a.comb = d.comb;
+  HIP_TRY(coa_launch_verify_lat(a, s));
+  HIP_TRY(hipMemcpyAsync(h + vofs, a.verdicts, n, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  std::memcpy(out, h + vofs, n);
+  return COA_OK;
 }
 
 int check_n(size_t n) {
@@ -926,6 +968,12 @@ int coa_ed25519_verify_strict_many(const uint8_t* msgs, size_t msg_len, const ui
   if (n == 0) return COA_OK;
   if ((!msgs && msg_len) || !pks || !sigs || !verdicts_out) return fail(COA_EINVAL, "null argument");
   if (check_n(n) != COA_OK) return COA_EINVAL;
+  if (msg_len == 32 && n <= lat_max()) {  // few signatures: the latency kernel, first device
+    Dev& d = *g_devs[0];
+    std::lock_guard<std::mutex> l(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    return lat_verify(d, msgs, pks, sigs, n, verdicts_out);
+  }
   return for_shards(n, [&](Dev& d, size_t lo, size_t hi) -> int {
     const size_t cnt = hi - lo;
     hipStream_t s = d.stream;
