@@ -585,15 +585,25 @@ def certificate_config(n_certs, latency_samples, cpu_threads, dev, stream, commi
     return res
 
 
-def lib_sha256():
-    """sha256 of the engine library this process loaded (ties a committed
-    counter profile to the exact build it was taken on)."""
+# Sources that make up the C2 verify kernels (k_pre_halve, k_verify_main) and
+# the build flags: a counter profile stays valid while these are unchanged.
+VERIFY_KERNEL_SOURCES = ("coa_halved.hip", "coa_halved.h", "coa_halve.h", "coa_fe.h", "coa_ge.h", "coa_sc.h",
+                         "coa_sha512.h", "coa_smul.h", "coa_kernels.h")
+
+
+def verify_kernel_src_sha256():
+    """sha256 over the C2 verify kernels' sources and the build flags (ties a
+    committed counter profile to the code it was taken on)."""
     import hashlib
 
-    import coa_crypto
+    sys.path.insert(0, PKG)
+    import build as engine_build
 
-    with open(coa_crypto.LIB_PATH, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()
+    h = hashlib.sha256(" ".join(engine_build.COMMON).encode())
+    for name in VERIFY_KERNEL_SOURCES:
+        with open(os.path.join(PKG, "csrc", name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()
 
 
 def load_pmc(n):
@@ -610,8 +620,8 @@ def load_pmc(n):
         return None, f"{os.path.relpath(path, ROOT)} unreadable: {e}"
     if pj.get("n") != n:
         return None, f"{os.path.relpath(path, ROOT)} was taken at n={pj.get('n')}"
-    if pj.get("lib_sha256") != lib_sha256():
-        return None, f"{os.path.relpath(path, ROOT)} was taken on another library build"
+    if pj.get("kernel_src_sha256") != verify_kernel_src_sha256():
+        return None, f"{os.path.relpath(path, ROOT)} was taken on other kernel sources"
     pj["_path"] = os.path.relpath(path, ROOT)
     return pj, None
 
@@ -754,7 +764,7 @@ def main():
         roof["counters"] = (f"{pmc['_path']}: rocprofv3 --pmc SQ_INSTS_VALU (issue_frac = VALU wave-instructions "
                             f"per call x {VALU_ISSUE_CYCLES} cycles / ({SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz x "
                             f"this run's call time)) and FETCH_SIZE x 2 + WRITE_SIZE (traffic, per call), taken "
-                            f"on this exact library build (sha256 match) at n={n}; copied, not measured in "
+                            f"on these exact kernel sources (sha256 match) at n={n}; copied, not measured in "
                             f"this run")
     else:
         roof["issue_frac"] = None

@@ -1,0 +1,178 @@
+//! `Certificate::verify` (primary/src/messages.rs:189-215) with its crypto in
+//! ONE engine call (`coa_certificate_verify`: Header::digest == id, the
+//! header's Signature::verify, Certificate::digest and the votes'
+//! verify_batch, fused on the device over the registered committee's key
+//! combs), the non-crypto checks in the reference's order.  The crypto bits
+//! are pure functions of the certificate's bytes, so reading them up front and
+//! consuming them in the reference's order returns exactly the reference's
+//! DagError.
+//!
+//! Wiring in `primary/src/messages.rs`:
+//!     #[path = "gpu_certificate.rs"] mod gpu_certificate;
+//!     impl Certificate {
+//!         pub fn verify(&self, committee: &Committee) -> DagResult<()> {
+//!             gpu_certificate::verify(self, committee)
+//!         }
+//!     }
+//! and in node/src/main.rs, once after Committee::import:
+//!     crypto::gpu::register_committee(committee.authorities.keys());
+//! `primary/Cargo.toml` needs nothing new (crypto is already a dependency;
+//! the FFI lives in crypto's `coa_ffi`, re-exported below).
+use crate::error::{DagError, DagResult};
+use crate::messages::{Certificate, Header};
+use config::Committee;
+use crypto::{CryptoError, PublicKey};
+use std::collections::HashSet;
+use std::os::raw::c_int;
+
+extern "C" {
+    // include/coa_verify.h; the symbols come from libcoa_verify.so, which the
+    // crypto crate's build.rs links
+    fn coa_certificate_verify(header_data: *const u8, header_len: usize, id: *const u8, origin: *const u8,
+                              header_sig: *const u8, round: u64, vote_pks: *const u8, vote_sigs: *const u8,
+                              n_votes: usize, rng_seed: u64) -> c_int;
+    fn coa_certificate_verify_many(header_data: *const u8, header_offsets: *const u64, ids: *const u8,
+                                   origins: *const u8, header_sigs: *const u8, rounds: *const u64,
+                                   vote_pks: *const u8, vote_sigs: *const u8, vote_offsets: *const u64,
+                                   n: usize, rng_seed: u64, status_out: *mut u8) -> c_int;
+    fn coa_last_error() -> *const std::os::raw::c_char;
+}
+
+const BAD_HEADER_ID: c_int = 1;
+const BAD_HEADER_SIG: c_int = 2;
+const BAD_VOTES: c_int = 4;
+
+fn engine_failure(rc: c_int) -> ! {
+    let msg = unsafe { std::ffi::CStr::from_ptr(coa_last_error()) }.to_string_lossy().into_owned();
+    panic!("MI355X verification engine failure {}: {}", rc, msg)
+}
+
+/// The bytes Header::digest hashes (primary/src/messages.rs:70-84):
+/// author || round (u64 LE) || (payload digest || worker id (u32 LE))* in the
+/// BTreeMap's key order || parent digests in the BTreeSet's order.
+pub fn header_digest_input(h: &Header) -> Vec<u8> {
+    let mut out = Vec::with_capacity(32 + 8 + 36 * h.payload.len() + 32 * h.parents.len());
+    out.extend_from_slice(&h.author.0);
+    out.extend_from_slice(&h.round.to_le_bytes());
+    for (digest, worker_id) in &h.payload {
+        out.extend_from_slice(&digest.0);
+        out.extend_from_slice(&worker_id.to_le_bytes());
+    }
+    for parent in &h.parents {
+        out.extend_from_slice(&parent.0);
+    }
+    out
+}
+
+/// The 64-byte R || s of a crypto::Signature through its serde form
+/// (the fields are private; bincode writes part1 then part2, 32 bytes each,
+/// with no length prefix for fixed arrays).
+fn signature_bytes(sig: &crypto::Signature) -> [u8; 64] {
+    let v = bincode::serialize(sig).expect("Signature serializes");
+    let mut out = [0u8; 64];
+    out.copy_from_slice(&v[..64]);
+    out
+}
+
+fn votes_flat(cert: &Certificate) -> (Vec<u8>, Vec<u8>) {
+    let (mut pks, mut sigs) = (Vec::with_capacity(32 * cert.votes.len()), Vec::with_capacity(64 * cert.votes.len()));
+    for (name, sig) in &cert.votes {
+        pks.extend_from_slice(&name.0);
+        sigs.extend_from_slice(&signature_bytes(sig));
+    }
+    (pks, sigs)
+}
+
+/// The checks of Certificate::verify in the reference's order, the crypto
+/// ones read from the engine's status bits.
+fn checks_in_order(cert: &Certificate, committee: &Committee, st: c_int) -> DagResult<()> {
+    let h = &cert.header;
+    // Header::verify (:48-67)
+    ensure!(st & BAD_HEADER_ID == 0, DagError::InvalidHeaderId);
+    ensure!(committee.stake(&h.author) > 0, DagError::UnknownAuthority(h.author));
+    for worker_id in h.payload.values() {
+        committee
+            .worker(&h.author, worker_id)
+            .map_err(|_| DagError::MalformedHeader(h.id.clone()))?;
+    }
+    ensure!(st & BAD_HEADER_SIG == 0, DagError::InvalidSignature(CryptoError::new()));
+    // quorum (:196-211)
+    let mut weight = 0;
+    let mut used: HashSet<PublicKey> = HashSet::new();
+    for (name, _) in cert.votes.iter() {
+        ensure!(!used.contains(name), DagError::AuthorityReuse(*name));
+        let voting_rights = committee.stake(name);
+        ensure!(voting_rights > 0, DagError::UnknownAuthority(*name));
+        used.insert(*name);
+        weight += voting_rights;
+    }
+    ensure!(weight >= committee.quorum_threshold(), DagError::CertificateRequiresQuorum);
+    // verify_batch (:214)
+    ensure!(st & BAD_VOTES == 0, DagError::InvalidSignature(CryptoError::new()));
+    Ok(())
+}
+
+/// Certificate::verify, one certificate (the engine's latency path: one
+/// H2D, one launch, one D2H).
+pub fn verify(cert: &Certificate, committee: &Committee) -> DagResult<()> {
+    // Genesis certificates are always valid (:191-193).
+    if Certificate::genesis(committee).contains(cert) {
+        return Ok(());
+    }
+    let h = &cert.header;
+    let bytes = header_digest_input(h);
+    let (pks, sigs) = votes_flat(cert);
+    let hsig = signature_bytes(&h.signature);
+    let st = unsafe {
+        coa_certificate_verify(bytes.as_ptr(), bytes.len(), h.id.0.as_ptr(), h.author.0.as_ptr(), hsig.as_ptr(),
+                               h.round, pks.as_ptr(), sigs.as_ptr(), cert.votes.len(), 0)
+    };
+    if st < 0 {
+        engine_failure(st);
+    }
+    checks_in_order(cert, committee, st)
+}
+
+/// Certificate::verify for a window of certificates (the aggregation stage):
+/// the crypto of all of them in one coa_certificate_verify_many call, then
+/// each certificate's checks in the reference's order.
+pub fn verify_many(certs: &[&Certificate], committee: &Committee) -> Vec<DagResult<()>> {
+    let genesis = Certificate::genesis(committee);
+    let todo: Vec<usize> = (0..certs.len()).filter(|&i| !genesis.contains(certs[i])).collect();
+    let n = todo.len();
+    let mut hdata = Vec::new();
+    let mut hoff = vec![0u64];
+    let (mut ids, mut origins, mut hsigs) = (Vec::with_capacity(32 * n), Vec::with_capacity(32 * n), Vec::with_capacity(64 * n));
+    let mut rounds = Vec::with_capacity(n);
+    let (mut vpks, mut vsigs) = (Vec::new(), Vec::new());
+    let mut voff = vec![0u64];
+    for &i in &todo {
+        let h = &certs[i].header;
+        hdata.extend_from_slice(&header_digest_input(h));
+        hoff.push(hdata.len() as u64);
+        ids.extend_from_slice(&h.id.0);
+        origins.extend_from_slice(&h.author.0);
+        hsigs.extend_from_slice(&signature_bytes(&h.signature));
+        rounds.push(h.round);
+        let (p, s) = votes_flat(certs[i]);
+        vpks.extend_from_slice(&p);
+        vsigs.extend_from_slice(&s);
+        voff.push((vpks.len() / 32) as u64);
+    }
+    let mut status = vec![0u8; n];
+    if n > 0 {
+        let rc = unsafe {
+            coa_certificate_verify_many(hdata.as_ptr(), hoff.as_ptr(), ids.as_ptr(), origins.as_ptr(),
+                                        hsigs.as_ptr(), rounds.as_ptr(), vpks.as_ptr(), vsigs.as_ptr(),
+                                        voff.as_ptr(), n, 0, status.as_mut_ptr())
+        };
+        if rc < 0 {
+            engine_failure(rc);
+        }
+    }
+    let mut out: Vec<DagResult<()>> = (0..certs.len()).map(|_| Ok(())).collect();
+    for (j, &i) in todo.iter().enumerate() {
+        out[i] = checks_in_order(certs[i], committee, status[j] as c_int);
+    }
+    out
+}

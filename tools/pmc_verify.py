@@ -8,8 +8,9 @@ Reads three rocprofv3 --pmc passes of `bench.py --no-cpu-baseline
   <root>/pmc_WRITE_SIZE  WRITE_SIZE
 keeps the dispatches of the given kernels whose grid matches the C2 launch
 (n items), takes per-kernel medians over dispatches and writes one JSON with
-the sha256 of the library the passes ran (bench.py uses the figures only on
-that exact build).  FETCH_SIZE/WRITE_SIZE are KiB; FETCH_SIZE is doubled (the
+the sha256 of the kernels' sources and build flags
+(bench.verify_kernel_src_sha256; bench.py uses the figures only while those
+are unchanged).  FETCH_SIZE/WRITE_SIZE are KiB; FETCH_SIZE is doubled (the
 gfx950 calibration for wide coalesced reads).
 
 usage: python tools/pmc_verify.py <root> <n> <out.json> [kernel ...]
@@ -49,7 +50,11 @@ def per_dispatch(root, sub, kernels):
 def main():
     root, n, dst = sys.argv[1], int(sys.argv[2]), sys.argv[3]
     kernels = sys.argv[4:] or ["k_pre_halve", "k_verify_main"]
+    sys.path.insert(0, ROOT)
+    import bench
+
     res = {"n": n, "kernels": {}, "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
+           "kernel_src_sha256": bench.verify_kernel_src_sha256(),
            "command": "rocprofv3 --pmc <set> -- python3 bench.py --no-cpu-baseline --no-secondary --steps 3 "
                       "--warmup 1 (one pass per counter set)",
            "note": "medians over dispatches of the C2 launch; SQ_WAVE_CYCLES in quad-cycles (x4); FETCH_SIZE "
