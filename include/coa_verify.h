@@ -50,6 +50,10 @@ int coa_init(int n_gpus);
 int coa_init_devices(const int* device_ids, int n);
 int coa_shutdown(void);
 int coa_device_count(void);
+/* HIP device id of each opened context, in the order host-pointer calls
+ * shard over them (a device opened k times appears k times).  Returns the
+ * number of contexts; copies min(count, cap) ids. */
+int coa_device_ids(int* ids_out, int cap);
 /* Self-test of device `device`'s fixed-base tables (no reference
  * counterpart): checks every entry of the wide HBM comb of B against its
  * neighbours (m*2^(Wj)*B = (m-1)*2^(Wj)*B + 2^(Wj)*B, 2^(W(j+1))*B =
@@ -289,9 +293,12 @@ int coa_ed25519_sign_many_device(int device, const uint8_t* d_seeds, const uint8
  * (when max_batch signatures are pending, when the oldest request is
  * max_delay_us old, or on flush) and replies per request through the
  * callback -- the SignatureService request/oneshot idiom of
- * crypto/src/lib.rs:222-250.  Inputs are copied at submission.  The callback
- * runs on the worker thread with status (COA_OK or a negative engine error)
- * and the request's verdict byte(s). */
+ * crypto/src/lib.rs:222-250.  Inputs are copied at submission.  A collector
+ * thread launches each window on the next of two device slots per GPU
+ * (pinned staging, own stream) without waiting for the previous window, and
+ * a completion thread answers windows in order: the callback runs there with
+ * status (COA_OK or a negative engine error) and the request's verdict
+ * byte(s). */
 typedef struct coa_queue coa_queue;
 typedef void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n);
 coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us);
@@ -312,6 +319,24 @@ int coa_queue_flush(coa_queue* q);
 /* items = verify requests; groups = vote batches + certificates. */
 int coa_queue_stats(coa_queue* q, uint64_t* launches, uint64_t* items, uint64_t* groups);
 int coa_queue_digest_count(coa_queue* q, uint64_t* digests);
+/* Queue metrics since creation.  A window is the set of requests one launch
+ * takes; windows are double-buffered (the next window is packed and its
+ * copies and kernels enqueued while the previous one runs).  wait_us_* is
+ * the time from a request's submission to the start of its callback
+ * (percentiles from a log-spaced histogram, +-9 %). */
+typedef struct {
+  uint64_t requests;      /* requests answered */
+  uint64_t windows;       /* launch windows */
+  uint64_t signatures;    /* verify requests */
+  uint64_t batches;       /* vote-batch requests */
+  uint64_t certificates;  /* certificate requests */
+  uint64_t digests;       /* digest requests */
+  uint64_t max_window;    /* most items (signatures + votes + digests) in one window */
+  uint64_t max_in_flight; /* most windows launched and not yet answered at once */
+  uint64_t max_pending;   /* most items waiting for a window at once */
+  double wait_us_mean, wait_us_p50, wait_us_p99, wait_us_max;
+} coa_queue_metrics_t;
+int coa_queue_metrics(coa_queue* q, coa_queue_metrics_t* out);
 int coa_queue_destroy(coa_queue* q);
 
 #ifdef __cplusplus

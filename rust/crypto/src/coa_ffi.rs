@@ -35,6 +35,25 @@ pub struct CoaQueue {
     _private: [u8; 0],
 }
 
+/// coa_queue_metrics_t
+#[repr(C)]
+#[derive(Default, Debug, Clone, Copy)]
+pub struct CoaQueueMetrics {
+    pub requests: u64,
+    pub windows: u64,
+    pub signatures: u64,
+    pub batches: u64,
+    pub certificates: u64,
+    pub digests: u64,
+    pub max_window: u64,
+    pub max_in_flight: u64,
+    pub max_pending: u64,
+    pub wait_us_mean: f64,
+    pub wait_us_p50: f64,
+    pub wait_us_p99: f64,
+    pub wait_us_max: f64,
+}
+
 /// void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n)
 pub type CoaVerdictCb = Option<unsafe extern "C" fn(user: *mut c_void, status: c_int, verdicts: *const u8, n: usize)>;
 
@@ -45,6 +64,7 @@ extern "C" {
     pub fn coa_init_devices(device_ids: *const c_int, n: c_int) -> c_int;
     pub fn coa_shutdown() -> c_int;
     pub fn coa_device_count() -> c_int;
+    pub fn coa_device_ids(ids_out: *mut c_int, cap: c_int) -> c_int;
     pub fn coa_self_test(device: c_int, bad_entries: *mut u64) -> c_int;
     pub fn coa_fe_rows_check_device(device: c_int, d_in: *const u8, n: usize, d_out: *mut u32,
                                     stream: *mut c_void) -> c_int;
@@ -146,6 +166,7 @@ extern "C" {
     pub fn coa_queue_flush(q: *mut CoaQueue) -> c_int;
     pub fn coa_queue_stats(q: *mut CoaQueue, launches: *mut u64, items: *mut u64, groups: *mut u64) -> c_int;
     pub fn coa_queue_digest_count(q: *mut CoaQueue, digests: *mut u64) -> c_int;
+    pub fn coa_queue_metrics(q: *mut CoaQueue, out: *mut CoaQueueMetrics) -> c_int;
     pub fn coa_queue_destroy(q: *mut CoaQueue) -> c_int;
 }
 

@@ -63,6 +63,9 @@ int main(int argc, char** argv) {
   CHECK(coa_init_devices(NULL, 0) == COA_EINVAL, "coa_init_devices(empty)");
   const int ndev = coa_device_count();
   CHECK(gpu ? ndev >= 1 : ndev == COA_ENODEVICE, "coa_device_count");
+  int idbuf[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  const int nids = coa_device_ids(idbuf, 8);
+  CHECK(gpu ? (nids == ndev && idbuf[0] >= 0) : nids == COA_ENODEVICE, "coa_device_ids");
   uint64_t bad_entries = 7;
   CHECK(coa_self_test(0, &bad_entries) == dev_rc, "coa_self_test");
   CHECK(!gpu || bad_entries == 0, "coa_self_test entries");
@@ -173,6 +176,10 @@ int main(int argc, char** argv) {
   uint64_t launches = 0, items = 0, groups = 0, digests = 0;
   CHECK(coa_queue_stats(q, &launches, &items, &groups) == COA_OK && items == 1 && groups == 2, "queue_stats");
   CHECK(coa_queue_digest_count(q, &digests) == COA_OK && digests == 1, "queue_digest_count");
+  coa_queue_metrics_t qm;
+  CHECK(coa_queue_metrics(q, &qm) == COA_OK && qm.requests == 4 && qm.signatures == 1 && qm.batches == 1 &&
+            qm.certificates == 1 && qm.digests == 1 && qm.wait_us_max >= qm.wait_us_mean,
+        "queue_metrics");
   CHECK(coa_queue_destroy(q) == COA_OK, "queue_destroy");
 
   CHECK(coa_shutdown() == COA_OK, "coa_shutdown");

@@ -1,13 +1,16 @@
 // ThreadSanitizer run of the aggregation queue (xrpl-coa-prototype_amd/csrc/
 // coa_queue.cpp) with many producer threads.  The queue's
-// engine calls are served by a deterministic stub linked in their place (no
-// GPU, no HIP): each verdict is a pure function of the request's bytes, so
-// every callback can be checked against the request it answers.
+// launch backend (coa_queue.h) is a deterministic stub linked in place of the
+// HIP one (no GPU, no HIP) with the same two-slot double buffering: each
+// verdict is a pure function of the request's bytes, so every callback can be
+// checked against the request it answers.
 //
 // Build (tests/test_sanitizers.py): g++ -fsanitize=thread coa_queue.cpp
 // queue_tsan.cpp.  usage: queue_tsan <producers> <requests per producer>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -16,11 +19,14 @@
 #include <thread>
 #include <vector>
 
+#include "coa_queue.h"
 #include "coa_verify.h"
 
-// ------------------------------------------------------------- stub engine
+// ------------------------------------------------------------ stub backend
+// Two slots like the HIP backend: launch() blocks while both are busy and
+// returns at once; complete() "runs" the window (a short sleep) and writes the
+// outputs.  Verdicts are pure functions of the request bytes.
 static std::atomic<long> g_engine_calls{0};
-static void gpu_time() { std::this_thread::sleep_for(std::chrono::microseconds(50)); }
 static uint8_t v_single(const uint8_t* msg, const uint8_t* sig) { return (uint8_t)((msg[0] ^ sig[0]) & 1u); }
 static uint8_t v_group(const uint8_t* msg, size_t nvotes) { return (uint8_t)((msg[1] + nvotes) & 1u); }
 static uint8_t v_cert(const uint8_t* id, size_t nvotes) { return (uint8_t)((id[2] + nvotes) & 7u); }
@@ -28,52 +34,45 @@ static uint8_t v_digest(const uint8_t* data, size_t len, int j) {
   return (uint8_t)((len ? data[0] : 0xa5) + 7 * j + (uint8_t)len);
 }
 
-extern "C" {
-int coa_ed25519_verify_strict_many(const uint8_t* msgs, size_t msg_len, const uint8_t* pks, const uint8_t* sigs,
-                                   size_t n, uint8_t* verdicts_out) {
-  (void)pks;
-  g_engine_calls++;
-  gpu_time();
-  for (size_t i = 0; i < n; i++) verdicts_out[i] = v_single(msgs + i * msg_len, sigs + i * 64);
-  return COA_OK;
-}
-int coa_ed25519_verify_batch_groups(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs,
-                                    const uint64_t* group_offsets, size_t n_groups, uint8_t* group_verdicts_out,
-                                    uint64_t rng_seed) {
-  (void)pks;
-  (void)sigs;
-  (void)rng_seed;
-  g_engine_calls++;
-  gpu_time();
-  for (size_t g = 0; g < n_groups; g++)
-    group_verdicts_out[g] = v_group(msgs + g * 32, group_offsets[g + 1] - group_offsets[g]);
-  return COA_OK;
-}
-int coa_certificate_verify_many(const uint8_t* header_data, const uint64_t* header_offsets, const uint8_t* ids,
-                                const uint8_t* origins, const uint8_t* header_sigs, const uint64_t* rounds,
-                                const uint8_t* vote_pks, const uint8_t* vote_sigs, const uint64_t* vote_offsets,
-                                size_t n, uint64_t rng_seed, uint8_t* status_out) {
-  (void)header_data;
-  (void)header_offsets;
-  (void)origins;
-  (void)header_sigs;
-  (void)rounds;
-  (void)vote_pks;
-  (void)vote_sigs;
-  (void)rng_seed;
-  g_engine_calls++;
-  gpu_time();
-  for (size_t c = 0; c < n; c++) status_out[c] = v_cert(ids + c * 32, vote_offsets[c + 1] - vote_offsets[c]);
-  return COA_OK;
-}
-int coa_sha512_trunc32_many(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out32) {
-  g_engine_calls++;
-  gpu_time();
-  for (size_t i = 0; i < n; i++)
-    for (int j = 0; j < 32; j++) out32[i * 32 + j] = v_digest(data + offsets[i], offsets[i + 1] - offsets[i], j);
-  return COA_OK;
-}
-}
+namespace {
+class StubBackend : public coa_q::Backend {
+ public:
+  int slots() const override { return 2; }
+  void launch(coa_q::Window& w) override {
+    std::unique_lock<std::mutex> l(m_);
+    const int k = (int)(next_++ % 2);
+    cv_.wait(l, [&] { return !busy_[k]; });
+    busy_[k] = true;
+    w.slot = k;
+    w.v_out.assign(w.nv, 1);
+    w.g_out.assign(w.ng, 1);
+    w.c_out.assign(w.nc, 7);
+    w.d_out.assign(w.nd * 32, 0);
+  }
+  void complete(coa_q::Window& w) override {
+    g_engine_calls++;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+    for (size_t i = 0; i < w.nv; i++) w.v_out[i] = v_single(&w.v_msgs[i * 32], &w.v_sigs[i * 64]);
+    for (size_t g = 0; g < w.ng; g++) w.g_out[g] = v_group(&w.g_msgs[g * 32], w.g_offs[g + 1] - w.g_offs[g]);
+    for (size_t c = 0; c < w.nc; c++) w.c_out[c] = v_cert(&w.c_ids[c * 32], w.c_voff[c + 1] - w.c_voff[c]);
+    for (size_t i = 0; i < w.nd; i++)
+      for (int j = 0; j < 32; j++)
+        w.d_out[i * 32 + j] = v_digest(w.d_data.data() + w.d_offs[i], w.d_offs[i + 1] - w.d_offs[i], j);
+    w.rc = COA_OK;
+    std::lock_guard<std::mutex> l(m_);
+    busy_[w.slot] = false;
+    cv_.notify_all();
+  }
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  bool busy_[2] = {false, false};
+  unsigned long next_ = 0;
+};
+}  // namespace
+
+coa_q::Backend* coa_q::make_backend() { return new StubBackend(); }
 
 // -------------------------------------------------------------- producers
 struct Req {
@@ -144,6 +143,8 @@ int main(int argc, char** argv) {
           uint64_t l, it, g, d;
           coa_queue_stats(q, &l, &it, &g);
           coa_queue_digest_count(q, &d);
+          coa_queue_metrics_t mm;
+          coa_queue_metrics(q, &mm);
         }
       }
     });
@@ -159,9 +160,15 @@ int main(int argc, char** argv) {
   uint64_t launches = 0, items = 0, groups = 0, digests = 0;
   coa_queue_stats(q, &launches, &items, &groups);
   coa_queue_digest_count(q, &digests);
+  coa_queue_metrics_t m;
+  coa_queue_metrics(q, &m);
   coa_queue_destroy(q);
   const long total = (long)producers * per;
-  std::printf("queue tsan: %ld/%ld answered, %ld wrong, %llu launches, %ld engine calls\n", done, total, bad,
-              (unsigned long long)launches, g_engine_calls.load());
-  return (done == total && bad == 0 && items + groups + digests == (uint64_t)total) ? 0 : 1;
+  std::printf("queue tsan: %ld/%ld answered, %ld wrong, %llu launches, %ld windows completed, max in flight %llu, "
+              "wait p50 %.0f us p99 %.0f us\n",
+              done, total, bad, (unsigned long long)launches, g_engine_calls.load(),
+              (unsigned long long)m.max_in_flight, m.wait_us_p50, m.wait_us_p99);
+  const bool metrics_ok = m.requests == (uint64_t)total && m.signatures + m.batches + m.certificates + m.digests ==
+                                                               (uint64_t)total && m.windows == launches;
+  return (done == total && bad == 0 && items + groups + digests == (uint64_t)total && metrics_ok) ? 0 : 1;
 }

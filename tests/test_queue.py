@@ -116,3 +116,73 @@ def test_queue_certificates_and_digests_gpu(engine):
         assert [bytes(f.result(timeout=60)) for f in df] == [hashlib.sha512(b).digest()[:32] for b in blobs]
         st = q.stats()
         assert st["batches"] == len(batch) and st["digests"] == len(blobs) and st["launches"] <= 2
+
+
+@pytest.mark.gpu
+def test_queue_pipelined_windows_gpu(engine):
+    """Many small windows in a row (max_batch 256) from four producers mixing
+    every kind: windows overlap on the two device slots (max_in_flight 2),
+    every answer equals its expectation -- valid/corrupted signatures,
+    certificates including ones that need the exact host re-decision (a vote
+    key outside the registered committee, a corrupted vote), digests -- and
+    the metrics account for every request."""
+    import hashlib
+    import struct
+
+    import certificates as C
+    import workloads
+
+    n = 3000
+    seeds, msgs = workloads.key_seeds(n, 40_000), workloads.messages(n, 40_000)
+    pks, sigs = engine.sign_many(seeds, msgs)
+    bad = np.zeros(n, bool)
+    bad[::10] = True
+    sigs[bad, 40] ^= 1
+    committee, batch = C.synth_certificates(24, committee_size=10, n_payload=2, seed=5)
+    committee.register()
+    # certificate 4: one vote by a key outside the committee, validly signed (uncached -> host path, Ok)
+    lo = int(batch.offsets[4])
+    p_out, s_out = engine.sign_many(workloads.key_seeds(1, 99_999), batch.cert_digests[4:5])
+    batch.vote_pks[lo], batch.vote_sigs[lo] = p_out[0], s_out[0]
+    batch.vote_sigs[int(batch.offsets[9]) + 1, 50] ^= 1  # certificate 9: bad vote
+    want_cert = [0] * len(batch)
+    want_cert[9] = engine.CERT_BAD_VOTES
+    blobs = [struct.pack("<Q", i) * (1 + i % 50) for i in range(300)]
+    results = []
+    lock = threading.Lock()
+    with engine.AggregationQueue(max_batch=256, max_delay_us=300) as q:
+        def producer(t):
+            out = []
+            for i in range(t, n, 4):
+                sg = engine.Signature.from_bytes(bytes(sigs[i]))
+                out.append(("sig", q.submit_verify(bytes(msgs[i]), bytes(pks[i]), sg), not bad[i]))
+                if i % 100 == t and i // 100 < len(batch):
+                    c = i // 100
+                    lo_, hi_ = int(batch.offsets[c]), int(batch.offsets[c + 1])
+                    votes = [(engine.PublicKey(bytes(batch.vote_pks[j])),
+                              engine.Signature.from_bytes(bytes(batch.vote_sigs[j]))) for j in range(lo_, hi_)]
+                    out.append(("cert", q.submit_certificate(batch.header_inputs[c], bytes(batch.ids[c]),
+                                                             bytes(batch.authors[c]), bytes(batch.header_sigs[c]),
+                                                             batch.round, votes), want_cert[c]))
+                if i % 10 == t and i // 10 < len(blobs):
+                    b = blobs[i // 10]
+                    out.append(("dig", q.submit_digest(b), hashlib.sha512(b).digest()[:32]))
+            with lock:
+                results.extend(out)
+
+        th = [threading.Thread(target=producer, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        q.flush()
+        for kind, f, exp in results:
+            got = f.result(timeout=120)
+            if kind == "dig":
+                assert bytes(got) == exp
+            else:
+                assert got == exp, (kind, got, exp)
+        m = q.metrics()
+    assert m["requests"] == len(results) and m["signatures"] == n
+    assert m["windows"] > 4 and m["max_in_flight"] == 2
+    assert 0 < m["wait_us_p50"] <= m["wait_us_p99"] <= m["wait_us_max"] * 1.1

@@ -9,8 +9,9 @@
 * coa_queue.cpp -- the multi-producer aggregation queue -- built with
   ThreadSanitizer (clang's runtime: GCC 11's libtsan does not intercept
   pthread_cond_clockwait and reports false double locks) and, separately,
-  ASan + UBSan, against a deterministic stub engine, with 16 producer threads
-  submitting every request kind while others flush and read the stats.
+  ASan + UBSan, with a deterministic stub in place of its HIP launch backend
+  (same two-slot double buffering), with 16 producer threads submitting
+  every request kind while they also flush and read the stats and metrics.
 No device code is involved (GPU sanitizers are not available on the pool)."""
 import os
 import subprocess
@@ -26,7 +27,7 @@ CLANG = "/opt/rocm/lib/llvm/bin/clang++"
 
 def _build(out, srcs, flags, cxx="g++"):
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [cxx, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-I", INC] + flags + srcs + ["-o", out,
+    cmd = [cxx, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-I", INC, "-I", CSRC] + flags + srcs + ["-o", out,
                                                                                                    "-pthread"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]

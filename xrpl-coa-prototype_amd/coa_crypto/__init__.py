@@ -48,6 +48,15 @@ class EngineError(RuntimeError):
 
 
 _lib = None
+
+
+class QueueMetrics(ctypes.Structure):
+    """coa_queue_metrics_t (include/coa_verify.h)."""
+    _fields_ = [(n, ctypes.c_uint64) for n in ("requests", "windows", "signatures", "batches", "certificates",
+                                               "digests", "max_window", "max_in_flight", "max_pending")] + \
+               [(n, ctypes.c_double) for n in ("wait_us_mean", "wait_us_p50", "wait_us_p99", "wait_us_max")]
+
+
 # void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n)
 VERDICT_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t)
 
@@ -76,6 +85,7 @@ def lib():
         "coa_init_devices": ([ctypes.POINTER(ctypes.c_int), ctypes.c_int], ctypes.c_int),
         "coa_shutdown": ([], ctypes.c_int),
         "coa_device_count": ([], ctypes.c_int),
+        "coa_device_ids": ([ctypes.POINTER(ctypes.c_int), ctypes.c_int], ctypes.c_int),
         "coa_self_test": ([ctypes.c_int, P64], ctypes.c_int),
         "coa_fe_rows_check_device": ([ctypes.c_int, vp, sz, vp, vp], ctypes.c_int),
         "coa_last_error": ([], ctypes.c_char_p),
@@ -121,6 +131,7 @@ def lib():
         "coa_queue_digest_count": ([vp, P64], ctypes.c_int),
         "coa_queue_flush": ([vp], ctypes.c_int),
         "coa_queue_stats": ([vp, P64, P64, P64], ctypes.c_int),
+        "coa_queue_metrics": ([vp, ctypes.POINTER(QueueMetrics)], ctypes.c_int),
         "coa_queue_destroy": ([vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
@@ -281,6 +292,14 @@ def init_devices(ids):
 
 def device_count():
     return _check(lib().coa_device_count())
+
+
+def device_ids():
+    """HIP device id of every opened context, in shard order."""
+    n = _check(lib().coa_device_ids(None, 0))
+    arr = (ctypes.c_int * max(n, 1))()
+    _check(lib().coa_device_ids(arr, n))
+    return list(arr[:n])
 
 
 def shutdown():
@@ -725,6 +744,14 @@ class AggregationQueue:
         _check(lib().coa_queue_stats(self._q, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         _check(lib().coa_queue_digest_count(self._q, ctypes.byref(d)))
         return {"launches": a.value, "signatures": b.value, "batches": c.value, "digests": d.value}
+
+    def metrics(self):
+        """coa_queue_metrics: request counts per kind, window sizes, windows in
+        flight (double buffering), pending depth and submit -> callback wait
+        times in microseconds."""
+        m = QueueMetrics()
+        _check(lib().coa_queue_metrics(self._q, ctypes.byref(m)))
+        return {name: getattr(m, name) for name, _ in QueueMetrics._fields_}
 
     def close(self):
         if self._q:

@@ -922,6 +922,14 @@ int coa_device_count(void) {
   return (int)g_devs.size();
 }
 
+int coa_device_ids(int* ids_out, int cap) {
+  const int r = ensure_init();
+  if (r != COA_OK) return r;
+  if (cap > 0 && !ids_out) return fail(COA_EINVAL, "null argument");
+  for (int i = 0; i < (int)g_devs.size() && i < cap; i++) ids_out[i] = g_devs[i]->id;
+  return (int)g_devs.size();
+}
+
 int coa_self_test(int device, uint64_t* bad_entries) {
   if (!bad_entries) return fail(COA_EINVAL, "null output");
   *bad_entries = 0;
