@@ -599,7 +599,7 @@ def verify_kernel_src_sha256():
     sys.path.insert(0, PKG)
     import build as engine_build
 
-    h = hashlib.sha256(" ".join(engine_build.COMMON).encode())
+    h = hashlib.sha256(" ".join(f for f in engine_build.COMMON if not f.startswith("-I")).encode())
     for name in VERIFY_KERNEL_SOURCES:
         with open(os.path.join(PKG, "csrc", name), "rb") as f:
             h.update(name.encode() + b"\0" + f.read())
@@ -760,6 +760,10 @@ def main():
         insts = pmc["valu_insts_per_call"]
         roof["issue_frac"] = round(insts * VALU_ISSUE_CYCLES / (SIMDS * CLOCK_HZ * verify_ms * 1e-3), 4)
         roof["valu_insts_per_verify"] = round(insts / n, 1)
+        if pmc.get("valu_active_share") is not None:
+            # SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES over the call's waves: how
+            # much of its lifetime a wave spends issuing VALU instructions
+            roof["valu_active_share"] = round(pmc["valu_active_share"], 4)
         roof["traffic"] = pmc.get("hbm_bytes_per_launch")
         roof["counters"] = (f"{pmc['_path']}: rocprofv3 --pmc SQ_INSTS_VALU (issue_frac = VALU wave-instructions "
                             f"per call x {VALU_ISSUE_CYCLES} cycles / ({SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz x "

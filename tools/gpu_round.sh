@@ -48,7 +48,7 @@ if [[ $STEPS == *fullprof* ]]; then
 fi
 if [[ $STEPS == *verifypmc* ]]; then
   # three counter passes of the C2 verify call -> profiles JSON tied to this build
-  run "pmc SQ" && timeout -k 10 -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY -T -d gpurun_out/vp/pmc_SQ -o run --output-format csv \
+  run "pmc SQ" && timeout -k 10 -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -T -d gpurun_out/vp/pmc_SQ -o run --output-format csv \
       -- python3 bench.py --no-cpu-baseline --no-secondary --steps 3 --warmup 1 > gpurun_out/vp_sq.json 2> gpurun_out/vp_sq.err \
     || { tail -30 gpurun_out/vp_sq.err; exit 1; }
   for c in FETCH_SIZE WRITE_SIZE; do

@@ -73,10 +73,13 @@ def main():
         med = lambda c: statistics.median(sq[k][d].get(c, 0.0) for d in ds)  # noqa: E731
         kv = {"grid": g, "dispatches": len(ds), "waves": med("SQ_WAVES"), "valu_insts": med("SQ_INSTS_VALU"),
               "salu_insts": med("SQ_INSTS_SALU"), "wave_cycles": 4 * med("SQ_WAVE_CYCLES"),
-              "busy_cycles": med("SQ_BUSY_CYCLES"), "wait_inst_any": med("SQ_WAIT_INST_ANY")}
+              "busy_cycles": med("SQ_BUSY_CYCLES"), "wait_inst_any": med("SQ_WAIT_INST_ANY"),
+              "active_inst_valu": med("SQ_ACTIVE_INST_VALU")}
         kv["valu_insts_per_wave"] = kv["valu_insts"] / max(kv["waves"], 1.0)
         kv["cycles_per_valu_inst"] = kv["wave_cycles"] / max(kv["valu_insts"], 1.0)
         kv["valu_issue_share"] = 2 * kv["valu_insts"] / max(kv["wave_cycles"], 1.0)
+        # fraction of the waves' lifetime spent issuing VALU (both counters in quad-cycles)
+        kv["valu_active_share"] = kv["active_inst_valu"] * 4 / max(kv["wave_cycles"], 1.0)
         f = [v["FETCH_SIZE"] for v in fe.get(k, {}).values()]
         w = [v["WRITE_SIZE"] for v in wr.get(k, {}).values()]
         if f and w:
@@ -87,6 +90,9 @@ def main():
         valu += kv["valu_insts"]
         res["kernels"][k] = kv
     res["valu_insts_per_call"] = valu
+    tot_cyc = sum(v["wave_cycles"] for v in res["kernels"].values())
+    res["valu_active_share"] = (sum(v["active_inst_valu"] * 4 for v in res["kernels"].values()) / tot_cyc
+                                if tot_cyc else None)
     res["hbm_bytes_per_launch"] = fetch + write if fetch else None
     res["alg_bytes_per_launch"] = n * (32 + 32 + 64 + 1)
     os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
