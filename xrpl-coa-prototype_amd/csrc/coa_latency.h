@@ -6,10 +6,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Signatures of a call passed inline in the kernel arguments (no H2D copy).
+#define COA_LAT_INLINE 16
+
 struct LatArgs {
-  const uint32_t* in;      // [n][32] dwords: msg (8) | pk (8) | R (8) | s (8)
+  const uint32_t* in;      // [n][32] dwords: msg (8) | pk (8) | R (8) | s (8), items >= n_inline
   uint32_t n;
-  uint8_t* verdicts;       // [n] 0 Ok / 1 Err
+  uint32_t n_inline;       // items [0, n_inline) are in inl
+  uint32_t inl[COA_LAT_INLINE][32];
+  uint32_t* res;           // [n] result words in page-locked host memory: (tag << 8) | verdict
+  uint32_t tag;            // nonzero, per call: the host polls res for it
   const uint32_t* keys;    // registered committee keys (sorted), or null
   const uint32_t* kflags;  // [nk]
   const uint32_t* ktabs;   // [nk] radix-256 combs of -A (coa_committee.h)

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -169,7 +170,10 @@ struct Dev {
   // committee key cache (f2): sorted keys, flags, one comb of -A per key
   DevBuf ckeys, kflags, ktabs, kwtabs, cert, cscr;
   DevBuf msm;  // Pippenger workspace (one large verify_batch group)
-  DevBuf lat;  // single-signature latency path: inputs + verdicts
+  DevBuf lat;  // single-signature latency path: inputs beyond the inline ones
+  uint32_t* lat_res = nullptr;  // page-locked result words the latency kernel writes
+  size_t lat_res_cap = 0;
+  uint32_t lat_tag = 0;
   bool kwide = false;  // kwtabs holds the committee's wide combs
   uint32_t nkeys = 0;
   PinBuf pin;
@@ -386,33 +390,72 @@ size_t lat_max() {
 }
 
 // n <= lat_max() triples with 32-byte messages through k_verify_lat on device
-// d (its lock held, device set): one pinned staging buffer, one H2D, one
-// launch, one D2H.
+// d (its lock held, device set).  Up to COA_LAT_INLINE signatures travel in
+// the kernel arguments (no H2D copy); the kernel writes tagged verdict words
+// into page-locked host memory and this thread polls for the tag (no D2H copy,
+// no stream synchronisation on the latency path).
 int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, size_t n, uint8_t* out) {
-  const size_t in_bytes = n * 128, vofs = align_up(in_bytes, 256);
-  HIP_TRY(d.pin.ensure(vofs + n));
-  HIP_TRY(d.lat.ensure(vofs + n));
-  uint8_t* h = static_cast<uint8_t*>(d.pin.p);
-  for (size_t i = 0; i < n; i++) {
-    std::memcpy(h + i * 128, msgs + i * 32, 32);
-    std::memcpy(h + i * 128 + 32, pks + i * 32, 32);
-    std::memcpy(h + i * 128 + 64, sigs + i * 64, 64);
+  if (n > d.lat_res_cap) {
+    if (d.lat_res) (void)hipHostFree(d.lat_res);
+    d.lat_res = nullptr;
+    d.lat_res_cap = 0;
+    const size_t cap = std::max<size_t>(n, 64);
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.lat_res), cap * 4, hipHostMallocCoherent));
+    std::memset(d.lat_res, 0, cap * 4);
+    d.lat_res_cap = cap;
   }
-  hipStream_t s = d.stream;
-  HIP_TRY(hipMemcpyAsync(d.lat.p, h, in_bytes, hipMemcpyHostToDevice, s));
   LatArgs a;
-  a.in = d.lat.as<uint32_t>();
+  std::memset(&a, 0, sizeof(a));
+  hipStream_t s = d.stream;
   a.n = (uint32_t)n;
-  a.verdicts = d.lat.as<uint8_t>() + vofs;
+  a.n_inline = (uint32_t)std::min<size_t>(n, COA_LAT_INLINE);
+  for (size_t i = 0; i < a.n_inline; i++) {
+    std::memcpy(&a.inl[i][0], msgs + i * 32, 32);
+    std::memcpy(&a.inl[i][8], pks + i * 32, 32);
+    std::memcpy(&a.inl[i][16], sigs + i * 64, 64);
+  }
+  if (n > COA_LAT_INLINE) {  // the rest through one pinned staging buffer and one H2D
+    const size_t in_bytes = n * 128;
+    HIP_TRY(d.pin.ensure(in_bytes));
+    HIP_TRY(d.lat.ensure(in_bytes));
+    uint8_t* h = static_cast<uint8_t*>(d.pin.p);
+    for (size_t i = COA_LAT_INLINE; i < n; i++) {
+      std::memcpy(h + i * 128, msgs + i * 32, 32);
+      std::memcpy(h + i * 128 + 32, pks + i * 32, 32);
+      std::memcpy(h + i * 128 + 64, sigs + i * 64, 64);
+    }
+    HIP_TRY(hipMemcpyAsync(d.lat.as<uint8_t>() + COA_LAT_INLINE * 128, h + COA_LAT_INLINE * 128,
+                           in_bytes - COA_LAT_INLINE * 128, hipMemcpyHostToDevice, s));
+    a.in = d.lat.as<uint32_t>();
+  }
+  d.lat_tag = (d.lat_tag + 1) & 0xffffffu;
+  if (d.lat_tag == 0) d.lat_tag = 1;
+  a.tag = d.lat_tag;
+  a.res = d.lat_res;
   a.keys = d.ckeys.as<uint32_t>();
   a.kflags = d.kflags.as<uint32_t>();
   a.ktabs = d.ktabs.as<uint32_t>();
   a.nk = d.nkeys;
   a.comb = d.comb;
   HIP_TRY(coa_launch_verify_lat(a, s));
-  HIP_TRY(hipMemcpyAsync(h + vofs, a.verdicts, n, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  std::memcpy(out, h + vofs, n);
+  // poll the tagged words; a kernel that never publishes (a fault) ends the
+  // wait through the stream's error after a bound
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t i = 0; i < n; i++) {
+    const volatile uint32_t* w = d.lat_res + i;
+    for (uint64_t spin = 0; (*w >> 8) != a.tag; spin++) {
+      if ((spin & 1023) == 1023) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q != hipSuccess && q != hipErrorNotReady)
+          return fail(COA_EHIP, std::string("latency kernel: ") + hipGetErrorString(q));
+        if (q == hipSuccess && (*w >> 8) != a.tag)
+          return fail(COA_EHIP, "latency kernel finished without publishing a verdict");
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+          return fail(COA_EHIP, "latency kernel timed out");
+      }
+    }
+    out[i] = (uint8_t)(*w & 0xffu);
+  }
   return COA_OK;
 }
 
@@ -905,6 +948,9 @@ int coa_shutdown(void) {
     (void)hipStreamSynchronize(d->stream);
     for (DevBuf* b : d->all()) b->release();
     d->pin.release();
+    if (d->lat_res) (void)hipHostFree(d->lat_res);
+    d->lat_res = nullptr;
+    d->lat_res_cap = 0;
     d->nkeys = 0;
     if (d->btab) (void)hipFree(d->btab);
     if (d->comb) (void)hipFree(d->comb);
