@@ -50,6 +50,12 @@ struct CertArgs {
   const uint32_t* comb;         // B comb (coa_halved.h)
   const uint32_t* wcomb;        // wide B comb (coa_smul.h) or null
   uint32_t* status;             // [nc], zeroed by the caller
+  // latency variant only (optional): the last block publishes (tag << 8) |
+  // status into host_res[c] (page-locked) and re-zeroes status and done_ctr
+  uint32_t* host_res = nullptr;
+  uint32_t* done_ctr = nullptr;  // device word, 0 between calls
+  uint32_t tag = 0;
+  uint32_t total_blocks = 0;     // set by the launcher
 };
 
 hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s);

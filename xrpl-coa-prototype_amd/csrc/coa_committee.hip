@@ -436,6 +436,23 @@ extern "C" int coa_lat_trace(unsigned long long* out) {
 #else
 #define LAT_MARK(w, i)
 #endif
+// With a.host_res set, the block that finishes last publishes every
+// certificate's status word into page-locked host memory, tagged with the
+// call (the host polls for the tag: no device-to-host copy, no stream
+// synchronisation), resets the status words and the block counter for the
+// next call.  Called by one thread per block after that block's status write.
+COA_DEV void lat_block_done(const CertArgs& a) {
+  if (!a.host_res) return;
+  __threadfence();
+  const uint32_t old = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1 != a.total_blocks) return;
+  __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t c = 0; c < a.nc; c++) {
+    const uint32_t st = __hip_atomic_exchange(a.status + c, 0u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.host_res + c, (a.tag << 8) | (st & 0xffu), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
   const uint32_t wave = coa_sha::uni(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
@@ -470,10 +487,14 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
 #pragma unroll
     for (int i = 0; i < 8; i++) same = same && h[i] == id[i];
     if (lane == 0 && !same) atomicOr(a.status + c, COA_CST_BAD_HEADER_ID);
+    if (lane == 0) lat_block_done(a);
     return;
   }
   __shared__ uint32_t r_lds[17];  // R.X, R.Y, decompress ok
   __shared__ uint32_t s_lds[32];  // [s]B from wave 2
+  __shared__ uint32_t s_ready;    // wave 2 published s_lds
+  if (threadIdx.x == 0) s_ready = 0;
+  __syncthreads();
   const uint32_t job = blockIdx.x - a.nc;
   const bool hdr = job < a.nc;
   const uint32_t vi = job - a.nc;
@@ -582,31 +603,44 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
         for (int q4 = 0; q4 < 4; q4++)
 #pragma unroll
           for (int i = 0; i < 8; i++) s_lds[q4 * 8 + i] = f[q4]->v[i];
+        __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       bits = pre << 8;  // pre-verdict flags, resolved after the hand-off
     }
+  }
+  // wave 0 finishes everything that needs only P while wave 1 is still
+  // decompressing R (the critical chain): P = [s]B + [k](-A) as soon as wave 2
+  // has published [s]B, verify_strict's small-order test, the projective form
+  ge_p2 P2;
+  if (wave == 0 && !(bits & COA_CST_UNCACHED)) {
+    uint32_t pre = bits >> 8;
+#pragma unroll 1
+    while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+      __builtin_amdgcn_s_sleep(1);
+    {  // P = [s]B + [k](-A)
+      ge_p3 S;
+      fe* f[4] = {&S.X, &S.Y, &S.Z, &S.T};
+#pragma unroll
+      for (int q4 = 0; q4 < 4; q4++)
+#pragma unroll
+        for (int i = 0; i < 8; i++) f[q4]->v[i] = s_lds[q4 * 8 + i];
+      ge_cached sc4;
+      ge_p3_to_cached(sc4, S);
+      ge_p1p1 t;
+      ge_add(t, P, sc4);
+      ge_p1p1_to_p3(P, t);
+    }
+    // verify_strict's small-order test of R, taken on P: an accepting
+    // verdict needs R == P, and every other verdict is Err already
+    if (hdr && ge_is_small_order(P)) pre |= 16u;
+    ge_p3_to_p2(P2, P);
+    bits = pre << 8;
   }
   __syncthreads();
   LAT_MARK(wave, 4)
   if (wave == 0) {
     if (!(bits & COA_CST_UNCACHED)) {
-      uint32_t pre = bits >> 8;
-      {  // P = [s]B + [k](-A)
-        ge_p3 S;
-        fe* f[4] = {&S.X, &S.Y, &S.Z, &S.T};
-#pragma unroll
-        for (int q4 = 0; q4 < 4; q4++)
-#pragma unroll
-          for (int i = 0; i < 8; i++) f[q4]->v[i] = s_lds[q4 * 8 + i];
-        ge_cached sc4;
-        ge_p3_to_cached(sc4, S);
-        ge_p1p1 t;
-        ge_add(t, P, sc4);
-        ge_p1p1_to_p3(P, t);
-      }
-      // verify_strict's small-order test of R, taken on P: an accepting
-      // verdict needs R == P, and every other verdict is Err already
-      if (hdr && ge_is_small_order(P)) pre |= 16u;
+      const uint32_t pre = bits >> 8;
       ge_p3 R;
 #pragma unroll
       for (int i = 0; i < 8; i++) {
@@ -615,8 +649,6 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
       }
       fe_set(R.Z, 1);
       const bool r_ok = r_lds[16] != 0, small_r = (pre & 16) != 0;
-      ge_p2 P2;
-      ge_p3_to_p2(P2, P);
       const bool eq = ge_p2_eq_p3(P2, R);
       const bool s_ok = !(pre & 1), a_ok = !(pre & 2), small_a = (pre & 4) != 0, tfree = !(pre & 8);
       if (hdr) {
@@ -629,6 +661,7 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
     }
     LAT_MARK(0, 5)
     if (lane == 0 && bits) atomicOr(a.status + c, bits);
+    if (lane == 0) lat_block_done(a);
   }
 }
 
@@ -705,6 +738,7 @@ hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr,
   a.hdr_blocks = (a.nc + 255) / 256;
   const uint64_t jobs = (uint64_t)a.nc + a.nv;
   if (lanes_per_sig == 64) {  // one workgroup per header digest and per signature
+    a.total_blocks = (uint32_t)(a.nc + jobs);
     hipLaunchKernelGGL(k_cert_verify_lat, dim3((uint32_t)(a.nc + jobs)), dim3(192), 0, s, a);
     return hipGetLastError();
   }

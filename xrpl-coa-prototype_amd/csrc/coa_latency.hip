@@ -210,7 +210,11 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
   const int slot = a.nk ? key_lookup_u(a.keys, a.nk, pk) : -1;
 
   if (slot >= 0) {  // ------------------------------------------ cached key
+    __shared__ uint32_t s_ready;  // wave 2 published [s]B
+    if (threadIdx.x == 0) s_ready = 0;
+    __syncthreads();
     ge_p3 P;
+    ge_p2 P2;
     uint32_t pre = 0;
     if (wave == 1) {
       ge_p3 R;
@@ -228,7 +232,10 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
 #pragma unroll
       for (int i = 0; i < 8; i++) dg[i] = sw[i];
       comb_butterfly(P, dg, a.comb, lane);
-      if (lane == 0) lds_put_p3(sh_pt[0], P);
+      if (lane == 0) {
+        lds_put_p3(sh_pt[0], P);
+        __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     } else if (wave == 0) {
       uint64_t st[8];
       uint32_t h[16], w[24];
@@ -246,11 +253,14 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
       pre = (sc_is_canonical(sw) ? 0u : 1u) | ((kf & COA_KEY_DECOMPRESSES) ? 0u : 2u) |
             ((kf & COA_KEY_SMALL_ORDER) ? 4u : 0u);
       comb_butterfly(P, k.v, a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS, lane);
-    }
-    VMARK(1)
-    __syncthreads();
-    VMARK(2)
-    if (wave == 0) {
+      // everything that needs only P while wave 1 still decompresses R (the
+      // critical chain): P = [s]B + [k](-A) once wave 2 has published [s]B,
+      // verify_strict's small-order test of R taken on P (an accepting
+      // verdict needs R == P, every other verdict is Err already), the
+      // projective form
+#pragma unroll 1
+      while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        __builtin_amdgcn_s_sleep(1);
       ge_p3 S;
       lds_get_p3(S, sh_pt[0]);
       ge_cached sc4;
@@ -258,9 +268,13 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
       ge_p1p1 t;
       ge_add(t, P, sc4);
       ge_p1p1_to_p3(P, t);
-      // verify_strict's small-order test of R, taken on P: an accepting
-      // verdict needs R == P, and every other verdict is Err already
-      const bool small_r = ge_is_small_order(P);
+      if (ge_is_small_order(P)) pre |= 8u;
+      ge_p3_to_p2(P2, P);
+    }
+    VMARK(1)
+    __syncthreads();
+    VMARK(2)
+    if (wave == 0) {
       ge_p3 R;
 #pragma unroll
       for (int i = 0; i < 8; i++) {
@@ -268,9 +282,7 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
         R.Y.v[i] = sh_r[8 + i];
       }
       fe_set(R.Z, 1);
-      ge_p2 P2;
-      ge_p3_to_p2(P2, P);
-      const bool ok = pre == 0 && sh_r[16] != 0 && !small_r && ge_p2_eq_p3(P2, R);
+      const bool ok = pre == 0 && sh_r[16] != 0 && ge_p2_eq_p3(P2, R);
       if (lane == 0) publish(a, item, ok);
       VMARK(3)
     }

@@ -171,9 +171,10 @@ struct Dev {
   DevBuf ckeys, kflags, ktabs, kwtabs, cert, cscr;
   DevBuf msm;  // Pippenger workspace (one large verify_batch group)
   DevBuf lat;  // single-signature latency path: inputs beyond the inline ones
-  uint32_t* lat_res = nullptr;  // page-locked result words the latency kernel writes
+  uint32_t* lat_res = nullptr;  // page-locked result words the latency kernels write
   size_t lat_res_cap = 0;
   uint32_t lat_tag = 0;
+  uint32_t* lat_ctr = nullptr;  // device block counter of k_cert_verify_lat (0 between calls)
   bool kwide = false;  // kwtabs holds the committee's wide combs
   uint32_t nkeys = 0;
   PinBuf pin;
@@ -394,7 +395,9 @@ size_t lat_max() {
 // the kernel arguments (no H2D copy); the kernel writes tagged verdict words
 // into page-locked host memory and this thread polls for the tag (no D2H copy,
 // no stream synchronisation on the latency path).
-int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, size_t n, uint8_t* out) {
+// Page-locked result words for n items and the call's tag (device d, its
+// lock held).
+int lat_res_prepare(Dev& d, size_t n, uint32_t& tag) {
   if (n > d.lat_res_cap) {
     if (d.lat_res) (void)hipHostFree(d.lat_res);
     d.lat_res = nullptr;
@@ -404,6 +407,40 @@ int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* s
     std::memset(d.lat_res, 0, cap * 4);
     d.lat_res_cap = cap;
   }
+  d.lat_tag = (d.lat_tag + 1) & 0xffffffu;
+  if (d.lat_tag == 0) d.lat_tag = 1;
+  tag = d.lat_tag;
+  return COA_OK;
+}
+
+// Waits until the n result words carry `tag` (written by the kernel just
+// launched on s); the low byte of each goes to out[i] (out may be null).  A
+// kernel that ends without publishing (a fault) ends the wait through the
+// stream's status; a bound stops a hang.
+int lat_res_wait(Dev& d, hipStream_t s, size_t n, uint32_t tag, uint32_t* out) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t i = 0; i < n; i++) {
+    const volatile uint32_t* w = d.lat_res + i;
+    for (uint64_t spin = 0; (*w >> 8) != tag; spin++) {
+      if ((spin & 1023) == 1023) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q != hipSuccess && q != hipErrorNotReady)
+          return fail(COA_EHIP, std::string("latency kernel: ") + hipGetErrorString(q));
+        if (q == hipSuccess && (*w >> 8) != tag)
+          return fail(COA_EHIP, "latency kernel finished without publishing a result");
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+          return fail(COA_EHIP, "latency kernel timed out");
+      }
+    }
+    if (out) out[i] = *w & 0xffu;
+  }
+  return COA_OK;
+}
+
+int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, size_t n, uint8_t* out) {
+  uint32_t tag = 0;
+  int rc = lat_res_prepare(d, n, tag);
+  if (rc != COA_OK) return rc;
   LatArgs a;
   std::memset(&a, 0, sizeof(a));
   hipStream_t s = d.stream;
@@ -428,9 +465,7 @@ int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* s
                            in_bytes - COA_LAT_INLINE * 128, hipMemcpyHostToDevice, s));
     a.in = d.lat.as<uint32_t>();
   }
-  d.lat_tag = (d.lat_tag + 1) & 0xffffffu;
-  if (d.lat_tag == 0) d.lat_tag = 1;
-  a.tag = d.lat_tag;
+  a.tag = tag;
   a.res = d.lat_res;
   a.keys = d.ckeys.as<uint32_t>();
   a.kflags = d.kflags.as<uint32_t>();
@@ -438,24 +473,10 @@ int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* s
   a.nk = d.nkeys;
   a.comb = d.comb;
   HIP_TRY(coa_launch_verify_lat(a, s));
-  // poll the tagged words; a kernel that never publishes (a fault) ends the
-  // wait through the stream's error after a bound
-  const auto t0 = std::chrono::steady_clock::now();
-  for (size_t i = 0; i < n; i++) {
-    const volatile uint32_t* w = d.lat_res + i;
-    for (uint64_t spin = 0; (*w >> 8) != a.tag; spin++) {
-      if ((spin & 1023) == 1023) {
-        const hipError_t q = hipStreamQuery(s);
-        if (q != hipSuccess && q != hipErrorNotReady)
-          return fail(COA_EHIP, std::string("latency kernel: ") + hipGetErrorString(q));
-        if (q == hipSuccess && (*w >> 8) != a.tag)
-          return fail(COA_EHIP, "latency kernel finished without publishing a verdict");
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
-          return fail(COA_EHIP, "latency kernel timed out");
-      }
-    }
-    out[i] = (uint8_t)(*w & 0xffu);
-  }
+  std::vector<uint32_t> words(n);
+  rc = lat_res_wait(d, s, n, tag, words.data());
+  if (rc != COA_OK) return rc;
+  for (size_t i = 0; i < n; i++) out[i] = (uint8_t)words[i];
   return COA_OK;
 }
 
@@ -790,7 +811,9 @@ CertArgs cert_args(Dev& d, uint8_t* base, const CertPack& p, size_t nc, size_t n
 }
 
 // Fast path for certificates [lo, hi) on one device: raw status words out.
-int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_out) {
+// publish: the latency variant writes its status words straight into
+// page-locked host memory (no D2H copy, no stream synchronisation).
+int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_out, bool publish = false) {
   const size_t nc = hi - lo;
   const uint64_t h0 = in.hdr_off[lo], hb = in.hdr_off[hi] - h0;
   const uint64_t v0 = in.voff[lo], nv = in.voff[hi] - v0;
@@ -818,6 +841,20 @@ int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_
   HIP_TRY(hipMemcpyAsync(d.cert.p, h, p.total, hipMemcpyHostToDevice, s));
   CertArgs a = cert_args(d, d.cert.as<uint8_t>(), p, nc, nv);
   const int lanes = cert_lanes(nc + nv);
+  if (lanes == 64 && publish) {  // the last block writes the status words to host memory
+    if (!d.lat_ctr) {
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.lat_ctr), 4));
+      HIP_TRY(hipMemsetAsync(d.lat_ctr, 0, 4, s));
+    }
+    uint32_t tag = 0;
+    int rc = lat_res_prepare(d, nc, tag);
+    if (rc != COA_OK) return rc;
+    a.host_res = d.lat_res;
+    a.done_ctr = d.lat_ctr;
+    a.tag = tag;
+    HIP_TRY(coa_launch_cert_verify(a, lanes, nullptr, s));
+    return lat_res_wait(d, s, nc, tag, status_out + lo);
+  }
   if (lanes == 1) HIP_TRY(d.cscr.ensure(coa_cert_scratch_bytes(nc + nv)));
   HIP_TRY(coa_launch_cert_verify(a, lanes, d.cscr.as<uint32_t>(), s));
   HIP_TRY(hipMemcpyAsync(h + p.status, d.cert.as<uint8_t>() + p.status, nc * 4, hipMemcpyDeviceToHost, s));
@@ -887,7 +924,15 @@ int certificates_impl(const CertIn& in, size_t n, uint64_t rng_seed, uint8_t* st
   if (in.voff[n] && (!in.vpks || !in.vsigs)) return fail(COA_EINVAL, "null vote arrays");
   if (check_n(n + in.voff[n]) != COA_OK) return COA_EINVAL;
   std::vector<uint32_t> st(n, 0);
-  int rc = for_shards(n, [&](Dev& d, size_t lo, size_t hi) -> int { return cert_shard(d, in, lo, hi, st.data()); });
+  int rc;
+  if (g_devs.size() == 1 && cert_lanes(n + in.voff[n]) == 64) {  // latency path: one device, no stream sync
+    Dev& d = *g_devs[0];
+    std::lock_guard<std::mutex> l(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    rc = cert_shard(d, in, 0, n, st.data(), true);
+  } else {
+    rc = for_shards(n, [&](Dev& d, size_t lo, size_t hi) -> int { return cert_shard(d, in, lo, hi, st.data()); });
+  }
   if (rc != COA_OK) return rc;
   std::vector<size_t> uncached, rlc;
   for (size_t i = 0; i < n; i++) {
@@ -951,6 +996,8 @@ int coa_shutdown(void) {
     if (d->lat_res) (void)hipHostFree(d->lat_res);
     d->lat_res = nullptr;
     d->lat_res_cap = 0;
+    if (d->lat_ctr) (void)hipFree(d->lat_ctr);
+    d->lat_ctr = nullptr;
     d->nkeys = 0;
     if (d->btab) (void)hipFree(d->btab);
     if (d->comb) (void)hipFree(d->comb);
