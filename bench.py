@@ -759,6 +759,11 @@ def main():
     if pmc:
         insts = pmc["valu_insts_per_call"]
         roof["issue_frac"] = round(insts * VALU_ISSUE_CYCLES / (SIMDS * CLOCK_HZ * verify_ms * 1e-3), 4)
+        # the same against 4 cycles per wave-instruction: the measured rate of
+        # the instruction classes the field arithmetic is made of
+        # (v_mad_u64_u32, carry pairs, 64-bit shifts/adds: 4.1-4.8 cycles even
+        # at 8 waves per SIMD, profiles/r01_ubench_mad.txt)
+        roof["issue_frac_quarter_rate"] = round(insts * 4 / (SIMDS * CLOCK_HZ * verify_ms * 1e-3), 4)
         roof["valu_insts_per_verify"] = round(insts / n, 1)
         if pmc.get("valu_active_share") is not None:
             # SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES over the call's waves: how
