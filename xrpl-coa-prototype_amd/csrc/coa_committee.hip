@@ -147,14 +147,20 @@ COA_DEV uint32_t vote_cert_u(const uint64_t* __restrict__ voff, uint32_t nc, uin
 #define PRE_UNCACHED 32u
 #define PRE_NONE 64u
 
+// p or q as a plain integer select (a ternary over two kernel-argument
+// pointers is lowered through a private two-entry array, i.e. scratch)
+COA_DEV const uint32_t* sel_ptr(bool c, const uint32_t* p, const uint32_t* q) {
+  return reinterpret_cast<const uint32_t*>(c ? reinterpret_cast<uintptr_t>(p) : reinterpret_cast<uintptr_t>(q));
+}
+
 COA_DEV void job_comb(const CertArgs& a, uint32_t job, ge_p3& P, uint32_t& pre, uint32_t& cert) {
   const bool hdr = job < a.nc;
   const uint32_t vi = job - a.nc;
   const uint32_t c = hdr ? job : vote_cert(a.voff, a.nc, vi);
   cert = c;
-  const uint32_t* sig = hdr ? a.hsigs + (uint64_t)c * 16 : a.vsigs + (uint64_t)vi * 16;
+  const uint32_t* sig = sel_ptr(hdr, a.hsigs + (uint64_t)c * 16, a.vsigs + (uint64_t)vi * 16);
   uint32_t pk[8], rw[8], sw[8], msg[8];
-  load8(pk, hdr ? a.origins + (uint64_t)c * 8 : a.vpks + (uint64_t)vi * 8);
+  load8(pk, sel_ptr(hdr, a.origins + (uint64_t)c * 8, a.vpks + (uint64_t)vi * 8));
   load8(rw, sig);
   load8(sw, sig + 8);
   load8(msg, a.ids + (uint64_t)c * 8);
@@ -243,7 +249,7 @@ COA_DEV void job_comb(const CertArgs& a, uint32_t job, ge_p3& P, uint32_t& pre, 
 COA_DEV uint32_t job_verdict(const CertArgs& a, uint32_t job, uint32_t pre, const fe& x, const fe& y) {
   if (pre & (PRE_NONE | PRE_UNCACHED)) return (pre & PRE_UNCACHED) ? COA_CST_UNCACHED : 0u;
   const bool hdr = (pre & PRE_HDR) != 0;
-  const uint32_t* sig = hdr ? a.hsigs + (uint64_t)job * 16 : a.vsigs + (uint64_t)(job - a.nc) * 16;
+  const uint32_t* sig = sel_ptr(hdr, a.hsigs + (uint64_t)job * 16, a.vsigs + (uint64_t)(job - a.nc) * 16);
   uint32_t rw[8];
   load8(rw, sig);
   fe yr, xc, yc;
@@ -499,7 +505,7 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
   const bool hdr = job < a.nc;
   const uint32_t vi = job - a.nc;
   const uint32_t c = hdr ? job : vote_cert_u(a.voff, a.nc, vi);
-  const uint32_t* sig = hdr ? a.hsigs + (uint64_t)c * 16 : a.vsigs + (uint64_t)vi * 16;
+  const uint32_t* sig = sel_ptr(hdr, a.hsigs + (uint64_t)c * 16, a.vsigs + (uint64_t)vi * 16);
   uint32_t rw[8];
   load8u(rw, sig);
   uint32_t bits = 0;
@@ -528,7 +534,7 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
       load8u(dg, sig + 8);
     } else {
       uint32_t pk[8], sw[8], msg[8];
-      load8u(pk, hdr ? a.origins + (uint64_t)c * 8 : a.vpks + (uint64_t)vi * 8);
+      load8u(pk, sel_ptr(hdr, a.origins + (uint64_t)c * 8, a.vpks + (uint64_t)vi * 8));
       load8u(sw, sig + 8);
       load8u(msg, a.ids + (uint64_t)c * 8);
       slot = key_lookup_u(a.keys, a.nk, pk);

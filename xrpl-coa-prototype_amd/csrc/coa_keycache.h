@@ -10,9 +10,11 @@
 namespace coa_kc {
 
 COA_DEV uint32_t word_sel(const uint32_t* x, int i) {
-  uint32_t w = x[0];
+  // masks, not selects: a select chain over a register array is turned back
+  // into dynamic indexing, i.e. a scratch round trip
+  uint32_t w = 0;
 #pragma unroll
-  for (int k = 1; k < 8; k++) w = i == k ? x[k] : w;
+  for (int k = 0; k < 8; k++) w |= x[k] & (0u - (uint32_t)(i == k));
   return w;
 }
 

@@ -227,67 +227,64 @@ COA_DEV void hash_segs(uint64_t st[8], const Segs& s, bool aligned) {
 
 // ------------------------------------------------------------------------
 // SHA-512 of p[0 .. len) in global memory, one lane (the worker batch and
-// header digests).  Full blocks are read as dwords when p is 4-byte aligned
-// (byte gathers otherwise); the tail block(s) carry the 0x80 terminator and
-// the 128-bit bit length.
+// header digests).  Every load is an aligned dword: a message that starts at
+// byte m of a dword is realigned with v_alignbyte, so serialized headers at
+// arbitrary offsets read 33 dwords per block instead of 128 bytes.  Dwords
+// that hold a message byte stay inside that byte's page, so the up to three
+// bytes read past the end never fault.  Block i+1's dwords are in flight
+// while block i is compressed (a lone lane hashing a long header is
+// latency-bound); the tail block(s) carry the 0x80 terminator and the
+// 128-bit bit length.
+COA_DEV uint32_t align_word(uint32_t lo, uint32_t hi, uint32_t m) {
+  return __builtin_amdgcn_alignbyte(hi, lo, m);  // ({hi, lo} >> 8m)[31:0]
+}
+
 COA_DEV void hash_mem(uint64_t st[8], const uint8_t* p, uint64_t len) {
   init(st);
-  uint64_t pos = 0;
-  if ((reinterpret_cast<uintptr_t>(p) & 3) == 0) {
-    // one block of prefetch: block i+1's loads are in flight while block i
-    // is compressed (a lone lane hashing a long header is latency-bound)
-    uint4 nxt[8];
-    if (len >= 128) {
+  const uint32_t m = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+  const uint32_t* b = reinterpret_cast<const uint32_t*>(p - m);  // dword holding p[0]
+  uint64_t pos = 0;  // bytes hashed; b + pos / 4 holds p[pos]
+  uint32_t nxt[33];
+  if (len >= 128) {
 #pragma unroll
-      for (int q = 0; q < 8; q++) nxt[q] = reinterpret_cast<const uint4*>(p)[q];
-    }
-    for (; pos + 128 <= len; pos += 128) {
-      uint64_t W[16];
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        W[2 * q] = be64(nxt[q].x, nxt[q].y);
-        W[2 * q + 1] = be64(nxt[q].z, nxt[q].w);
-      }
-      if (pos + 256 <= len) {
-#pragma unroll
-        for (int q = 0; q < 8; q++) nxt[q] = reinterpret_cast<const uint4*>(p + pos + 128)[q];
-      }
-      compress(st, W);
-    }
-  } else {
-    for (; pos + 128 <= len; pos += 128) {
-      uint64_t W[16];
-#pragma unroll
-      for (int w = 0; w < 16; w++) {
-        uint32_t lo = 0, hi = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          lo |= (uint32_t)p[pos + 8 * w + b] << (8 * b);
-          hi |= (uint32_t)p[pos + 8 * w + 4 + b] << (8 * b);
-        }
-        W[w] = be64(lo, hi);
-      }
-      compress(st, W);
-    }
+    for (int q = 0; q < 32; q++) nxt[q] = b[q];
+    nxt[32] = m ? b[32] : 0u;
   }
-  const uint32_t rem = (uint32_t)(len - pos);
+  for (; pos + 128 <= len; pos += 128) {
+    uint64_t W[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++)
+      W[w] = be64(align_word(nxt[2 * w], nxt[2 * w + 1], m), align_word(nxt[2 * w + 1], nxt[2 * w + 2], m));
+    if (pos + 256 <= len) {
+      const uint32_t* nb = b + (pos + 128) / 4;
+#pragma unroll
+      for (int q = 0; q < 32; q++) nxt[q] = nb[q];
+      nxt[32] = m ? nb[32] : 0u;
+    }
+    compress(st, W);
+  }
+  const uint32_t rem = (uint32_t)(len - pos);  // < 128 bytes left
   const uint32_t tail_blocks = rem + 17 <= 128 ? 1 : 2;
+  const uint32_t* tb0 = b + pos / 4;
   for (uint32_t tb = 0; tb < tail_blocks; tb++) {
+    uint32_t d[33];  // the dwords of this tail block that hold message bytes, else 0
+#pragma unroll
+    for (int q = 0; q < 33; q++) {
+      const uint32_t at = tb * 32 + q;
+      d[q] = 4 * at < m + rem ? tb0[at] : 0u;
+    }
     uint64_t W[16];
 #pragma unroll
     for (int w = 0; w < 16; w++) {
       uint32_t half[2];
 #pragma unroll
       for (int hh = 0; hh < 2; hh++) {
-        uint32_t x = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          const uint32_t q = tb * 128 + 8 * w + 4 * hh + b;
-          uint32_t byte = 0;
-          if (q < rem) byte = p[pos + q];
-          else if (q == rem) byte = 0x80;
-          x |= byte << (8 * b);
-        }
+        const int q = 2 * w + hh;
+        uint32_t x = align_word(d[q], d[q + 1], m);
+        // bytes at or after the end: 0, except 0x80 at offset rem
+        const int k = (int)rem - (int)(tb * 128 + 4 * q);
+        if (k <= 0) x = k == 0 ? 0x80u : 0u;
+        else if (k < 4) x = (x & ((1u << (8 * k)) - 1u)) | (0x80u << (8 * k));
         half[hh] = x;
       }
       W[w] = be64(half[0], half[1]);
