@@ -9,13 +9,16 @@
 // Why radix 2^32: the measured gfx950 issue costs (tools/ubench_valu.hip,
 // profiles/r01_ubench_valu.txt) put v_mad_u64_u32 -- a full 32x32->64 product
 // plus a 64-bit addend -- at the same rate as a lone v_mul_lo_u32, so 64 of
-// them per schoolbook product beat the 100 of a 10 x 25.5-bit layout.  The
-// column (comba) accumulation keeps a 96-bit accumulator (64-bit pair + carry
-// word) and takes the mad's own carry-out, so each partial product costs one
-// v_mad_u64_u32 + one v_addc_co_u32 (tools/ubench_fe.hip: 214 VALU
-// instructions per multiply, 176 per squaring; profiles/r01_ubench_fe*.txt).
+// them per schoolbook product beat the 100 of a 10 x 25.5-bit layout.
 //
-// Reduction uses 2^256 == 38 (mod p).
+// The column (comba) accumulation keeps a 96-bit accumulator (64-bit pair +
+// carry word) and takes the mad's own carry-out, so each partial product costs
+// one v_mad_u64_u32 + one v_addc_co_u32.  A carry-save variant (a fresh 64-bit
+// accumulator per column, high columns folded as 64-bit mads) issues 10 fewer
+// instructions but 6 more mads per multiply and measured 9 % slower at one
+// wave per SIMD (tools/gen_fe_cs.py, tools/ubench_fecs.hip,
+// profiles/r02_ubench_fecs.txt).  The second carry fold of every product,
+// add and sub is taken only when a lane needs it (a wave-uniform branch).
 //
 // Carry chains are inline-asm strings.  hipcc's gfx950 hazard model pads
 // every VALU write of VCC/an SGPR that a later VALU reads (carry-in
@@ -23,11 +26,9 @@
 // before the first reader of its outputs; at one wave per SIMD those pads are
 // exposed issue slots.  Here each comba column, each add/sub/fold chain and
 // the squaring's diagonal add is one string whose carries pass through VCC
-// between adjacent instructions (the VOP2 carry-in read), so the static
-// s_nop count of k_verify_halved fell from 8763 to ~680 and its instruction
-// count from 33.8K to 25.3K (tools/isa_stats.py).  The unpadded hand-off is
-// checked bit-exact against host ports at 1, 4 and 8 waves per SIMD
-// (tools/ubench_carry.hip, tools/ubench_fe3.hip; profiles/r01_ubench_*.txt)
+// between adjacent instructions (the VOP2 carry-in read).  The unpadded hand-off is checked bit-exact
+// against host ports at 1, 4 and 8 waves per SIMD (tools/ubench_carry.hip,
+// tools/ubench_fecs.hip; profiles/r01_ubench_*.txt, profiles/r02_ubench_fecs.txt)
 // and by the whole GPU parity suite.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -160,83 +161,81 @@ COA_DEV void fe_set(fe& r, uint32_t x) {
 // takes its carry-in from VCC, written by the instruction before it.  hipcc's
 // own code pads every such hand-off with `s_nop 1` on gfx950; at one wave per
 // SIMD (the C2 occupancy) that costs 1.6x (tools/ubench_carry.hip,
-// profiles/r01_ubench_carry.txt: 241 -> 153 cycles per fe_add, bit-exact on
-// 3.4e7 lanes x 128 chained adds at 1, 4 and 8 waves per SIMD).
-#define COA_FOLD38_TAIL(R0, R1, R2, R3, R4, R5, R6, R7, T, Z)               \
-  "v_addc_co_u32_e32 %" #T ", vcc, 0, %" #Z ", vcc\n\t"                      \
-  "v_mul_u32_u24_e32 %" #T ", 38, %" #T "\n\t"                               \
-  "v_add_co_u32_e32 %" #R0 ", vcc, %" #R0 ", %" #T "\n\t"                    \
-  "v_addc_co_u32_e32 %" #R1 ", vcc, 0, %" #R1 ", vcc\n\t"                    \
-  "v_addc_co_u32_e32 %" #R2 ", vcc, 0, %" #R2 ", vcc\n\t"                    \
-  "v_addc_co_u32_e32 %" #R3 ", vcc, 0, %" #R3 ", vcc\n\t"                    \
-  "v_addc_co_u32_e32 %" #R4 ", vcc, 0, %" #R4 ", vcc\n\t"                    \
-  "v_addc_co_u32_e32 %" #R5 ", vcc, 0, %" #R5 ", vcc\n\t"                    \
-  "v_addc_co_u32_e32 %" #R6 ", vcc, 0, %" #R6 ", vcc\n\t"                    \
-  "v_addc_co_u32_e32 %" #R7 ", vcc, 0, %" #R7 ", vcc\n\t"                    \
-  "v_addc_co_u32_e32 %" #T ", vcc, 0, %" #Z ", vcc\n\t"                      \
-  "v_mul_u32_u24_e32 %" #T ", 38, %" #T "\n\t"                               \
-  "v_add_u32_e32 %" #R0 ", %" #R0 ", %" #T
+// profiles/r01_ubench_carry.txt).
 #define COA_R8_INOUT(r)                                                                                    \
   "+&v"(r.v[0]), "+&v"(r.v[1]), "+&v"(r.v[2]), "+&v"(r.v[3]), "+&v"(r.v[4]), "+&v"(r.v[5]), "+&v"(r.v[6]), \
       "+&v"(r.v[7])
 #define COA_B8_IN(b) \
   "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]), "v"(b.v[7])
 
-// r = a + b (mod p), result < 2^256.  2^256 == 38: the carry is folded back
-// in; a second carry can only occur when the sum wrapped to a value < 38, so
-// the last fold cannot carry.
+// r = a + b (mod p), result < 2^256.  2^256 == 38: the carry out of word 7
+// becomes 38 added to word 0.  That add carries on only when word 0 was
+// within 38 of 2^32 (probability ~2^-26 per lane), so the propagation through
+// words 1..7 runs behind a wave-uniform branch (s_cbranch_vccz skips it when
+// no lane carried); a carry out of that second pass leaves words that wrapped
+// to values < 38, so its fold cannot carry.
 COA_DEV void fe_add(fe& r, const fe& a, const fe& b) {
   fe x = a;
   uint32_t t;
-  const uint32_t z = 0;
-  asm("v_add_co_u32_e32 %0, vcc, %0, %10\n\t"
-      "v_addc_co_u32_e32 %1, vcc, %1, %11, vcc\n\t"
-      "v_addc_co_u32_e32 %2, vcc, %2, %12, vcc\n\t"
-      "v_addc_co_u32_e32 %3, vcc, %3, %13, vcc\n\t"
-      "v_addc_co_u32_e32 %4, vcc, %4, %14, vcc\n\t"
-      "v_addc_co_u32_e32 %5, vcc, %5, %15, vcc\n\t"
-      "v_addc_co_u32_e32 %6, vcc, %6, %16, vcc\n\t"
-      "v_addc_co_u32_e32 %7, vcc, %7, %17, vcc\n\t"
-      COA_FOLD38_TAIL(0, 1, 2, 3, 4, 5, 6, 7, 8, 9)
+  asm("v_add_co_u32_e32 %0, vcc, %0, %9\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %1, %10, vcc\n\t"
+      "v_addc_co_u32_e32 %2, vcc, %2, %11, vcc\n\t"
+      "v_addc_co_u32_e32 %3, vcc, %3, %12, vcc\n\t"
+      "v_addc_co_u32_e32 %4, vcc, %4, %13, vcc\n\t"
+      "v_addc_co_u32_e32 %5, vcc, %5, %14, vcc\n\t"
+      "v_addc_co_u32_e32 %6, vcc, %6, %15, vcc\n\t"
+      "v_addc_co_u32_e32 %7, vcc, %7, %16, vcc\n\t"
+      "v_cndmask_b32_e64 %8, 0, 38, vcc\n\t"
+      "v_add_co_u32_e32 %0, vcc, %0, %8\n\t"
+      "s_cbranch_vccz 1f\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
+      "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
+      "v_addc_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
+      "v_addc_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
+      "v_addc_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
+      "v_addc_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
+      "v_cndmask_b32_e64 %8, 0, 38, vcc\n\t"
+      "v_add_u32_e32 %0, %0, %8\n"
+      "1:"
       : COA_R8_INOUT(x), "=&v"(t)
-      : "v"(z), COA_B8_IN(b)
+      : COA_B8_IN(b)
       : "vcc");
   r = x;
 }
 
 // r = a - b (mod p), result < 2^256: a - b + 2^256 is computed, then
-// 2^256 == 38 subtracted once per borrow.
+// 2^256 == 38 subtracted once per borrow; the second borrow pass is behind
+// the same kind of wave-uniform branch as fe_add's.
 COA_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
   fe x = a;
   uint32_t t;
-  const uint32_t z = 0;
-  asm("v_sub_co_u32_e32 %0, vcc, %0, %10\n\t"
-      "v_subb_co_u32_e32 %1, vcc, %1, %11, vcc\n\t"
-      "v_subb_co_u32_e32 %2, vcc, %2, %12, vcc\n\t"
-      "v_subb_co_u32_e32 %3, vcc, %3, %13, vcc\n\t"
-      "v_subb_co_u32_e32 %4, vcc, %4, %14, vcc\n\t"
-      "v_subb_co_u32_e32 %5, vcc, %5, %15, vcc\n\t"
-      "v_subb_co_u32_e32 %6, vcc, %6, %16, vcc\n\t"
-      "v_subb_co_u32_e32 %7, vcc, %7, %17, vcc\n\t"
-      "v_addc_co_u32_e32 %8, vcc, 0, %9, vcc\n\t"
-      "v_mul_u32_u24_e32 %8, 38, %8\n\t"
+  asm("v_sub_co_u32_e32 %0, vcc, %0, %9\n\t"
+      "v_subb_co_u32_e32 %1, vcc, %1, %10, vcc\n\t"
+      "v_subb_co_u32_e32 %2, vcc, %2, %11, vcc\n\t"
+      "v_subb_co_u32_e32 %3, vcc, %3, %12, vcc\n\t"
+      "v_subb_co_u32_e32 %4, vcc, %4, %13, vcc\n\t"
+      "v_subb_co_u32_e32 %5, vcc, %5, %14, vcc\n\t"
+      "v_subb_co_u32_e32 %6, vcc, %6, %15, vcc\n\t"
+      "v_subb_co_u32_e32 %7, vcc, %7, %16, vcc\n\t"
+      "v_cndmask_b32_e64 %8, 0, 38, vcc\n\t"
       "v_sub_co_u32_e32 %0, vcc, %0, %8\n\t"
-      "v_subb_co_u32_e32 %1, vcc, %1, %9, vcc\n\t"
-      "v_subb_co_u32_e32 %2, vcc, %2, %9, vcc\n\t"
-      "v_subb_co_u32_e32 %3, vcc, %3, %9, vcc\n\t"
-      "v_subb_co_u32_e32 %4, vcc, %4, %9, vcc\n\t"
-      "v_subb_co_u32_e32 %5, vcc, %5, %9, vcc\n\t"
-      "v_subb_co_u32_e32 %6, vcc, %6, %9, vcc\n\t"
-      "v_subb_co_u32_e32 %7, vcc, %7, %9, vcc\n\t"
-      "v_addc_co_u32_e32 %8, vcc, 0, %9, vcc\n\t"
-      "v_mul_u32_u24_e32 %8, 38, %8\n\t"
-      "v_sub_u32_e32 %0, %0, %8"
+      "s_cbranch_vccz 1f\n\t"
+      "v_subbrev_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_subbrev_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
+      "v_subbrev_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
+      "v_subbrev_co_u32_e32 %4, vcc, 0, %4, vcc\n\t"
+      "v_subbrev_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
+      "v_subbrev_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
+      "v_subbrev_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
+      "v_cndmask_b32_e64 %8, 0, 38, vcc\n\t"
+      "v_sub_u32_e32 %0, %0, %8\n"
+      "1:"
       : COA_R8_INOUT(x), "=&v"(t)
-      : "v"(z), COA_B8_IN(b)
+      : COA_B8_IN(b)
       : "vcc");
   r = x;
 }
-
 
 // r += w (w < 2^32 - 2^10), then the carry folded as 38; result < 2^256.
 COA_DEV void fe_fold_word(fe& r, uint32_t w) {
@@ -266,8 +265,12 @@ COA_DEV void fe_neg(fe& r, const fe& a) {
 // ------------------------------------------------------------- reduction
 // r = t[0..15] (512-bit) mod p, result < 2^256.  The eight limb products
 // u_i = 38 t[8+i] + t[i] < 39 * 2^32 are independent mads (no carries, so
-// nothing to pad); one VCC chain then adds the high words one limb up, and a
-// second folds the top word (< 40) as 38 and its carry as 38 again.
+// nothing to pad); one VCC chain then adds the high words one limb up, and
+// the top word (< 40) is folded as 38 into word 0.  That add carries only
+// when word 0 was within 1,482 of 2^32 (~2^-21 per lane), so the
+// propagation through words 1..7 sits behind a wave-uniform s_cbranch_vccz
+// (skipped unless some lane carried); its own carry out leaves words that
+// wrapped to zero, so the 38 it adds to word 0 cannot carry.
 COA_DEV void fe_reduce512(fe& r, const uint32_t* t) {
   uint32_t lo[8], hi[8];
 #pragma unroll
@@ -287,7 +290,7 @@ COA_DEV void fe_reduce512(fe& r, const uint32_t* t) {
       "v_addc_co_u32_e32 %8, vcc, 0, %24, vcc\n\t"
       "v_mul_u32_u24_e32 %8, 38, %8\n\t"
       "v_add_co_u32_e32 %0, vcc, %9, %8\n\t"
-      "v_mov_b32_e32 %8, 0\n\t"
+      "s_cbranch_vccz 1f\n\t"
       "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
       "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
       "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
@@ -295,9 +298,9 @@ COA_DEV void fe_reduce512(fe& r, const uint32_t* t) {
       "v_addc_co_u32_e32 %5, vcc, 0, %5, vcc\n\t"
       "v_addc_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
       "v_addc_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
-      "v_addc_co_u32_e32 %8, vcc, 0, %8, vcc\n\t"
-      "v_mul_u32_u24_e32 %8, 38, %8\n\t"
-      "v_add_u32_e32 %0, %0, %8"
+      "v_cndmask_b32_e64 %8, 0, 38, vcc\n\t"
+      "v_add_u32_e32 %0, %0, %8\n"
+      "1:"
       : "=&v"(r.v[0]), "=&v"(r.v[1]), "=&v"(r.v[2]), "=&v"(r.v[3]), "=&v"(r.v[4]), "=&v"(r.v[5]), "=&v"(r.v[6]),
         "=&v"(r.v[7]), "=&v"(w)
       : "v"(lo[0]), "v"(lo[1]), "v"(lo[2]), "v"(lo[3]), "v"(lo[4]), "v"(lo[5]), "v"(lo[6]), "v"(lo[7]), "v"(hi[0]),
