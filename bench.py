@@ -546,7 +546,10 @@ def certificate_config(n_certs, latency_samples, cpu_threads, dev, stream, commi
            "signatures_per_s": round((nv + n_certs) / (dev_ms * 1e-3), 1),
            "host_certs_per_s": round(n_certs / host_el, 1),
            "p50_ms": round(float(np.percentile(lat, 50)), 3), "p99_ms": round(float(np.percentile(lat, 99)), 3),
-           "latency_samples": latency_samples}
+           "latency_samples": latency_samples, "latency_caller": "Python test binding (ctypes)"}
+    c50, c99 = latc_certificates(batch, min(20, n_certs), latency_samples)
+    res["c_caller"] = {"p50_ms": c50, "p99_ms": c99, "samples": latency_samples,
+                       "note": "the same calls from a C loop (tools/latc.c), as the Rust binding makes them"}
     # CPU: Certificate::verify crypto (dalek algorithms) on one core (the
     # reference verifies certificates serially in Core::run), and the whole
     # round on every usable CPU (one pthread each, C driver), both measured
@@ -582,6 +585,7 @@ def certificate_config(n_certs, latency_samples, cpu_threads, dev, stream, commi
                                          "sample": f"{done} certificates ({done // n_certs} passes over the "
                                                    f"round) on {cpu_threads} threads, {el:.2f} s wall"}}
     res["p50_vs_cpu"] = round(res["cpu_baseline"]["p50_ms"] / res["p50_ms"], 2)
+    res["c_caller"]["p50_vs_cpu"] = round(res["cpu_baseline"]["p50_ms"] / c50, 2)
     return res
 
 
@@ -649,12 +653,59 @@ def timed_steps(step, steps, warmup, world, dist, sync):
     return sharding.max_over_ranks(elapsed, dist, None)
 
 
+def _latc():
+    """tools/latc.c (lib/liblatc.so): the same one-item calls timed in a C
+    loop, as the Rust crate's extern "C" binding makes them (no Python
+    argument marshalling in the clock)."""
+    import ctypes
+
+    lib = ctypes.CDLL(os.path.join(PKG, "lib", "liblatc.so"))
+    vp, sz, dp = ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_double)
+    lib.latc_certificate.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                     ctypes.c_uint64, vp, vp, sz, ctypes.c_int, dp]
+    lib.latc_verify.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, dp]
+    return lib
+
+
+def _pctl(us):
+    import numpy as np
+
+    ms = np.asarray(us) * 1e-3
+    return round(float(np.percentile(ms, 50)), 4), round(float(np.percentile(ms, 99)), 4)
+
+
+def latc_certificates(batch, n, samples):
+    """C-caller p50/p99 (ms) of coa_certificate_verify over the first n
+    certificates of a batch, samples // n calls each."""
+    import ctypes
+
+    import numpy as np
+
+    lib = _latc()
+    per = max(1, samples // n)
+    out = (ctypes.c_double * per)()
+    us = []
+    for c in range(n):
+        lo, hi = int(batch.offsets[c]), int(batch.offsets[c + 1])
+        vp = np.ascontiguousarray(batch.vote_pks[lo:hi])
+        vs = np.ascontiguousarray(batch.vote_sigs[lo:hi])
+        rc = lib.latc_certificate(bytes(batch.header_inputs[c]), len(batch.header_inputs[c]), bytes(batch.ids[c]),
+                                  bytes(batch.authors[c]), bytes(batch.header_sigs[c]), batch.round,
+                                  vp.ctypes.data, vs.ctypes.data, hi - lo, per, out)
+        assert rc == 0, f"latc_certificate: {rc}"
+        us.extend(out[5:] if per > 10 else out[:])
+    return _pctl(us)
+
+
 def verify_single(local, cpu_p50_ms, samples=2000):
     """Signature::verify latency (Header::verify / Vote::verify call it one
     message at a time, primary/src/messages.rs:64-66,139-141): one
     coa_ed25519_verify_strict call per sample (host pointers in, verdict out),
     with the key registered in the committee cache and without, beside the
-    single-thread CPU restatement's p50."""
+    single-thread CPU restatement's p50; timed from Python and from a C loop
+    (tools/latc.c, as the Rust binding calls it)."""
+    import ctypes
+
     import numpy as np
 
     import coa_crypto
@@ -663,6 +714,7 @@ def verify_single(local, cpu_p50_ms, samples=2000):
     n = 64
     seeds, msgs = workloads.key_seeds(n, start=5000), workloads.messages(n, start=5000)
     pks, sigs = coa_crypto.sign_many(seeds, msgs)
+    msgs, pks, sigs = (np.ascontiguousarray(x, dtype=np.uint8) for x in (msgs, pks, sigs))
     out = {"workload": "one Signature::verify per call (32 B digest), host pointers, p50 over "
                        f"{samples} calls"}
     for label, reg in (("uncached_key", False), ("committee_key", True)):
@@ -678,8 +730,14 @@ def verify_single(local, cpu_p50_ms, samples=2000):
         lat = np.array(lat[50:]) * 1e3
         out[label] = {"p50_ms": round(float(np.percentile(lat, 50)), 4),
                       "p99_ms": round(float(np.percentile(lat, 99)), 4)}
+        buf = (ctypes.c_double * samples)()
+        rc = _latc().latc_verify(msgs.ctypes.data, pks.ctypes.data, sigs.ctypes.data, n, samples, buf)
+        assert rc == 0, f"latc_verify: {rc}"
+        c50, c99 = _pctl(buf[:])
+        out[label]["c_caller"] = {"p50_ms": c50, "p99_ms": c99}
         if cpu_p50_ms:
             out[label]["p50_vs_cpu"] = round(cpu_p50_ms / out[label]["p50_ms"], 3)
+            out[label]["c_caller"]["p50_vs_cpu"] = round(cpu_p50_ms / c50, 3)
     coa_crypto.committee_register(np.zeros((0, 32), np.uint8))
     out["cpu_single_thread_p50_ms"] = cpu_p50_ms
     return out

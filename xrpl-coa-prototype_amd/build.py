@@ -59,7 +59,24 @@ def build(verbose=False):
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
         if verbose:
             print("built", LIB)
+    _build_latc()
     return LIB
+
+
+def _build_latc():
+    """lib/liblatc.so: the C-caller latency loop of tools/latc.c (measurement
+    only; bench.py loads it), linked against the engine library."""
+    src = os.path.join(ROOT, "tools", "latc.c")
+    out = os.path.join(LIBDIR, "liblatc.so")
+    if not os.path.exists(src):
+        return
+    if os.path.exists(out) and os.path.getmtime(out) >= _newest([src, LIB, os.path.join(ROOT, "include", "coa_verify.h")]):
+        return
+    cmd = ["gcc", "-O2", "-std=c11", "-shared", "-fPIC", "-I" + os.path.join(ROOT, "include"), src, "-o", out,
+           "-L" + LIBDIR, "-lcoa_verify", "-Wl,-rpath,$ORIGIN"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"liblatc build failed:\n{r.stderr[-3000:]}")
 
 
 if __name__ == "__main__":

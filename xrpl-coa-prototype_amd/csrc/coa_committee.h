@@ -58,6 +58,20 @@ struct CertArgs {
   uint32_t total_blocks = 0;     // set by the launcher
 };
 
+// A small certificate passed inline in the kernel arguments of the latency
+// kernel (no host-to-device copy on the one-certificate path): the arrays of
+// CertArgs sit at the given byte offsets of buf (16-byte aligned; the header
+// bytes are followed by 16 bytes of slack for the aligned-dword reads).
+// CertArgs' pointers of those arrays are ignored; status, done_ctr and the
+// key-cache pointers are used as given.
+#define COA_CERT_INLINE_BYTES 2816
+struct CertInl {
+  CertArgs a;
+  uint32_t off_hdr, off_hoff, off_ids, off_origins, off_hsigs, off_rounds, off_voff, off_vpks, off_vsigs;
+  alignas(16) uint8_t buf[COA_CERT_INLINE_BYTES];
+};
+hipError_t coa_launch_cert_verify_inl(const CertInl& ci, hipStream_t s);
+
 hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s);
 hipError_t coa_launch_key_tables(const uint32_t* keys, uint32_t nk, uint32_t* tabs, hipStream_t s);
 // wide combs from the radix-256 key combs (tabs already built)

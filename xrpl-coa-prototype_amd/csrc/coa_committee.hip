@@ -53,6 +53,7 @@
 //                      runs the rounds (coa_sha512.h, compress_kw).
 #include "coa_committee.h"
 
+#include <cstddef>
 #include <cstdlib>
 
 #include "coa_fe.h"
@@ -459,7 +460,7 @@ COA_DEV void lat_block_done(const CertArgs& a) {
   }
 }
 
-__global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
+COA_DEV void cert_lat_body(const CertArgs& a) {
   const uint32_t wave = coa_sha::uni(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   if (blockIdx.x < a.nc) {  // header digest: schedule in parallel, rounds on wave 0
@@ -671,6 +672,29 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) {
   }
 }
 
+__global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) { cert_lat_body(a); }
+
+// The same with the certificate's arrays read from the kernel arguments.  The
+// buffer is addressed through the kernarg segment pointer (ci is the only
+// argument, at offset 0): a pointer taken from the by-value parameter itself
+// would make hipcc copy the whole 3 KB argument into scratch per thread.
+__global__ void __launch_bounds__(192) k_cert_verify_lat_inl(CertInl ci) {
+  CertArgs a = ci.a;
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(
+                         reinterpret_cast<uintptr_t>(__builtin_amdgcn_kernarg_segment_ptr())) +
+                     offsetof(CertInl, buf);
+  a.hdr_data = b + ci.off_hdr;
+  a.hdr_off = reinterpret_cast<const uint64_t*>(b + ci.off_hoff);
+  a.ids = reinterpret_cast<const uint32_t*>(b + ci.off_ids);
+  a.origins = reinterpret_cast<const uint32_t*>(b + ci.off_origins);
+  a.hsigs = reinterpret_cast<const uint32_t*>(b + ci.off_hsigs);
+  a.rounds = reinterpret_cast<const uint64_t*>(b + ci.off_rounds);
+  a.voff = reinterpret_cast<const uint64_t*>(b + ci.off_voff);
+  a.vpks = reinterpret_cast<const uint32_t*>(b + ci.off_vpks);
+  a.vsigs = reinterpret_cast<const uint32_t*>(b + ci.off_vsigs);
+  cert_lat_body(a);
+}
+
 // ---------------------------------------------------------------------------
 // Grid of the throughput kernel: two waves per SIMD (256 CUs x 4 SIMDs x 2
 // x 64 lanes), or one lane per job when there are fewer jobs.
@@ -730,6 +754,16 @@ hipError_t coa_launch_key_tables(const uint32_t* keys, uint32_t nk, uint32_t* ta
   if (nk == 0) return hipSuccess;
   const uint64_t lanes = (uint64_t)nk * COA_KEY_TAB_ENTRIES;
   hipLaunchKernelGGL(k_key_tables, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, keys, nk, tabs);
+  return hipGetLastError();
+}
+
+hipError_t coa_launch_cert_verify_inl(const CertInl& ci, hipStream_t s) {
+  if (ci.a.nc == 0) return hipSuccess;
+  CertInl c = ci;
+  c.a.hdr_blocks = (c.a.nc + 255) / 256;
+  const uint32_t jobs = c.a.nc + c.a.nv;
+  c.a.total_blocks = c.a.nc + jobs;
+  hipLaunchKernelGGL(k_cert_verify_lat_inl, dim3(c.a.total_blocks), dim3(192), 0, s, c);
   return hipGetLastError();
 }
 

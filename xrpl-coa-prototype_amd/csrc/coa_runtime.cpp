@@ -813,10 +813,73 @@ CertArgs cert_args(Dev& d, uint8_t* base, const CertPack& p, size_t nc, size_t n
 // Fast path for certificates [lo, hi) on one device: raw status words out.
 // publish: the latency variant writes its status words straight into
 // page-locked host memory (no D2H copy, no stream synchronisation).
+// The latency launch with the certificates inline in the kernel arguments
+// (no pinned staging copy, no H2D transfer): for calls whose arrays fit
+// COA_CERT_INLINE_BYTES.  Returns 1 when they do not fit (nothing launched).
+int cert_inline(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_out) {
+  const size_t nc = hi - lo;
+  const uint64_t h0 = in.hdr_off[lo], hb = in.hdr_off[hi] - h0;
+  const uint64_t v0 = in.voff[lo], nv = in.voff[hi] - v0;
+  static thread_local CertInl ci;  // ~3 KB, staged on the host; copied into the launch
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = align_up(o + bytes, 16);
+    return (uint32_t)at;
+  };
+  ci.off_hoff = take((nc + 1) * 8);
+  ci.off_voff = take((nc + 1) * 8);
+  ci.off_ids = take(nc * 32);
+  ci.off_origins = take(nc * 32);
+  ci.off_hsigs = take(nc * 64);
+  ci.off_rounds = take(nc * 8);
+  ci.off_vpks = take(nv * 32);
+  ci.off_vsigs = take(nv * 64);
+  ci.off_hdr = take(hb + 16);
+  if (o > COA_CERT_INLINE_BYTES || nc > 64) return 1;
+  uint8_t* b = ci.buf;
+  uint64_t* ho = reinterpret_cast<uint64_t*>(b + ci.off_hoff);
+  uint64_t* vo = reinterpret_cast<uint64_t*>(b + ci.off_voff);
+  for (size_t i = 0; i <= nc; i++) {
+    ho[i] = in.hdr_off[lo + i] - h0;
+    vo[i] = in.voff[lo + i] - v0;
+  }
+  std::memcpy(b + ci.off_ids, in.ids + lo * 32, nc * 32);
+  std::memcpy(b + ci.off_origins, in.origins + lo * 32, nc * 32);
+  std::memcpy(b + ci.off_hsigs, in.hsigs + lo * 64, nc * 64);
+  std::memcpy(b + ci.off_rounds, in.rounds + lo, nc * 8);
+  if (nv) {
+    std::memcpy(b + ci.off_vpks, in.vpks + v0 * 32, nv * 32);
+    std::memcpy(b + ci.off_vsigs, in.vsigs + v0 * 64, nv * 64);
+  }
+  if (hb) std::memcpy(b + ci.off_hdr, in.hdr_data + h0, hb);
+  std::memset(b + ci.off_hdr + hb, 0, 16);
+  hipStream_t s = d.stream;
+  if (!d.lat_ctr) {  // [0] block counter, [1..64] status words; the kernel re-zeroes both
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.lat_ctr), 65 * 4));
+    HIP_TRY(hipMemsetAsync(d.lat_ctr, 0, 65 * 4, s));
+  }
+  uint32_t tag = 0;
+  int rc = lat_res_prepare(d, nc, tag);
+  if (rc != COA_OK) return rc;
+  CertArgs& a = ci.a;
+  a = cert_args(d, nullptr, CertPack{}, nc, nv);
+  a.status = d.lat_ctr + 1;
+  a.host_res = d.lat_res;
+  a.done_ctr = d.lat_ctr;
+  a.tag = tag;
+  HIP_TRY(coa_launch_cert_verify_inl(ci, s));
+  return lat_res_wait(d, s, nc, tag, status_out + lo);
+}
+
 int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_out, bool publish = false) {
   const size_t nc = hi - lo;
   const uint64_t h0 = in.hdr_off[lo], hb = in.hdr_off[hi] - h0;
   const uint64_t v0 = in.voff[lo], nv = in.voff[hi] - v0;
+  if (publish && cert_lanes(nc + nv) == 64 && !env_is("COA_CERT_INLINE", "0")) {
+    const int rc = cert_inline(d, in, lo, hi, status_out);
+    if (rc != 1) return rc;
+  }
   const CertPack p = cert_layout(nc, nv, hb);
   HIP_TRY(d.pin.ensure(p.total));
   HIP_TRY(d.cert.ensure(p.total));
@@ -843,8 +906,8 @@ int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_
   const int lanes = cert_lanes(nc + nv);
   if (lanes == 64 && publish) {  // the last block writes the status words to host memory
     if (!d.lat_ctr) {
-      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.lat_ctr), 4));
-      HIP_TRY(hipMemsetAsync(d.lat_ctr, 0, 4, s));
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.lat_ctr), 65 * 4));
+      HIP_TRY(hipMemsetAsync(d.lat_ctr, 0, 65 * 4, s));
     }
     uint32_t tag = 0;
     int rc = lat_res_prepare(d, nc, tag);
