@@ -326,31 +326,25 @@ COA_DEV void load8_u4(uint32_t* dst, const void* src) {
   dst[4] = b.x; dst[5] = b.y; dst[6] = b.z; dst[7] = b.w;
 }
 
-// The checks that do not need k (the "pre" role of k_pre_halve): s < l, A and
-// R decompress (dalek rules), neither is small order; then the tables
-// j*(-A) (tab 0) and j*(-R) (tab 1), j = 1..8, in slab i.  Returns ok.
-COA_DEV bool pre_one(const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs, uint32_t i,
+// The checks that do not need k (the "pre" roles of k_pre_halve), for one of
+// the item's two points: which = 0 takes A (and s < l), which = 1 takes R.
+// The point decompresses (dalek rules) and is not small order; then its
+// table j*(-P), j = 1..8, goes to table `which` of slab i.  Returns ok.
+COA_DEV bool pre_one(const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs, uint32_t i, uint32_t which,
                      uint32_t* __restrict__ scr) {
-  uint32_t aw[8], rw[8], sw[8];
-  load8_u4(aw, pks + (uint64_t)i * 32);
-  load8_u4(rw, sigs + (uint64_t)i * 64);
+  uint32_t w[8], sw[8];
+  load8_u4(w, which ? sigs + (uint64_t)i * 64 : pks + (uint64_t)i * 32);
   load8_u4(sw, sigs + (uint64_t)i * 64 + 32);
-  bool ok = sc_is_canonical(sw);
-#pragma unroll 1
-  for (int which = 0; which < 2; which++) {
-    uint32_t w[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) w[j] = which ? rw[j] : aw[j];
-    ge_p3 Q;
-    const bool dec = ge_decompress(Q, w);
-    const bool small = ge_is_small_order(Q);
-    ok = ok && dec && !small;
-    fe_neg(Q.X, Q.X);
-    fe_neg(Q.T, Q.T);
-    // A's table may be built for an item whose R then fails: flags[i] = 0
-    // keeps k_verify_main from reading it
-    if (ok) tab2_build(scr, i, which, Q);
-  }
+  const bool s_ok = which || sc_is_canonical(sw);
+  ge_p3 Q;
+  const bool dec = ge_decompress(Q, w);
+  const bool small = ge_is_small_order(Q);
+  const bool ok = s_ok && dec && !small;
+  fe_neg(Q.X, Q.X);
+  fe_neg(Q.T, Q.T);
+  // a table may be built for an item whose other point then fails: that
+  // role's flag byte keeps k_verify_main from reading it
+  if (ok) tab2_build(scr, i, (int)which, Q);
   return ok;
 }
 }  // namespace
@@ -361,14 +355,16 @@ __global__ void __launch_bounds__(256) k_halve(const uint32_t* __restrict__ kbuf
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) halve_one(kbuf, sigs, i, rec);
 }
 
-// Split verification, phase 1 (one launch, two roles): blocks below
-// pre_blocks run pre_one for item blockIdx*256 + t; the others, for item
-// (blockIdx - pre_blocks)*256 + t, take k (from kbuf, or hashed here as
-// SHA-512(R || A || M) mod l when msgs is set), the halving record, and [e]B
-// from the comb, stored in cached form in ebp (32 dwords per item).  Neither
-// role needs the other's output, and at <= 256 VGPRs two waves share each
-// SIMD, so the latency-bound halving (f64 quotient chains) and the hash issue
-// in the gaps of the decompressions.
+// Split verification, phase 1 (one launch, three roles): blocks below
+// pre_blocks run pre_one on A for item blockIdx*256 + t, the next pre_blocks
+// on R; the others, for item (blockIdx - 2 pre_blocks)*256 + t, take k (from
+// kbuf, or hashed here as SHA-512(R || A || M) mod l when msgs is set), the
+// halving record, and optionally [e]B from the comb, stored in cached form in
+// ebp (32 dwords per item).  No role needs another's output, and at <= 168
+// VGPRs three waves share each SIMD: the two decompression waves issue into
+// each other's gaps (a lone wave issues a VALU instruction at most every ~4
+// cycles), and the latency-bound halving (f64 quotient chains) and the hash
+// fill what is left.  flags[2i + which] is the A / R role's pre-check.
 template <int WAVES>
 __global__ void __launch_bounds__(256, WAVES) k_pre_halve(const uint8_t* __restrict__ pks,
                                                       const uint8_t* __restrict__ sigs,
@@ -377,14 +373,23 @@ __global__ void __launch_bounds__(256, WAVES) k_pre_halve(const uint8_t* __restr
                                                       uint32_t n, uint32_t* __restrict__ rec,
                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ scr,
                                                       uint32_t* __restrict__ ebp, const uint32_t* __restrict__ comb,
-                                                      const uint32_t* __restrict__ wcomb, uint32_t pre_blocks) {
-  if (blockIdx.x < pre_blocks) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) flags[i] = pre_one(pks, sigs, i, scr) ? 1 : 0;
+                                                      const uint32_t* __restrict__ wcomb, uint32_t pre_blocks,
+                                                      int prio) {
+  if (blockIdx.x < 2 * pre_blocks) {
+    if (prio & 2) return;  // diagnostic (COA_PRE_DIAG): time the hash role alone
+    const uint32_t which = blockIdx.x >= pre_blocks ? 1u : 0u;
+    const uint32_t i = (blockIdx.x - which * pre_blocks) * blockDim.x + threadIdx.x;
+    if (i < n) flags[2 * i + which] = pre_one(pks, sigs, i, which, scr) ? 1 : 0;
     return;
   }
-  const uint32_t i = (blockIdx.x - pre_blocks) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  const uint32_t i = (blockIdx.x - 2 * pre_blocks) * blockDim.x + threadIdx.x;
+  if (i >= n || (prio & 4)) return;  // diagnostic: time the decompression roles alone
+  // The hash and the halving are dependency chains (f64 quotient estimates)
+  // that need few issue slots but need them promptly; the decompression waves
+  // beside them issue every cycle they can.  VALU issue goes to the higher
+  // priority first (then the older wave), so at equal priority this role
+  // would only run in the decompressions' leftover slots.
+  if (prio & 1) __builtin_amdgcn_s_setprio(3);
   uint32_t k[8], sw[8], e[8];
   if (msgs) {
     coa_sha::Segs sg;
@@ -448,7 +453,7 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
                                                         const uint32_t* __restrict__ wcomb) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = i < n;
-  const bool ok = live && flags[i] != 0;
+  const bool ok = live && reinterpret_cast<const uint16_t*>(flags)[i] == 0x0101u;
   const uint32_t* myrec = rec + (uint64_t)(live ? i : 0) * 32;
   const uint32_t meta = live ? myrec[24] : 0u;
   const int H = wave_max(ok ? (int)(meta & 0xffu) : 0);
@@ -676,8 +681,13 @@ hipError_t coa_launch_verify_split(const uint8_t* pks, const uint8_t* sigs, cons
   static const uint32_t pre_b = block_env("COA_PRE_BLOCK"), main_b = block_env("COA_MAIN_BLOCK");
   const uint32_t blocks = (n + pre_b - 1) / pre_b;
   const int aligned = ((msg_len & 3) == 0) && (((uintptr_t)msgs & 3) == 0);
-  hipLaunchKernelGGL(k_pre_halve<2>, dim3(2 * blocks), dim3(pre_b), 0, s, pks, sigs, msgs, msg_len, aligned, kbuf, n,
-                     rec, flags, scratch, ebp, comb, wcomb, blocks);
+  // COA_PRE_PRIO=0: the hash/halving role at the default wave priority (A/B)
+  // COA_PRE_DIAG=2 / 4: skip the decompression / hash roles (timing only;
+  // verdicts are then meaningless)
+  static const int prio = (getenv("COA_PRE_PRIO") && atoi(getenv("COA_PRE_PRIO")) == 0 ? 0 : 1) |
+                          (getenv("COA_PRE_DIAG") ? atoi(getenv("COA_PRE_DIAG")) & 6 : 0);
+  hipLaunchKernelGGL(k_pre_halve<3>, dim3(3 * blocks), dim3(pre_b), 0, s, pks, sigs, msgs, msg_len, aligned, kbuf, n,
+                     rec, flags, scratch, ebp, comb, wcomb, blocks, prio);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_verify_main<2>, dim3((n + main_b - 1) / main_b), dim3(main_b), 0, s, rec, flags, n, verdicts,

@@ -309,7 +309,7 @@ std::vector<Range> shard(size_t n) {
 struct Workspace {
   uint32_t* k;
   uint32_t* rec;
-  uint8_t* flags;  // split path: pre-check verdict per item
+  uint8_t* flags;  // split path: pre-check verdicts, two bytes (A, R) per item
   uint32_t* ebp;   // split path: [e]B per item (cached form, 128 B)
   uint32_t* scratch;
 };
@@ -318,7 +318,7 @@ size_t ws_bytes(size_t n) {
   // scratch: per-lane slabs (single-kernel path) or per-item slabs of one
   // split chunk, whichever is larger (the path is chosen per call)
   const size_t slabs = std::max<size_t>(verify_lanes(n), std::min<size_t>(n, COA_SPLIT_CHUNK));
-  return align_up(n * 32, 256) + align_up(n * COA_HALVE_REC_BYTES, 256) + align_up(n, 256) + n * 128 +
+  return align_up(n * 32, 256) + align_up(n * COA_HALVE_REC_BYTES, 256) + align_up(2 * n, 256) + n * 128 +
          slabs * COA_HALVED_SCRATCH_PER_LANE;
 }
 Workspace ws_carve(void* base, size_t n) {
@@ -330,7 +330,7 @@ Workspace ws_carve(void* base, size_t n) {
   w.rec = reinterpret_cast<uint32_t*>(p);
   p += align_up(n * COA_HALVE_REC_BYTES, 256);
   w.flags = p;
-  p += align_up(n, 256);
+  p += align_up(2 * n, 256);
   w.ebp = reinterpret_cast<uint32_t*>(p);
   p += n * 128;
   w.scratch = reinterpret_cast<uint32_t*>(p);
@@ -350,7 +350,7 @@ int enqueue_split(Dev& d, const uint8_t* d_msgs, size_t msg_len, const uint32_t*
     const uint32_t cnt = (uint32_t)std::min<size_t>(COA_SPLIT_CHUNK, n - lo);
     HIP_TRY(coa_launch_verify_split(d_pks + lo * 32, d_sigs + lo * 64, d_k ? nullptr : d_msgs + lo * msg_len,
                                     (uint32_t)msg_len, d_k ? d_k + lo * 8 : nullptr, cnt, w.rec + lo * 32,
-                                    w.flags + lo, d_verdicts + lo, w.scratch,
+                                    w.flags + 2 * lo, d_verdicts + lo, w.scratch,
                                     env_is("COA_SPLIT_EB", "1") ? w.ebp : nullptr, d.comb, wcomb_of(d), s));
   }
   return COA_OK;
