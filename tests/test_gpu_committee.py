@@ -299,15 +299,19 @@ def world(engine):
     return World(engine)
 
 
-@pytest.fixture(params=["64", "1/T0", "1/T256", "1/T512", "1/T0/narrow"])
+@pytest.fixture(params=["64", "64/staged", "1/T0", "1/T256", "1/T512", "1/T0/narrow"])
 def lanes(request):
     """Latency kernel (64) and throughput kernel with one signature per lane
     (T0 = default grid) or a grid of 256 / 512 lanes, so each lane shares one
     inversion among several signatures (P compared with R's encoding).
     `narrow`: [s]B and [k](-A) from the radix-256 combs instead of the wide
-    HBM comb of B and the keys' wide combs."""
+    HBM comb of B and the keys' wide combs.  `staged`: one-certificate calls
+    through the pinned staging copy instead of the kernel arguments
+    (COA_CERT_INLINE=0; certificates over 2,816 bytes take it anyway)."""
     parts = request.param.split("/")
     os.environ["COA_CERT_LANES"] = parts[0]
+    if "staged" in parts:
+        os.environ["COA_CERT_INLINE"] = "0"
     if len(parts) > 1 and parts[1] != "T0":
         os.environ["COA_CERT_LANES_TOTAL"] = parts[1][1:]
     if "narrow" in parts:
@@ -315,6 +319,7 @@ def lanes(request):
         os.environ["COA_KEY_WCOMB"] = "0"
     yield int(parts[0])
     del os.environ["COA_CERT_LANES"]
+    os.environ.pop("COA_CERT_INLINE", None)
     os.environ.pop("COA_CERT_LANES_TOTAL", None)
     os.environ.pop("COA_WCOMB", None)
     os.environ.pop("COA_KEY_WCOMB", None)

@@ -2,6 +2,7 @@
 //   launch   hipLaunchKernelGGL of a 5-workgroup kernel whose last block
 //            writes a tagged word into page-locked host memory; the host
 //            polls it (the engine's latency-path protocol)
+//   launch3KB the same with 3 KB of kernel arguments (the inline certificate)
 //   resident the same 5 workgroups already running, each polling a job word
 //            in page-locked host memory; the host writes the job, the last
 //            block publishes the tagged result (a persistent kernel's
@@ -23,6 +24,19 @@ __global__ void k_once(uint32_t* res, uint32_t* ctr, uint32_t tag, uint32_t bloc
   if (old + 1 != blocks) return;
   __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(res, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+struct Big {
+  uint32_t w[768];  // 3 KB of kernel arguments, as the inline certificate launch
+};
+__global__ void k_once_big(Big b, uint32_t* res, uint32_t* ctr, uint32_t tag, uint32_t blocks) {
+  if (threadIdx.x) return;
+  const uint32_t x = b.w[blockIdx.x * 64];  // touch the argument block
+  __threadfence();
+  const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1 != blocks) return;
+  __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(res, tag + (x & 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // job word: (seq << 1) | quit.  Every block waits for a new seq, then counts
@@ -75,6 +89,18 @@ int main() {
     if (i > 50) t.push_back(now_us() - t0);
   }
   report("launch", t);
+  (void)hipStreamSynchronize(s);
+  static Big big;
+  for (int i = 0; i < 768; i++) big.w[i] = i;
+  t.clear();
+  for (int i = 1; i <= N + 50; i++) {
+    const double t0 = now_us();
+    hipLaunchKernelGGL(k_once_big, dim3(blocks), dim3(192), 0, s, big, res, ctr, (uint32_t)(i + 100000), blocks);
+    while (__atomic_load_n(res, __ATOMIC_ACQUIRE) != (uint32_t)(i + 100000)) {
+    }
+    if (i > 50) t.push_back(now_us() - t0);
+  }
+  report("launch3KB", t);
   (void)hipStreamSynchronize(s);
   *res = 0;
   hipLaunchKernelGGL(k_resident, dim3(blocks), dim3(192), 0, s, job, res, ctr, blocks);
