@@ -80,3 +80,20 @@ def test_every_verify_path_agrees(engine, impl, monkeypatch):
     got = engine.verify_strict_many(msgs, pks, sigs)
     exp = co.verify_strict_many(msgs, pks, sigs, min(16, os.cpu_count() or 1))
     assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+
+
+@pytest.mark.parametrize("n", [1, 3, 255, 257, 769])
+def test_split_path_ragged_small_calls(engine, n, monkeypatch):
+    """The split kernels on call sizes around their block edges (one to three
+    blocks per role of k_pre_halve, partial last blocks): COA_LAT_MAX=0 keeps
+    these small calls off the latency route.  Adversarial mix vs the oracle."""
+    from workloads import adversarial_mix, messages
+
+    monkeypatch.setenv("COA_LAT_MAX", "0")
+    m0 = messages(n, 31)
+    pks, sigs = engine.sign_many(np.frombuffer(bytes(range(256)) * ((32 * n) // 256 + 1), np.uint8)[: 32 * n]
+                                 .reshape(n, 32), m0)
+    msgs, pks, sigs, _ = adversarial_mix(m0, pks, sigs, frac=0.3, seed=n, mixed_pool=_pool())
+    got = engine.verify_strict_many(msgs, pks, sigs)
+    exp = co.verify_strict_many(msgs, pks, sigs, 1)
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
