@@ -443,20 +443,29 @@ extern "C" int coa_lat_trace(unsigned long long* out) {
 #else
 #define LAT_MARK(w, i)
 #endif
-// With a.host_res set, the block that finishes last publishes every
-// certificate's status word into page-locked host memory, tagged with the
-// call (the host polls for the tag: no device-to-host copy, no stream
-// synchronisation), resets the status words and the block counter for the
-// next call.  Called by one thread per block after that block's status write.
-COA_DEV void lat_block_done(const CertArgs& a) {
+// One block's end of the latency kernel (one thread): OR its status bits
+// into certificate c's word and, with a.host_res set, count itself done; the
+// block that finishes last publishes every certificate's status word into
+// page-locked host memory, tagged with the call (the host polls for the tag:
+// no device-to-host copy, no stream synchronisation), and resets the status
+// words and the block counter for the next call.
+// Every value that crosses blocks is an atomic on its own word, so no fence
+// orders other memory: the OR is a returning atomic whose completion the
+// block waits for (s_waitcnt) before its count, so the last block's exchange
+// (issued after its count saw every other block's) finds every OR.  The
+// acq_rel fences this replaced cost an L2 write-back and an L1 invalidate
+// each (buffer_wbl2 / buffer_inv sc1), four and three of them on the
+// critical block's tail.
+COA_DEV void lat_block_done(const CertArgs& a, uint32_t c, uint32_t bits) {
+  if (bits) (void)__hip_atomic_fetch_or(a.status + c, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (!a.host_res) return;
-  __threadfence();
-  const uint32_t old = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint32_t old = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (old + 1 != a.total_blocks) return;
   __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (uint32_t c = 0; c < a.nc; c++) {
-    const uint32_t st = __hip_atomic_exchange(a.status + c, 0u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a.host_res + c, (a.tag << 8) | (st & 0xffu), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (uint32_t k = 0; k < a.nc; k++) {
+    const uint32_t st = __hip_atomic_exchange(a.status + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.host_res + k, (a.tag << 8) | (st & 0xffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -493,8 +502,7 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
     bool same = true;
 #pragma unroll
     for (int i = 0; i < 8; i++) same = same && h[i] == id[i];
-    if (lane == 0 && !same) atomicOr(a.status + c, COA_CST_BAD_HEADER_ID);
-    if (lane == 0) lat_block_done(a);
+    if (lane == 0) lat_block_done(a, c, same ? 0u : (uint32_t)COA_CST_BAD_HEADER_ID);
     return;
   }
   __shared__ uint32_t r_lds[17];  // R.X, R.Y, decompress ok
@@ -667,8 +675,7 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
       }
     }
     LAT_MARK(0, 5)
-    if (lane == 0 && bits) atomicOr(a.status + c, bits);
-    if (lane == 0) lat_block_done(a);
+    if (lane == 0) lat_block_done(a, c, bits);
   }
 }
 

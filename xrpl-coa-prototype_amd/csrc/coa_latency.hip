@@ -172,9 +172,11 @@ COA_DEV void horner(ge_p3& out, const uint32_t* tab, const uint32_t* rec, int H,
 
 // The verdict straight into page-locked host memory, tagged with the call:
 // the host polls for the tag instead of a device-to-host copy and a stream
-// synchronisation (one PCIe write per signature).
+// synchronisation (one PCIe write per signature).  The word is the whole
+// message, so the store is relaxed: a release would first write back the L2
+// (buffer_wbl2) for data nobody reads.
 COA_DEV void publish(const LatArgs& a, uint32_t item, bool ok) {
-  __hip_atomic_store(a.res + item, (a.tag << 8) | (ok ? 0u : 1u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(a.res + item, (a.tag << 8) | (ok ? 0u : 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
