@@ -304,6 +304,11 @@ typedef void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, 
 coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us);
 int coa_queue_submit_verify(coa_queue* q, const uint8_t msg[32], const uint8_t pk[32], const uint8_t sig[64],
                             coa_verdict_cb cb, void* user);
+/* n independent triples in one request (one copy, one lock, one callback
+ * with the n verdict bytes in order): for producers that already hold a
+ * group of messages, e.g. a window of received votes. */
+int coa_queue_submit_verify_many(coa_queue* q, const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, size_t n,
+                                 coa_verdict_cb cb, void* user);
 int coa_queue_submit_batch(coa_queue* q, const uint8_t msg[32], const uint8_t* pks, const uint8_t* sigs, size_t n,
                            coa_verdict_cb cb, void* user);
 /* Whole certificates (the fused Certificate::verify crypto, f3): the

@@ -155,6 +155,8 @@ extern "C" {
     pub fn coa_queue_create(max_batch: usize, max_delay_us: u32) -> *mut CoaQueue;
     pub fn coa_queue_submit_verify(q: *mut CoaQueue, msg: *const u8, pk: *const u8, sig: *const u8,
                                    cb: CoaVerdictCb, user: *mut c_void) -> c_int;
+    pub fn coa_queue_submit_verify_many(q: *mut CoaQueue, msgs: *const u8, pks: *const u8, sigs: *const u8,
+                                        n: usize, cb: CoaVerdictCb, user: *mut c_void) -> c_int;
     pub fn coa_queue_submit_batch(q: *mut CoaQueue, msg: *const u8, pks: *const u8, sigs: *const u8, n: usize,
                                   cb: CoaVerdictCb, user: *mut c_void) -> c_int;
     pub fn coa_queue_submit_certificate(q: *mut CoaQueue, header_data: *const u8, header_len: usize,

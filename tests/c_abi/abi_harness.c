@@ -167,6 +167,10 @@ int main(int argc, char** argv) {
   CHECK(coa_queue_submit_verify(q, msg, pk, sig, cb, &seen) == COA_OK, "queue_submit_verify");
   CHECK(coa_queue_flush(q) == COA_OK, "queue_flush");
   CHECK(seen == dev_rc, "queue verify callback status");
+  CHECK(coa_queue_submit_verify_many(q, msg, pk, sig, 1, cb, &seen) == COA_OK, "queue_submit_verify_many");
+  CHECK(coa_queue_submit_verify_many(q, msg, pk, sig, 0, cb, &seen) == COA_EINVAL, "queue_submit_verify_many(n=0)");
+  CHECK(coa_queue_flush(q) == COA_OK, "queue_flush many");
+  CHECK(seen == dev_rc, "queue verify_many callback status");
   CHECK(coa_queue_submit_batch(q, msg, pk, sig, 1, cb, &seen) == COA_OK, "queue_submit_batch");
   CHECK(coa_queue_submit_certificate(q, data, 13, msg, pk, sig, 1, NULL, NULL, 0, cb, &seen) == COA_OK,
         "queue_submit_certificate");
@@ -174,10 +178,10 @@ int main(int argc, char** argv) {
   CHECK(coa_queue_submit_verify(q, msg, pk, sig, NULL, NULL) == COA_EINVAL, "queue_submit_verify(null cb)");
   CHECK(coa_queue_flush(q) == COA_OK, "queue_flush 2");
   uint64_t launches = 0, items = 0, groups = 0, digests = 0;
-  CHECK(coa_queue_stats(q, &launches, &items, &groups) == COA_OK && items == 1 && groups == 2, "queue_stats");
+  CHECK(coa_queue_stats(q, &launches, &items, &groups) == COA_OK && items == 2 && groups == 2, "queue_stats");
   CHECK(coa_queue_digest_count(q, &digests) == COA_OK && digests == 1, "queue_digest_count");
   coa_queue_metrics_t qm;
-  CHECK(coa_queue_metrics(q, &qm) == COA_OK && qm.requests == 4 && qm.signatures == 1 && qm.batches == 1 &&
+  CHECK(coa_queue_metrics(q, &qm) == COA_OK && qm.requests == 5 && qm.signatures == 2 && qm.batches == 1 &&
             qm.certificates == 1 && qm.digests == 1 && qm.wait_us_max >= qm.wait_us_mean,
         "queue_metrics");
   CHECK(coa_queue_destroy(q) == COA_OK, "queue_destroy");

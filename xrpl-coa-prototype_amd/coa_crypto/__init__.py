@@ -124,6 +124,7 @@ def lib():
                                     ctypes.c_int),
         "coa_queue_create": ([sz, ctypes.c_uint32], vp),
         "coa_queue_submit_verify": ([vp, P8, P8, P8, VERDICT_CB, vp], ctypes.c_int),
+        "coa_queue_submit_verify_many": ([vp, P8, P8, P8, sz, VERDICT_CB, vp], ctypes.c_int),
         "coa_queue_submit_batch": ([vp, P8, P8, P8, sz, VERDICT_CB, vp], ctypes.c_int),
         "coa_queue_submit_certificate": ([vp, P8, sz, P8, P8, P8, ctypes.c_uint64, P8, P8, sz, VERDICT_CB, vp],
                                          ctypes.c_int),

@@ -37,6 +37,23 @@ struct Window {
   std::vector<uint8_t> d_out;    // nd x 32
   int rc = COA_OK;               // engine status of the window (negative = failure)
   int slot = -1;                 // backend slot the window ran on
+
+  // Empty again for the next window, keeping every vector's capacity (the
+  // queue recycles answered windows, so a window fills without reallocating
+  // under the intake lock).
+  void reset() {
+    nv = ng = nc = nd = 0;
+    for (auto* v : {&v_msgs, &v_pks, &v_sigs, &v_out, &g_msgs, &g_pks, &g_sigs, &g_out, &c_hdata, &c_ids, &c_origins,
+                    &c_hsigs, &c_pks, &c_sigs, &c_out, &d_data, &d_out})
+      v->clear();
+    for (auto* v : {&g_offs, &c_hoff, &c_rounds, &c_voff, &d_offs}) v->clear();
+    g_offs.push_back(0);
+    c_hoff.push_back(0);
+    c_voff.push_back(0);
+    d_offs.push_back(0);
+    rc = COA_OK;
+    slot = -1;
+  }
 };
 
 class Backend {

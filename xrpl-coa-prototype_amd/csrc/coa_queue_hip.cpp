@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -29,6 +30,8 @@
 
 #include "coa_committee.h"
 #include "coa_queue.h"
+
+#define COA_QUEUE_SLOTS_DEFAULT 2
 
 namespace {
 
@@ -146,7 +149,14 @@ class HipBackend : public coa_q::Backend {
       init_rc_ = n < 0 ? n : COA_ENODEVICE;
       return false;
     }
-    slots_.resize(2 * (size_t)std::min(n, 64));
+    // device slots per GPU: windows in flight at once (COA_QUEUE_SLOTS,
+    // 1..8; tools/queue_probe.c measures the choice)
+    size_t per = COA_QUEUE_SLOTS_DEFAULT;
+    if (const char* e = getenv("COA_QUEUE_SLOTS")) {
+      const int v = atoi(e);
+      if (v >= 1 && v <= 8) per = (size_t)v;
+    }
+    slots_.resize(per * (size_t)std::min(n, 64));
     for (size_t k = 0; k < slots_.size(); k++) {
       Slot& sl = slots_[k];
       sl.dev = ids[k % (size_t)std::min(n, 64)];
