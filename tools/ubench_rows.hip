@@ -17,7 +17,7 @@ __global__ void k(const uint32_t* in, uint32_t* out, long long* cyc) {
   s ^= r.v[0];
   long long t2 = clock64();
   uint32_t x = fw::from_fe(z);
-  x = fw::sqn(x, 100);
+  x = fw::sqn<100>(x);
   long long t3 = clock64();
   fe y = z;
   fe_sqn(y, y, 100);

@@ -51,6 +51,8 @@
 //                      workgroup per header digest: its lanes expand every
 //                      block's message schedule into LDS, then one wave
 //                      runs the rounds (coa_sha512.h, compress_kw).
+// kernels here exceed the +-128 KiB reach of an out-of-line fold (coa_fe.h)
+#define COA_RARE_INLINE
 #include "coa_committee.h"
 
 #include <cstddef>
@@ -61,6 +63,7 @@
 #include "coa_halved.h"
 #include "coa_sc.h"
 #include "coa_keycache.h"
+#include "coa_rcmp.h"
 #include "coa_sha512.h"
 #include "coa_smul.h"
 
@@ -505,10 +508,13 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
     if (lane == 0) lat_block_done(a, c, same ? 0u : (uint32_t)COA_CST_BAD_HEADER_ID);
     return;
   }
-  __shared__ uint32_t r_lds[17];  // R.X, R.Y, decompress ok
   __shared__ uint32_t s_lds[32];  // [s]B from wave 2
-  __shared__ uint32_t s_ready;    // wave 2 published s_lds
-  if (threadIdx.x == 0) s_ready = 0;
+  __shared__ uint32_t s_ready;    // wave 2 published [s]B
+  __shared__ rcmp::Shared cmp;    // wave 0's half of the compare, for wave 1
+  if (threadIdx.x == 0) {
+    s_ready = 0;
+    cmp.ready = 0;
+  }
   __syncthreads();
   const uint32_t job = blockIdx.x - a.nc;
   const bool hdr = job < a.nc;
@@ -517,154 +523,14 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
   const uint32_t* sig = sel_ptr(hdr, a.hsigs + (uint64_t)c * 16, a.vsigs + (uint64_t)vi * 16);
   uint32_t rw[8];
   load8u(rw, sig);
-  uint32_t bits = 0;
-  ge_p3 P;
   LAT_MARK(wave, 0)
-  if (wave == 1) {  // R's decompression, the power chain on the wave's DPP rows
-    ge_p3 R;
-    const bool ok = ge_decompress<true>(R, rw);
+  if (wave == 1) {  // R's decompression on the wave's DPP rows, the compare, the verdict
+    uint32_t bits = 0;
+    const uint32_t res = rcmp::decompress_eq(cmp, rw, bits);
     LAT_MARK(1, 1)
-    if (lane == 0) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        r_lds[i] = R.X.v[i];
-        r_lds[8 + i] = R.Y.v[i];
-      }
-      r_lds[16] = ok;
-    }
-  } else {
-    // one comb term per lane (lanes 0..31; the upper half sums a copy),
-    // [s]B on wave 2 from B's comb, [k](-A) on wave 0 from the key's comb
-    uint32_t dg[8];
-    const uint32_t* tab = a.comb;
-    int slot = 0;
-    uint32_t pre = 0;
-    if (wave == 2) {
-      load8u(dg, sig + 8);
-    } else {
-      uint32_t pk[8], sw[8], msg[8];
-      load8u(pk, sel_ptr(hdr, a.origins + (uint64_t)c * 8, a.vpks + (uint64_t)vi * 8));
-      load8u(sw, sig + 8);
-      load8u(msg, a.ids + (uint64_t)c * 8);
-      slot = key_lookup_u(a.keys, a.nk, pk);
-      if (slot < 0) {
-        bits = COA_CST_UNCACHED;
-        slot = 0;
-      } else {
-        uint64_t st[8];
-        uint32_t h[16];
-        if (!hdr) {  // Certificate::digest on the scalar unit
-          uint32_t in[18];
-          const uint64_t rd = uni64(a.rounds[c]);
-#pragma unroll
-          for (int i = 0; i < 8; i++) in[i] = msg[i];
-          in[8] = (uint32_t)rd;
-          in[9] = (uint32_t)(rd >> 32);
-          load8u(in + 10, a.origins + (uint64_t)c * 8);
-          coa_sha::hash_words<18>(st, in);
-          coa_sha::state_to_le_words(h, st);
-#pragma unroll
-          for (int i = 0; i < 8; i++) msg[i] = h[i];
-        }
-        uint32_t in[24];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          in[i] = rw[i];
-          in[8 + i] = pk[i];
-          in[16 + i] = msg[i];
-        }
-        coa_sha::hash_words<24>(st, in);
-        coa_sha::state_to_le_words(h, st);
-        sc k;
-        sc_reduce512(k, h);
-        const uint32_t kf = coa_sha::uni(a.kflags[slot]);
-        const bool s_ok = sc_is_canonical(sw);
-        const bool a_ok = (kf & COA_KEY_DECOMPRESSES) != 0;
-        pre = (s_ok ? 0u : 1u) | (a_ok ? 0u : 2u) | ((kf & COA_KEY_SMALL_ORDER) ? 4u : 0u) |
-              ((kf & COA_KEY_TORSION_FREE) ? 0u : 8u);
-#pragma unroll
-        for (int i = 0; i < 8; i++) dg[i] = k.v[i];
-        tab = a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS;
-      }
-    }
-    LAT_MARK(wave, 1)
-    if (!(bits & COA_CST_UNCACHED)) {
-      add_const_word(dg, 0x80808080u);
-      const int j = lane & 31;
-      const int e = (int)byte_of(dg, j) - 128;
-      ge_niels q;
-      comb_select(q, tab, j, e);
-      ge_p1p1 t;
-      ge_p3_identity(P);
-      ge_madd(t, P, q);
-      ge_p1p1_to_p3(P, t);
-      LAT_MARK(wave, 2)
-#pragma unroll 1
-      for (int off = 16; off >= 1; off >>= 1) {
-        ge_p3 O;
-        shfl_fe<64>(O.X, P.X, off);
-        shfl_fe<64>(O.Y, P.Y, off);
-        shfl_fe<64>(O.Z, P.Z, off);
-        shfl_fe<64>(O.T, P.T, off);
-        ge_cached oc;
-        ge_p3_to_cached(oc, O);
-        ge_add(t, P, oc);
-        ge_p1p1_to_p3(P, t);
-      }
-      LAT_MARK(wave, 3)
-      if (wave == 2 && lane == 0) {
-        const fe* f[4] = {&P.X, &P.Y, &P.Z, &P.T};
-#pragma unroll
-        for (int q4 = 0; q4 < 4; q4++)
-#pragma unroll
-          for (int i = 0; i < 8; i++) s_lds[q4 * 8 + i] = f[q4]->v[i];
-        __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      bits = pre << 8;  // pre-verdict flags, resolved after the hand-off
-    }
-  }
-  // wave 0 finishes everything that needs only P while wave 1 is still
-  // decompressing R (the critical chain): P = [s]B + [k](-A) as soon as wave 2
-  // has published [s]B, verify_strict's small-order test, the projective form
-  ge_p2 P2;
-  if (wave == 0 && !(bits & COA_CST_UNCACHED)) {
-    uint32_t pre = bits >> 8;
-#pragma unroll 1
-    while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-      __builtin_amdgcn_s_sleep(1);
-    {  // P = [s]B + [k](-A)
-      ge_p3 S;
-      fe* f[4] = {&S.X, &S.Y, &S.Z, &S.T};
-#pragma unroll
-      for (int q4 = 0; q4 < 4; q4++)
-#pragma unroll
-        for (int i = 0; i < 8; i++) f[q4]->v[i] = s_lds[q4 * 8 + i];
-      ge_cached sc4;
-      ge_p3_to_cached(sc4, S);
-      ge_p1p1 t;
-      ge_add(t, P, sc4);
-      ge_p1p1_to_p3(P, t);
-    }
-    // verify_strict's small-order test of R, taken on P: an accepting
-    // verdict needs R == P, and every other verdict is Err already
-    if (hdr && ge_is_small_order(P)) pre |= 16u;
-    ge_p3_to_p2(P2, P);
-    bits = pre << 8;
-  }
-  __syncthreads();
-  LAT_MARK(wave, 4)
-  if (wave == 0) {
     if (!(bits & COA_CST_UNCACHED)) {
       const uint32_t pre = bits >> 8;
-      ge_p3 R;
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        R.X.v[i] = r_lds[i];
-        R.Y.v[i] = r_lds[8 + i];
-      }
-      fe_set(R.Z, 1);
-      const bool r_ok = r_lds[16] != 0, small_r = (pre & 16) != 0;
-      const bool eq = ge_p2_eq_p3(P2, R);
+      const bool r_ok = (res & 1u) != 0, eq = (res & 2u) != 0, small_r = (pre & 16) != 0;
       const bool s_ok = !(pre & 1), a_ok = !(pre & 2), small_a = (pre & 4) != 0, tfree = !(pre & 8);
       if (hdr) {
         bits = (s_ok && a_ok && r_ok && !small_a && !small_r && eq) ? 0u : COA_CST_BAD_HEADER_SIG;
@@ -674,9 +540,130 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
         bits = (eq && tfree) ? 0u : COA_CST_VOTES_INCONCLUSIVE;
       }
     }
-    LAT_MARK(0, 5)
+    LAT_MARK(1, 5)
     if (lane == 0) lat_block_done(a, c, bits);
+    return;
   }
+  // one comb term per lane (lanes 0..31; the upper half sums a copy),
+  // [s]B on wave 2 from B's comb, [k](-A) on wave 0 from the key's comb
+  uint32_t bits = 0;
+  ge_p3 P;
+  uint32_t dg[8];
+  const uint32_t* tab = a.comb;
+  int slot = 0;
+  uint32_t pre = 0;
+  if (wave == 2) {
+    load8u(dg, sig + 8);
+  } else {
+    uint32_t pk[8], sw[8], msg[8];
+    load8u(pk, sel_ptr(hdr, a.origins + (uint64_t)c * 8, a.vpks + (uint64_t)vi * 8));
+    load8u(sw, sig + 8);
+    load8u(msg, a.ids + (uint64_t)c * 8);
+    slot = key_lookup_u(a.keys, a.nk, pk);
+    if (slot < 0) {
+      bits = COA_CST_UNCACHED;
+      slot = 0;
+    } else {
+      uint64_t st[8];
+      uint32_t h[16];
+      if (!hdr) {  // Certificate::digest on the scalar unit
+        uint32_t in[18];
+        const uint64_t rd = uni64(a.rounds[c]);
+#pragma unroll
+        for (int i = 0; i < 8; i++) in[i] = msg[i];
+        in[8] = (uint32_t)rd;
+        in[9] = (uint32_t)(rd >> 32);
+        load8u(in + 10, a.origins + (uint64_t)c * 8);
+        coa_sha::hash_words<18>(st, in);
+        coa_sha::state_to_le_words(h, st);
+#pragma unroll
+        for (int i = 0; i < 8; i++) msg[i] = h[i];
+      }
+      uint32_t in[24];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        in[i] = rw[i];
+        in[8 + i] = pk[i];
+        in[16 + i] = msg[i];
+      }
+      coa_sha::hash_words<24>(st, in);
+      coa_sha::state_to_le_words(h, st);
+      sc k;
+      sc_reduce512(k, h);
+      const uint32_t kf = coa_sha::uni(a.kflags[slot]);
+      const bool s_ok = sc_is_canonical(sw);
+      const bool a_ok = (kf & COA_KEY_DECOMPRESSES) != 0;
+      pre = (s_ok ? 0u : 1u) | (a_ok ? 0u : 2u) | ((kf & COA_KEY_SMALL_ORDER) ? 4u : 0u) |
+            ((kf & COA_KEY_TORSION_FREE) ? 0u : 8u);
+#pragma unroll
+      for (int i = 0; i < 8; i++) dg[i] = k.v[i];
+      tab = a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS;
+    }
+  }
+  LAT_MARK(wave, 1)
+  if (bits & COA_CST_UNCACHED) {  // wave 0 only: nothing to compare
+    rcmp::skip(cmp, bits, lane == 0);
+    return;
+  }
+  add_const_word(dg, 0x80808080u);
+  const int j = lane & 31;
+  const int e = (int)byte_of(dg, j) - 128;
+  ge_niels q;
+  comb_select(q, tab, j, e);
+  ge_p1p1 t;
+  ge_p3_identity(P);
+  ge_madd(t, P, q);
+  ge_p1p1_to_p3(P, t);
+  LAT_MARK(wave, 2)
+#pragma unroll 1
+  for (int off = 16; off >= 1; off >>= 1) {
+    ge_p3 O;
+    shfl_fe<64>(O.X, P.X, off);
+    shfl_fe<64>(O.Y, P.Y, off);
+    shfl_fe<64>(O.Z, P.Z, off);
+    shfl_fe<64>(O.T, P.T, off);
+    ge_cached oc;
+    ge_p3_to_cached(oc, O);
+    ge_add(t, P, oc);
+    ge_p1p1_to_p3(P, t);
+  }
+  LAT_MARK(wave, 3)
+  if (wave == 2) {
+    if (lane == 0) {
+      const fe* f[4] = {&P.X, &P.Y, &P.Z, &P.T};
+#pragma unroll
+      for (int q4 = 0; q4 < 4; q4++)
+#pragma unroll
+        for (int i = 0; i < 8; i++) s_lds[q4 * 8 + i] = f[q4]->v[i];
+      __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return;
+  }
+  // wave 0: everything that needs only P while wave 1 is still decompressing
+  // R (the critical chain): P = [s]B + [k](-A) as soon as wave 2 has
+  // published [s]B, verify_strict's small-order test, the compare's P half
+#pragma unroll 1
+  while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+    __builtin_amdgcn_s_sleep(1);
+  {  // P = [s]B + [k](-A)
+    ge_p3 S;
+    fe* f[4] = {&S.X, &S.Y, &S.Z, &S.T};
+#pragma unroll
+    for (int q4 = 0; q4 < 4; q4++)
+#pragma unroll
+      for (int i = 0; i < 8; i++) f[q4]->v[i] = s_lds[q4 * 8 + i];
+    ge_cached sc4;
+    ge_p3_to_cached(sc4, S);
+    ge_add(t, P, sc4);
+    ge_p1p1_to_p3(P, t);
+  }
+  // verify_strict's small-order test of R, taken on P: an accepting verdict
+  // needs R == P, and every other verdict is Err already
+  if (hdr && ge_is_small_order(P)) pre |= 16u;
+  ge_p2 P2;
+  ge_p3_to_p2(P2, P);
+  rcmp::prepare(cmp, P2, rw, pre << 8, lane == 0);
+  LAT_MARK(0, 4)
 }
 
 __global__ void __launch_bounds__(192) k_cert_verify_lat(CertArgs a) { cert_lat_body(a); }

@@ -168,12 +168,27 @@ COA_DEV void fe_set(fe& r, uint32_t x) {
 #define COA_B8_IN(b) \
   "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]), "v"(b.v[7])
 
+// The rare second pass of a fold runs out of line: the common path falls
+// through the s_cbranch_vccnz (no taken branch, which a lone wave pays for in
+// issue cycles), and the rare block is assembled into subsection 1 of the
+// function's own text section (build.py compiles with -ffunction-sections),
+// after the function's code, from where it branches back.  A branch reaches
+// +-128 KiB, so a translation unit with a larger kernel defines
+// COA_RARE_INLINE and keeps the block inline (skipped by a taken branch).
+#ifndef COA_RARE_INLINE
+#define COA_RARE_BEGIN "s_cbranch_vccnz 2f\n1:\n\t.subsection 1\n2:\n\t"
+#define COA_RARE_END "s_branch 1b\n\t.subsection 0"
+#else
+#define COA_RARE_BEGIN "s_cbranch_vccz 1f\n\t"
+#define COA_RARE_END "1:"
+#endif
+
 // r = a + b (mod p), result < 2^256.  2^256 == 38: the carry out of word 7
 // becomes 38 added to word 0.  That add carries on only when word 0 was
 // within 38 of 2^32 (probability ~2^-26 per lane), so the propagation through
-// words 1..7 runs behind a wave-uniform branch (s_cbranch_vccz skips it when
-// no lane carried); a carry out of that second pass leaves words that wrapped
-// to values < 38, so its fold cannot carry.
+// words 1..7 runs only when some lane carried (a wave-uniform branch to the
+// out-of-line block, COA_RARE_BEGIN); a carry out of that second
+// pass leaves words that wrapped to values < 38, so its fold cannot carry.
 COA_DEV void fe_add(fe& r, const fe& a, const fe& b) {
   fe x = a;
   uint32_t t;
@@ -187,7 +202,7 @@ COA_DEV void fe_add(fe& r, const fe& a, const fe& b) {
       "v_addc_co_u32_e32 %7, vcc, %7, %16, vcc\n\t"
       "v_cndmask_b32_e64 %8, 0, 38, vcc\n\t"
       "v_add_co_u32_e32 %0, vcc, %0, %8\n\t"
-      "s_cbranch_vccz 1f\n\t"
+      COA_RARE_BEGIN
       "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
       "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
       "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
@@ -196,8 +211,8 @@ COA_DEV void fe_add(fe& r, const fe& a, const fe& b) {
       "v_addc_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
       "v_addc_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
       "v_cndmask_b32_e64 %8, 0, 38, vcc\n\t"
-      "v_add_u32_e32 %0, %0, %8\n"
-      "1:"
+      "v_add_u32_e32 %0, %0, %8\n\t"
+      COA_RARE_END
       : COA_R8_INOUT(x), "=&v"(t)
       : COA_B8_IN(b)
       : "vcc");
@@ -220,7 +235,7 @@ COA_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
       "v_subb_co_u32_e32 %7, vcc, %7, %16, vcc\n\t"
       "v_cndmask_b32_e64 %8, 0, 38, vcc\n\t"
       "v_sub_co_u32_e32 %0, vcc, %0, %8\n\t"
-      "s_cbranch_vccz 1f\n\t"
+      COA_RARE_BEGIN
       "v_subbrev_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
       "v_subbrev_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
       "v_subbrev_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
@@ -229,8 +244,8 @@ COA_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
       "v_subbrev_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
       "v_subbrev_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
       "v_cndmask_b32_e64 %8, 0, 38, vcc\n\t"
-      "v_sub_u32_e32 %0, %0, %8\n"
-      "1:"
+      "v_sub_u32_e32 %0, %0, %8\n\t"
+      COA_RARE_END
       : COA_R8_INOUT(x), "=&v"(t)
       : COA_B8_IN(b)
       : "vcc");
@@ -268,8 +283,8 @@ COA_DEV void fe_neg(fe& r, const fe& a) {
 // nothing to pad); one VCC chain then adds the high words one limb up, and
 // the top word (< 40) is folded as 38 into word 0.  That add carries only
 // when word 0 was within 1,482 of 2^32 (~2^-21 per lane), so the
-// propagation through words 1..7 sits behind a wave-uniform s_cbranch_vccz
-// (skipped unless some lane carried); its own carry out leaves words that
+// propagation through words 1..7 runs out of line, only when some lane
+// carried (COA_RARE_BEGIN); its own carry out leaves words that
 // wrapped to zero, so the 38 it adds to word 0 cannot carry.
 COA_DEV void fe_reduce512(fe& r, const uint32_t* t) {
   uint32_t lo[8], hi[8];
@@ -290,7 +305,7 @@ COA_DEV void fe_reduce512(fe& r, const uint32_t* t) {
       "v_addc_co_u32_e32 %8, vcc, 0, %24, vcc\n\t"
       "v_mul_u32_u24_e32 %8, 38, %8\n\t"
       "v_add_co_u32_e32 %0, vcc, %9, %8\n\t"
-      "s_cbranch_vccz 1f\n\t"
+      COA_RARE_BEGIN
       "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
       "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
       "v_addc_co_u32_e32 %3, vcc, 0, %3, vcc\n\t"
@@ -299,8 +314,8 @@ COA_DEV void fe_reduce512(fe& r, const uint32_t* t) {
       "v_addc_co_u32_e32 %6, vcc, 0, %6, vcc\n\t"
       "v_addc_co_u32_e32 %7, vcc, 0, %7, vcc\n\t"
       "v_cndmask_b32_e64 %8, 0, 38, vcc\n\t"
-      "v_add_u32_e32 %0, %0, %8\n"
-      "1:"
+      "v_add_u32_e32 %0, %0, %8\n\t"
+      COA_RARE_END
       : "=&v"(r.v[0]), "=&v"(r.v[1]), "=&v"(r.v[2]), "=&v"(r.v[3]), "=&v"(r.v[4]), "=&v"(r.v[5]), "=&v"(r.v[6]),
         "=&v"(r.v[7]), "=&v"(w)
       : "v"(lo[0]), "v"(lo[1]), "v"(lo[2]), "v"(lo[3]), "v"(lo[4]), "v"(lo[5]), "v"(lo[6]), "v"(lo[7]), "v"(hi[0]),

@@ -61,12 +61,18 @@ COA_DEV uint32_t wrap_step(uint64_t& m, uint32_t r) {
 // congruent value < 2^256.  One pass leaves every lane below 2^32 + 2^14
 // (the carry from the lane below, or 38 times limb 7's), so a lane still has
 // a high word only when its low word was within 2^14 of 2^32: the uniform
-// branch to the rippling passes is almost never taken.
+// branch to the rippling passes is almost never taken.  It is marked so
+// (__builtin_expect): as a plain loop the common path took three branches
+// per product, which made a lone wave's row squaring 352 cycles instead of
+// 293 (tools/ubench_rows2.hip).
 COA_DEV uint32_t normalize(uint64_t m) {
   const uint32_t r = row_lane();
   wrap_step(m, r);
+  if (__builtin_expect(__any((uint32_t)(m >> 32) != 0u), 0)) {
 #pragma unroll 1
-  while (__any((uint32_t)(m >> 32) != 0u)) wrap_step(m, r);
+    do wrap_step(m, r);
+    while (__any((uint32_t)(m >> 32) != 0u));
+  }
   return (uint32_t)m;
 }
 // 4p and 8p in unnormalised limbs (limb 0: 4p_0 = 2^33 - 76, limbs 1..7:
@@ -137,9 +143,19 @@ COA_DEV uint32_t mul(uint32_t a, uint32_t b) {
   return normalize(m);
 }
 COA_DEV uint32_t sq(uint32_t a) { return mul(a, a); }
-COA_DEV uint32_t sqn(uint32_t a, int n) {
+// a^(2^N): four squarings per loop trip (one loop branch per four: 293 ->
+// ~278 cycles per squaring, tools/ubench_rows2.hip)
+template <int N>
+COA_DEV uint32_t sqn(uint32_t a) {
 #pragma unroll 1
-  for (int i = 0; i < n; i++) a = mul(a, a);
+  for (int i = 0; i < N / 4; i++) {
+    a = mul(a, a);
+    a = mul(a, a);
+    a = mul(a, a);
+    a = mul(a, a);
+  }
+#pragma unroll
+  for (int i = 0; i < N % 4; i++) a = mul(a, a);
   return a;
 }
 
@@ -165,26 +181,26 @@ COA_DEV void to_fe(fe& r, uint32_t x) {  // every lane of the row gets the row's
 // coa_fe.h fe_pow_chain on rows.
 COA_DEV uint32_t pow_chain(uint32_t& z11, uint32_t z) {
   const uint32_t z2 = sq(z);
-  const uint32_t z9 = mul(sqn(z2, 2), z);
+  const uint32_t z9 = mul(sqn<2>(z2), z);
   z11 = mul(z9, z2);
   const uint32_t z_5_0 = mul(sq(z11), z9);
-  const uint32_t z_10_0 = mul(sqn(z_5_0, 5), z_5_0);
-  const uint32_t z_20_0 = mul(sqn(z_10_0, 10), z_10_0);
-  const uint32_t z_40_0 = mul(sqn(z_20_0, 20), z_20_0);
-  const uint32_t z_50_0 = mul(sqn(z_40_0, 10), z_10_0);
-  const uint32_t z_100_0 = mul(sqn(z_50_0, 50), z_50_0);
-  const uint32_t z_200_0 = mul(sqn(z_100_0, 100), z_100_0);
-  return mul(sqn(z_200_0, 50), z_50_0);  // 2^250 - 1
+  const uint32_t z_10_0 = mul(sqn<5>(z_5_0), z_5_0);
+  const uint32_t z_20_0 = mul(sqn<10>(z_10_0), z_10_0);
+  const uint32_t z_40_0 = mul(sqn<20>(z_20_0), z_20_0);
+  const uint32_t z_50_0 = mul(sqn<10>(z_40_0), z_10_0);
+  const uint32_t z_100_0 = mul(sqn<50>(z_50_0), z_50_0);
+  const uint32_t z_200_0 = mul(sqn<100>(z_100_0), z_100_0);
+  return mul(sqn<50>(z_200_0), z_50_0);  // 2^250 - 1
 }
 COA_DEV uint32_t pow_p58(uint32_t z) {
   uint32_t z11;
   const uint32_t t = pow_chain(z11, z);
-  return mul(sqn(t, 2), z);
+  return mul(sqn<2>(t), z);
 }
 COA_DEV uint32_t invert(uint32_t z) {
   uint32_t z11;
   const uint32_t t = pow_chain(z11, z);
-  return mul(sqn(t, 5), z11);
+  return mul(sqn<5>(t), z11);
 }
 
 }  // namespace fw

@@ -681,11 +681,15 @@ hipError_t coa_launch_verify_split(const uint8_t* pks, const uint8_t* sigs, cons
   static const uint32_t pre_b = block_env("COA_PRE_BLOCK"), main_b = block_env("COA_MAIN_BLOCK");
   const uint32_t blocks = (n + pre_b - 1) / pre_b;
   const int aligned = ((msg_len & 3) == 0) && (((uintptr_t)msgs & 3) == 0);
-  // COA_PRE_PRIO=0: the hash/halving role at the default wave priority (A/B)
-  // COA_PRE_DIAG=2 / 4: skip the decompression / hash roles (timing only;
-  // verdicts are then meaningless)
-  static const int prio = (getenv("COA_PRE_PRIO") && atoi(getenv("COA_PRE_PRIO")) == 0 ? 0 : 1) |
-                          (getenv("COA_PRE_DIAG") ? atoi(getenv("COA_PRE_DIAG")) & 6 : 0);
+  // COA_PRE_PRIO=0: the hash/halving role at the default wave priority (A/B).
+  // A library compiled with -DCOA_PRE_DIAG_BUILD also reads COA_PRE_DIAG=2 / 4:
+  // skip the decompression / hash roles (role timing only, tools/pre_roles.sh;
+  // verdicts are then meaningless, so release builds cannot reach it).
+  static const int prio = (getenv("COA_PRE_PRIO") && atoi(getenv("COA_PRE_PRIO")) == 0 ? 0 : 1)
+#ifdef COA_PRE_DIAG_BUILD
+                          | (getenv("COA_PRE_DIAG") ? atoi(getenv("COA_PRE_DIAG")) & 6 : 0)
+#endif
+      ;
   hipLaunchKernelGGL(k_pre_halve<3>, dim3(3 * blocks), dim3(pre_b), 0, s, pks, sigs, msgs, msg_len, aligned, kbuf, n,
                      rec, flags, scratch, ebp, comb, wcomb, blocks, prio);
   hipError_t e = hipGetLastError();

@@ -16,8 +16,10 @@
 //             radix-256 comb: one term per lane, summed by a 5-level butterfly
 //     wave 2  [s]B from B's comb the same way (needs no hash, runs meanwhile)
 //     wave 1  R's decompression, the power chain on the rows
-//     then wave 0: P = [s]B + [k](-A), verify_strict's small-order test of R
-//     taken on P (an accepting verdict needs R == P), P == R projectively.
+//     meanwhile wave 0: P = [s]B + [k](-A), verify_strict's small-order test
+//     of R taken on P (an accepting verdict needs R == P), and the half of
+//     the compare that needs only P; wave 1 finishes decompression, compare
+//     and verdict in two row products after its chain (coa_rcmp.h).
 //   key not registered (the halved-scalar check of coa_halved.hip):
 //     wave 0  k, the halving (c, d) with c == d k (mod 8l), e = d s mod l
 //     wave 3  A's decompression (rows), small-order test, table j(-A), j <= 8
@@ -28,6 +30,8 @@
 // Both verdicts are dalek's bit for bit: the cached one by the same argument
 // as k_cert_verify_lat's header job, the uncached one by the halving argument
 // of coa_halved.hip (Q == [d]P exactly, d odd).
+// kernels here exceed the +-128 KiB reach of an out-of-line fold (coa_fe.h)
+#define COA_RARE_INLINE
 #include "coa_latency.h"
 
 #include "coa_fe.h"
@@ -37,6 +41,7 @@
 #include "coa_halved.h"
 #include "coa_committee.h"
 #include "coa_keycache.h"
+#include "coa_rcmp.h"
 #include "coa_sc.h"
 #include "coa_sha512.h"
 #include "coa_smul.h"
@@ -198,7 +203,6 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
   __shared__ uint32_t sh_ok[4];        // per wave: decompression ok and not small order
   __shared__ uint32_t sh_pt[3][32];    // points handed to wave 0
   __shared__ uint32_t sh_tab[2][8 * 32];  // j(-A), j(-R) in cached form (uncached path)
-  __shared__ uint32_t sh_r[17];        // R (X, Y) and its decompression verdict (cached path)
   const uint32_t wave = coa_sha::uni(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t item = blockIdx.x;
@@ -213,22 +217,18 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
 
   if (slot >= 0) {  // ------------------------------------------ cached key
     __shared__ uint32_t s_ready;  // wave 2 published [s]B
-    if (threadIdx.x == 0) s_ready = 0;
+    __shared__ rcmp::Shared cmp;  // wave 0's half of the compare, for wave 1
+    if (threadIdx.x == 0) {
+      s_ready = 0;
+      cmp.ready = 0;
+    }
     __syncthreads();
     ge_p3 P;
-    ge_p2 P2;
-    uint32_t pre = 0;
-    if (wave == 1) {
-      ge_p3 R;
-      const bool ok = ge_decompress<true>(R, rw);
-      if (lane == 0) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          sh_r[i] = R.X.v[i];
-          sh_r[8 + i] = R.Y.v[i];
-        }
-        sh_r[16] = ok;
-      }
+    if (wave == 1) {  // R's decompression on the rows, the compare, the verdict
+      uint32_t pre = 0;
+      const uint32_t res = rcmp::decompress_eq(cmp, rw, pre);
+      if (lane == 0) publish(a, item, pre == 0 && res == 3u);
+      VMARK(3)
     } else if (wave == 2) {
       uint32_t dg[8];
 #pragma unroll
@@ -252,14 +252,14 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
       sc k;
       sc_reduce512(k, h);
       const uint32_t kf = coa_sha::uni(a.kflags[slot]);
-      pre = (sc_is_canonical(sw) ? 0u : 1u) | ((kf & COA_KEY_DECOMPRESSES) ? 0u : 2u) |
-            ((kf & COA_KEY_SMALL_ORDER) ? 4u : 0u);
+      uint32_t pre = (sc_is_canonical(sw) ? 0u : 1u) | ((kf & COA_KEY_DECOMPRESSES) ? 0u : 2u) |
+                     ((kf & COA_KEY_SMALL_ORDER) ? 4u : 0u);
       comb_butterfly(P, k.v, a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS, lane);
       // everything that needs only P while wave 1 still decompresses R (the
       // critical chain): P = [s]B + [k](-A) once wave 2 has published [s]B,
       // verify_strict's small-order test of R taken on P (an accepting
       // verdict needs R == P, every other verdict is Err already), the
-      // projective form
+      // compare's P half
 #pragma unroll 1
       while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
         __builtin_amdgcn_s_sleep(1);
@@ -271,23 +271,11 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
       ge_add(t, P, sc4);
       ge_p1p1_to_p3(P, t);
       if (ge_is_small_order(P)) pre |= 8u;
+      ge_p2 P2;
       ge_p3_to_p2(P2, P);
+      rcmp::prepare(cmp, P2, rw, pre, lane == 0);
     }
     VMARK(1)
-    __syncthreads();
-    VMARK(2)
-    if (wave == 0) {
-      ge_p3 R;
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        R.X.v[i] = sh_r[i];
-        R.Y.v[i] = sh_r[8 + i];
-      }
-      fe_set(R.Z, 1);
-      const bool ok = pre == 0 && sh_r[16] != 0 && ge_p2_eq_p3(P2, R);
-      if (lane == 0) publish(a, item, ok);
-      VMARK(3)
-    }
     return;
   }
 

@@ -1006,7 +1006,9 @@ int certificates_impl(const CertIn& in, size_t n, uint64_t rng_seed, uint8_t* st
       rlc.push_back(i);
     }
   }
-  const uint64_t seed = rng_seed ? rng_seed : os_entropy_seed();
+  // weights for the exact re-decision only: OS entropy is a syscall, and the
+  // common call (every certificate decided by the cached kernel) needs none
+  const uint64_t seed = rng_seed || (uncached.empty() && rlc.empty()) ? rng_seed : os_entropy_seed();
   rc = cert_resolve(in, uncached, true, seed, st.data());
   if (rc != COA_OK) return rc;
   rc = cert_resolve(in, rlc, false, seed, st.data());
