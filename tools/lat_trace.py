@@ -4,8 +4,10 @@ signature job, from a build with -DCOA_LAT_TRACE.
   python tools/lat_trace.py build     (CPU: writes build/lat_trace/libcoa_verify.so)
   python tools/lat_trace.py run       (GPU: one C1-sized certificate, prints per-wave marks)
 
-Marks per wave: 0 start, 1 hash/decompression done, 2 comb term loaded,
-3 butterfly done, 4 after the hand-off barrier, 5 verdict (wave 0)."""
+Marks: wave 0: 0 start, 1 hash done, 2 comb term loaded, 3 butterfly done,
+4 P's half of the compare published; wave 2: 0 start, 1 (no hash), 2 comb
+term loaded, 3 butterfly done; wave 1: 0 start, 1 power chain done, 2 compare
+done (after waiting for wave 0), 5 verdict."""
 import json
 import os
 import subprocess

@@ -526,8 +526,8 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
   LAT_MARK(wave, 0)
   if (wave == 1) {  // R's decompression on the wave's DPP rows, the compare, the verdict
     uint32_t bits = 0;
-    const uint32_t res = rcmp::decompress_eq(cmp, rw, bits);
-    LAT_MARK(1, 1)
+    const uint32_t res = rcmp::decompress_eq(cmp, rw, bits, [&] { LAT_MARK(1, 1) });
+    LAT_MARK(1, 2)
     if (!(bits & COA_CST_UNCACHED)) {
       const uint32_t pre = bits >> 8;
       const bool r_ok = (res & 1u) != 0, eq = (res & 2u) != 0, small_r = (pre & 16) != 0;
@@ -547,7 +547,6 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
   // one comb term per lane (lanes 0..31; the upper half sums a copy),
   // [s]B on wave 2 from B's comb, [k](-A) on wave 0 from the key's comb
   uint32_t bits = 0;
-  ge_p3 P;
   uint32_t dg[8];
   const uint32_t* tab = a.comb;
   int slot = 0;
@@ -605,64 +604,33 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
     rcmp::skip(cmp, bits, lane == 0);
     return;
   }
-  add_const_word(dg, 0x80808080u);
-  const int j = lane & 31;
-  const int e = (int)byte_of(dg, j) - 128;
-  ge_niels q;
-  comb_select(q, tab, j, e);
-  ge_p1p1 t;
-  ge_p3_identity(P);
-  ge_madd(t, P, q);
-  ge_p1p1_to_p3(P, t);
-  LAT_MARK(wave, 2)
-#pragma unroll 1
-  for (int off = 16; off >= 1; off >>= 1) {
-    ge_p3 O;
-    shfl_fe<64>(O.X, P.X, off);
-    shfl_fe<64>(O.Y, P.Y, off);
-    shfl_fe<64>(O.Z, P.Z, off);
-    shfl_fe<64>(O.T, P.T, off);
-    ge_cached oc;
-    ge_p3_to_cached(oc, O);
-    ge_add(t, P, oc);
-    ge_p1p1_to_p3(P, t);
-  }
+  rp::P1 P;  // row form (coa_ge_rows.h)
+  rcmp::comb_sum_rows(P, dg, tab, lane);
   LAT_MARK(wave, 3)
   if (wave == 2) {
-    if (lane == 0) {
-      const fe* f[4] = {&P.X, &P.Y, &P.Z, &P.T};
-#pragma unroll
-      for (int q4 = 0; q4 < 4; q4++)
-#pragma unroll
-        for (int i = 0; i < 8; i++) s_lds[q4 * 8 + i] = f[q4]->v[i];
-      __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane < 8) {
+      s_lds[lane] = P.X;
+      s_lds[8 + lane] = P.Y;
+      s_lds[16 + lane] = P.Z;
+      s_lds[24 + lane] = P.T;
     }
+    if (lane == 0) __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     return;
   }
   // wave 0: everything that needs only P while wave 1 is still decompressing
   // R (the critical chain): P = [s]B + [k](-A) as soon as wave 2 has
-  // published [s]B, verify_strict's small-order test, the compare's P half
+  // published [s]B, verify_strict's small-order test of R taken on P (an
+  // accepting verdict needs R == P; headers only), the compare's P half
 #pragma unroll 1
   while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
     __builtin_amdgcn_s_sleep(1);
-  {  // P = [s]B + [k](-A)
-    ge_p3 S;
-    fe* f[4] = {&S.X, &S.Y, &S.Z, &S.T};
-#pragma unroll
-    for (int q4 = 0; q4 < 4; q4++)
-#pragma unroll
-      for (int i = 0; i < 8; i++) f[q4]->v[i] = s_lds[q4 * 8 + i];
-    ge_cached sc4;
-    ge_p3_to_cached(sc4, S);
-    ge_add(t, P, sc4);
-    ge_p1p1_to_p3(P, t);
-  }
-  // verify_strict's small-order test of R, taken on P: an accepting verdict
-  // needs R == P, and every other verdict is Err already
-  if (hdr && ge_is_small_order(P)) pre |= 16u;
-  ge_p2 P2;
-  ge_p3_to_p2(P2, P);
-  rcmp::prepare(cmp, P2, rw, pre << 8, lane == 0);
+  rp::P1 S;
+  S.X = rp::ld(s_lds);
+  S.Y = rp::ld(s_lds + 8);
+  S.Z = rp::ld(s_lds + 16);
+  S.T = rp::ld(s_lds + 24);
+  rcmp::add_rows(P, P, S);
+  rcmp::prepare_rows(cmp, P, rw, pre << 8, hdr ? (16u << 8) : 0u, lane == 0);
   LAT_MARK(0, 4)
 }
 

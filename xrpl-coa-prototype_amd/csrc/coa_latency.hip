@@ -223,21 +223,24 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
       cmp.ready = 0;
     }
     __syncthreads();
-    ge_p3 P;
     if (wave == 1) {  // R's decompression on the rows, the compare, the verdict
       uint32_t pre = 0;
       const uint32_t res = rcmp::decompress_eq(cmp, rw, pre);
       if (lane == 0) publish(a, item, pre == 0 && res == 3u);
       VMARK(3)
-    } else if (wave == 2) {
+    } else if (wave == 2) {  // [s]B on the rows, published in row-limb layout
       uint32_t dg[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) dg[i] = sw[i];
-      comb_butterfly(P, dg, a.comb, lane);
-      if (lane == 0) {
-        lds_put_p3(sh_pt[0], P);
-        __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      rp::P1 S;
+      rcmp::comb_sum_rows(S, dg, a.comb, lane);
+      if (lane < 8) {
+        sh_pt[0][lane] = S.X;
+        sh_pt[0][8 + lane] = S.Y;
+        sh_pt[0][16 + lane] = S.Z;
+        sh_pt[0][24 + lane] = S.T;
       }
+      if (lane == 0) __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else if (wave == 0) {
       uint64_t st[8];
       uint32_t h[16], w[24];
@@ -252,9 +255,10 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
       sc k;
       sc_reduce512(k, h);
       const uint32_t kf = coa_sha::uni(a.kflags[slot]);
-      uint32_t pre = (sc_is_canonical(sw) ? 0u : 1u) | ((kf & COA_KEY_DECOMPRESSES) ? 0u : 2u) |
-                     ((kf & COA_KEY_SMALL_ORDER) ? 4u : 0u);
-      comb_butterfly(P, k.v, a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS, lane);
+      const uint32_t pre = (sc_is_canonical(sw) ? 0u : 1u) | ((kf & COA_KEY_DECOMPRESSES) ? 0u : 2u) |
+                           ((kf & COA_KEY_SMALL_ORDER) ? 4u : 0u);
+      rp::P1 P;
+      rcmp::comb_sum_rows(P, k.v, a.ktabs + (uint64_t)slot * COA_KEY_TAB_DWORDS, lane);
       // everything that needs only P while wave 1 still decompresses R (the
       // critical chain): P = [s]B + [k](-A) once wave 2 has published [s]B,
       // verify_strict's small-order test of R taken on P (an accepting
@@ -263,17 +267,13 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
 #pragma unroll 1
       while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
         __builtin_amdgcn_s_sleep(1);
-      ge_p3 S;
-      lds_get_p3(S, sh_pt[0]);
-      ge_cached sc4;
-      ge_p3_to_cached(sc4, S);
-      ge_p1p1 t;
-      ge_add(t, P, sc4);
-      ge_p1p1_to_p3(P, t);
-      if (ge_is_small_order(P)) pre |= 8u;
-      ge_p2 P2;
-      ge_p3_to_p2(P2, P);
-      rcmp::prepare(cmp, P2, rw, pre, lane == 0);
+      rp::P1 S;
+      S.X = rp::ld(sh_pt[0]);
+      S.Y = rp::ld(sh_pt[0] + 8);
+      S.Z = rp::ld(sh_pt[0] + 16);
+      S.T = rp::ld(sh_pt[0] + 24);
+      rcmp::add_rows(P, P, S);
+      rcmp::prepare_rows(cmp, P, rw, pre, 8u, lane == 0);
     }
     VMARK(1)
     return;
