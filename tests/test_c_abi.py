@@ -20,10 +20,14 @@ def build_harness():
 
     lib = build.build()
     libdir = os.path.dirname(lib)
+    # built under a per-process name and renamed into place, so concurrent
+    # test processes never write an executable another one is running
+    tmp = f"{OUT}.{os.getpid()}"
     cmd = ["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-pedantic", "-O1", "-I", os.path.join(ROOT, "include"),
-           SRC, "-o", OUT, "-L", libdir, "-lcoa_verify", f"-Wl,-rpath,{libdir}", "-L/opt/rocm/lib",
+           SRC, "-o", tmp, "-L", libdir, "-lcoa_verify", f"-Wl,-rpath,{libdir}", "-L/opt/rocm/lib",
            "-Wl,-rpath,/opt/rocm/lib"]
     subprocess.run(cmd, check=True, capture_output=True, text=True)
+    os.replace(tmp, OUT)
     return OUT
 
 
