@@ -58,10 +58,34 @@ __global__ void __launch_bounds__(256) k(fe* x, int n) {
     }
     if (V == 3 || V == 4) fe_mul2(a, a, b, c, c, b);
     if (V == 4) fe_mul2(e, e, b, f, f, b);
+    if (V == 5) {
+      fe x[4] = {a, c, e, f}, y[4] = {b, b, b, b};
+      fe_mul_n<4>(x, x, y);
+      a = x[0]; c = x[1]; e = x[2]; f = x[3];
+    }
+    if (V == 6) fe_sq(a, a);
+    if (V == 7 || V == 9) {
+      fe_sq(a, a);
+      fe_sq(c, c);
+    }
+    if (V == 9) {
+      fe_sq(e, e);
+      fe_sq(f, f);
+    }
+    if (V == 8) {
+      fe x[2] = {a, c};
+      fe_sq_n<2>(x, x);
+      a = x[0]; c = x[1];
+    }
+    if (V == 10) {
+      fe x[4] = {a, c, e, f};
+      fe_sq_n<4>(x, x);
+      a = x[0]; c = x[1]; e = x[2]; f = x[3];
+    }
   }
-  if (V >= 1) {
+  if (V >= 1 && V != 6) {
     fe_add(a, a, c);
-    if (V == 2 || V == 4) {
+    if (V == 2 || V == 4 || V == 5 || V == 9 || V == 10) {
       fe_add(a, a, e);
       fe_add(a, a, f);
     }
@@ -84,22 +108,25 @@ int main() {
   hipMalloc(&d, sizeof(fe) * nthreads);
   ref = (fe*)malloc(sizeof(fe) * nthreads);
   fe* got = (fe*)malloc(sizeof(fe) * nthreads);
-  const int NV = 5;
-  void (*ks[NV])(fe*, int) = {k<0>, k<1>, k<2>, k<3>, k<4>};
-  const char* names[NV] = {"1 chain", "2 chains", "4 chains", "2 by fe_mul2", "4 by 2x fe_mul2"};
-  const int per[NV] = {1, 2, 4, 2, 4};
+  const int NV = 11;
+  void (*ks[NV])(fe*, int) = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>, k<6>, k<7>, k<8>, k<9>, k<10>};
+  const char* names[NV] = {"mul 1 chain", "mul 2 chains", "mul 4 chains", "mul 2 by fe_mul2", "mul 4 by 2x fe_mul2",
+                           "mul 4 by mul_n<4>", "sq 1 chain", "sq 2 chains", "sq 2 by sq_n<2>", "sq 4 chains",
+                           "sq 4 by sq_n<4>"};
+  const int per[NV] = {1, 2, 4, 2, 4, 4, 1, 2, 2, 4, 4};
+  const int cmp[NV] = {-1, -1, -1, 1, 2, 2, -1, -1, 7, -1, 9};  // variant that must agree
   // correctness: variants 1/3 and 2/4 must agree with each other
   for (int v = 0; v < NV; v++) {
     hipMemcpy(d, h0, sizeof(fe) * nthreads, hipMemcpyHostToDevice);
     hipLaunchKernelGGL(ks[v], dim3(nthreads / 256), dim3(256), 0, 0, d, 5);
-    hipMemcpy(v == 1 || v == 2 ? ref : got, d, sizeof(fe) * nthreads, hipMemcpyDeviceToHost);
-    if (v == 3 || v == 4) {
+    hipMemcpy(got, d, sizeof(fe) * nthreads, hipMemcpyDeviceToHost);
+    if (cmp[v] >= 0) {
       hipMemcpy(d, h0, sizeof(fe) * nthreads, hipMemcpyHostToDevice);
-      hipLaunchKernelGGL(ks[v - 2], dim3(nthreads / 256), dim3(256), 0, 0, d, 5);
+      hipLaunchKernelGGL(ks[cmp[v]], dim3(nthreads / 256), dim3(256), 0, 0, d, 5);
       hipMemcpy(ref, d, sizeof(fe) * nthreads, hipMemcpyDeviceToHost);
       int bad = 0;
       for (int i = 0; i < nthreads; i++) bad += memcmp(&ref[i], &got[i], sizeof(fe)) != 0;
-      printf("%-16s vs %-10s: %d lanes differ\n", names[v], names[v - 2], bad);
+      printf("%-20s vs %-14s: %d lanes differ\n", names[v], names[cmp[v]], bad);
       if (bad) return 1;
     }
   }
@@ -124,7 +151,7 @@ int main() {
         if (ms < best) best = ms;
       }
       const double ops = (double)blocks * 256 * N * per[v];
-      printf("%d wave/SIMD %-16s %7.1f cyc per fe_mul per SIMD @2.4GHz\n", waves, names[v],
+      printf("%d wave/SIMD %-20s %7.1f cyc per op per SIMD @2.4GHz\n", waves, names[v],
              (best * 1e-3) * 2.4e9 * 1024 / (ops / 64));
     }
   }

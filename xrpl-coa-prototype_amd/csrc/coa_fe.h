@@ -336,11 +336,8 @@ COA_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
 // carry chain), then the 8 squares added with one unpadded VCC chain (44 mads
 // vs 72 for fe_mul).  The doubled cross sum is < 2^511, so the shift loses
 // nothing and the final chain cannot carry out.
-COA_DEV void fe_sq(fe& r, const fe& a) {
-  uint32_t t[16];
-  t[0] = 0;
-  uint64_t acc = 0;
-  mul_cols<true>(t, acc, a, a);
+// The squaring after its cross columns: t[1..13] and acc hold the cross sum.
+COA_DEV void sq_finish(fe& r, uint32_t* t, uint64_t acc, const fe& a) {
   t[14] = (uint32_t)acc;
   t[15] = (uint32_t)(acc >> 32);
   uint32_t u[16];
@@ -376,6 +373,68 @@ COA_DEV void fe_sq(fe& r, const fe& a) {
         "v"(d[10]), "v"(d[11]), "v"(d[12]), "v"(d[13]), "v"(d[14]), "v"(d[15])
       : "vcc");
   fe_reduce512(r, u);
+}
+
+COA_DEV void fe_sq(fe& r, const fe& a) {
+  uint32_t t[16];
+  t[0] = 0;
+  uint64_t acc = 0;
+  mul_cols<true>(t, acc, a, a);
+  sq_finish(r, t, acc, a);
+}
+
+// ------------------------------------------- interleaved independent products
+// N independent products (or squarings), issued column by column: column K
+// of product 0, of product 1, ... then column K + 1.  Inside one column the
+// mads are a dependency chain through the accumulator; a wave alone on its
+// SIMD (the C2 occupancy of k_verify_main) otherwise waits on that chain at
+// every column boundary.  tools/ubench_ilp.hip, one wave per SIMD: 888
+// cycles per product as one chain, 802 with two interleaved
+// (profiles/r02_ubench_ilp.txt).
+template <bool SQ, int N, int K = SQ ? 1 : 0>
+COA_DEV void mul_cols_n(uint32_t (&t)[N][16], uint64_t (&acc)[N], const fe (&a)[N], const fe (&b)[N]) {
+  if constexpr (K < (SQ ? 14 : 15)) {
+    uint32_t c2[N];
+#pragma unroll
+    for (int q = 0; q < N; q++) mul_col<K, SQ>(acc[q], c2[q], a[q], SQ ? a[q] : b[q]);
+#pragma unroll
+    for (int q = 0; q < N; q++) {
+      t[q][K] = (uint32_t)acc[q];
+      acc[q] = (acc[q] >> 32) | ((uint64_t)c2[q] << 32);
+    }
+    mul_cols_n<SQ, N, K + 1>(t, acc, a, b);
+  }
+}
+
+// r[q] = a[q] * b[q]; the outputs are written after every input is read, so
+// they may alias the inputs.
+template <int N>
+COA_DEV void fe_mul_n(fe (&r)[N], const fe (&a)[N], const fe (&b)[N]) {
+  uint32_t t[N][16];
+  uint64_t acc[N];
+#pragma unroll
+  for (int q = 0; q < N; q++) acc[q] = 0;
+  mul_cols_n<false, N>(t, acc, a, b);
+#pragma unroll
+  for (int q = 0; q < N; q++) {
+    t[q][15] = (uint32_t)acc[q];
+    fe_reduce512(r[q], t[q]);
+  }
+}
+
+// r[q] = a[q]^2.
+template <int N>
+COA_DEV void fe_sq_n(fe (&r)[N], const fe (&a)[N]) {
+  uint32_t t[N][16];
+  uint64_t acc[N];
+#pragma unroll
+  for (int q = 0; q < N; q++) {
+    acc[q] = 0;
+    t[q][0] = 0;
+  }
+  mul_cols_n<true, N>(t, acc, a, a);
+#pragma unroll
+  for (int q = 0; q < N; q++) sq_finish(r[q], t[q], acc[q], a[q]);
 }
 
 

@@ -146,6 +146,56 @@ COA_DEV void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
   fe_sub(r.T, zz, c);
 }
 
+// The same formulas with their independent products interleaved column by
+// column (fe_mul_n / fe_sq_n): for a wave alone on its SIMD, where the
+// per-column dependency chains are exposed.  More live registers than the
+// plain forms (up to four 16-word column buffers).
+COA_DEV void ge_p1p1_to_p2_il(ge_p2& r, const ge_p1p1& p) {
+  const fe a[3] = {p.X, p.Y, p.Z}, b[3] = {p.T, p.Z, p.T};
+  fe o[3];
+  fe_mul_n<3>(o, a, b);
+  r.X = o[0];
+  r.Y = o[1];
+  r.Z = o[2];
+}
+COA_DEV void ge_p1p1_to_p3_il(ge_p3& r, const ge_p1p1& p) {
+  const fe a[4] = {p.X, p.Y, p.Z, p.X}, b[4] = {p.T, p.Z, p.T, p.Y};
+  fe o[4];
+  fe_mul_n<4>(o, a, b);
+  r.X = o[0];
+  r.Y = o[1];
+  r.Z = o[2];
+  r.T = o[3];
+}
+COA_DEV void ge_p2_dbl_il(ge_p1p1& r, const ge_p2& p) {
+  fe s[4];
+  s[0] = p.X;
+  s[1] = p.Y;
+  s[2] = p.Z;
+  fe_add(s[3], p.X, p.Y);
+  fe o[4];
+  fe_sq_n<4>(o, s);
+  fe_add(o[2], o[2], o[2]);
+  fe_add(r.Y, o[1], o[0]);
+  fe_sub(r.Z, o[1], o[0]);
+  fe_sub(r.X, o[3], r.Y);
+  fe_sub(r.T, o[2], r.Z);
+}
+COA_DEV void ge_add_il(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
+  fe a[4], o[4];
+  fe_add(a[0], p.Y, p.X);
+  fe_sub(a[1], p.Y, p.X);
+  a[2] = q.T2d;
+  a[3] = p.Z;
+  const fe b[4] = {q.YplusX, q.YminusX, p.T, q.Z};
+  fe_mul_n<4>(o, a, b);
+  fe_add(o[3], o[3], o[3]);
+  fe_sub(r.X, o[0], o[1]);
+  fe_add(r.Y, o[0], o[1]);
+  fe_add(r.Z, o[3], o[2]);
+  fe_sub(r.T, o[3], o[2]);
+}
+
 // Conditionally negate an addend: -(x, y) = (-x, y) swaps Y+X / Y-X and
 // negates the T term.
 COA_DEV void ge_cached_cneg(ge_cached& q, bool neg) {

@@ -472,19 +472,19 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
       if (pos != H - 1) {
 #pragma unroll 1
         for (int k = 0; k < 3; k++) {
-          ge_p2_dbl(t, acc2);
-          ge_p1p1_to_p2(acc2, t);
+          ge_p2_dbl_il(t, acc2);
+          ge_p1p1_to_p2_il(acc2, t);
         }
-        ge_p2_dbl(t, acc2);
-        ge_p1p1_to_p3(acc3, t);
+        ge_p2_dbl_il(t, acc2);
+        ge_p1p1_to_p3_il(acc3, t);
       }
       ge_cached q;
       tab2_select(q, scr, i, 0, dc);
-      ge_add(t, acc3, q);
-      ge_p1p1_to_p3(acc3, t);
+      ge_add_il(t, acc3, q);
+      ge_p1p1_to_p3_il(acc3, t);
       tab2_select(q, scr, i, 1, dneg ? -dd : dd);
-      ge_add(t, acc3, q);
-      if (pos != 0) ge_p1p1_to_p2(acc2, t);
+      ge_add_il(t, acc3, q);
+      if (pos != 0) ge_p1p1_to_p2_il(acc2, t);
     }
     ge_p1p1_to_p3(acc3, t);
     if (!ebp) {  // [e]B here, from the combs
