@@ -38,6 +38,64 @@ COA_DEV void fe_mul2(fe& r, const fe& a, const fe& b, fe& r2, const fe& c, const
   fe_reduce512(r, t);
   fe_reduce512(r2, u);
 }
+// Probe (not in the engine): two independent subtractions interleaved through
+// two SGPR carry pairs, as fe_addsub does for a + b / a - b.  Measured slower
+// than two plain fe_sub chains (profiles/r02_ubench_ilp.txt).
+COA_DEV void fe_sub2(fe& d1, const fe& a1, const fe& b1, fe& d2, const fe& a2, const fe& b2) {
+  fe x = a1, y = a2;
+  uint32_t t, u;
+  uint64_t c1, c2;
+  asm("v_sub_co_u32_e64 %0, %[c1], %0, %[p0]\n\t"
+      "v_sub_co_u32_e64 %8, %[c2], %8, %[q0]\n\t"
+      "v_subb_co_u32_e64 %1, %[c1], %1, %[p1], %[c1]\n\t"
+      "v_subb_co_u32_e64 %9, %[c2], %9, %[q1], %[c2]\n\t"
+      "v_subb_co_u32_e64 %2, %[c1], %2, %[p2], %[c1]\n\t"
+      "v_subb_co_u32_e64 %10, %[c2], %10, %[q2], %[c2]\n\t"
+      "v_subb_co_u32_e64 %3, %[c1], %3, %[p3], %[c1]\n\t"
+      "v_subb_co_u32_e64 %11, %[c2], %11, %[q3], %[c2]\n\t"
+      "v_subb_co_u32_e64 %4, %[c1], %4, %[p4], %[c1]\n\t"
+      "v_subb_co_u32_e64 %12, %[c2], %12, %[q4], %[c2]\n\t"
+      "v_subb_co_u32_e64 %5, %[c1], %5, %[p5], %[c1]\n\t"
+      "v_subb_co_u32_e64 %13, %[c2], %13, %[q5], %[c2]\n\t"
+      "v_subb_co_u32_e64 %6, %[c1], %6, %[p6], %[c1]\n\t"
+      "v_subb_co_u32_e64 %14, %[c2], %14, %[q6], %[c2]\n\t"
+      "v_subb_co_u32_e64 %7, %[c1], %7, %[p7], %[c1]\n\t"
+      "v_subb_co_u32_e64 %15, %[c2], %15, %[q7], %[c2]\n\t"
+      "v_cndmask_b32_e64 %[t], 0, 38, %[c1]\n\t"
+      "v_cndmask_b32_e64 %[u], 0, 38, %[c2]\n\t"
+      "v_sub_co_u32_e64 %0, %[c1], %0, %[t]\n\t"
+      "v_sub_co_u32_e64 %8, %[c2], %8, %[u]\n\t"
+      "s_or_b64 vcc, %[c1], %[c2]\n\t"
+      COA_RARE_BEGIN
+      "v_subbrev_co_u32_e64 %1, %[c1], 0, %1, %[c1]\n\t"
+      "v_subbrev_co_u32_e64 %9, %[c2], 0, %9, %[c2]\n\t"
+      "v_subbrev_co_u32_e64 %2, %[c1], 0, %2, %[c1]\n\t"
+      "v_subbrev_co_u32_e64 %10, %[c2], 0, %10, %[c2]\n\t"
+      "v_subbrev_co_u32_e64 %3, %[c1], 0, %3, %[c1]\n\t"
+      "v_subbrev_co_u32_e64 %11, %[c2], 0, %11, %[c2]\n\t"
+      "v_subbrev_co_u32_e64 %4, %[c1], 0, %4, %[c1]\n\t"
+      "v_subbrev_co_u32_e64 %12, %[c2], 0, %12, %[c2]\n\t"
+      "v_subbrev_co_u32_e64 %5, %[c1], 0, %5, %[c1]\n\t"
+      "v_subbrev_co_u32_e64 %13, %[c2], 0, %13, %[c2]\n\t"
+      "v_subbrev_co_u32_e64 %6, %[c1], 0, %6, %[c1]\n\t"
+      "v_subbrev_co_u32_e64 %14, %[c2], 0, %14, %[c2]\n\t"
+      "v_subbrev_co_u32_e64 %7, %[c1], 0, %7, %[c1]\n\t"
+      "v_subbrev_co_u32_e64 %15, %[c2], 0, %15, %[c2]\n\t"
+      "v_cndmask_b32_e64 %[t], 0, 38, %[c1]\n\t"
+      "v_cndmask_b32_e64 %[u], 0, 38, %[c2]\n\t"
+      "v_sub_u32_e32 %0, %0, %[t]\n\t"
+      "v_sub_u32_e32 %8, %8, %[u]\n\t"
+      COA_RARE_END
+      : COA_R8_INOUT(x), COA_R8_INOUT(y), [t] "=&v"(t), [u] "=&v"(u), [c1] "=&s"(c1), [c2] "=&s"(c2)
+      : [p0] "v"(b1.v[0]), [p1] "v"(b1.v[1]), [p2] "v"(b1.v[2]), [p3] "v"(b1.v[3]), [p4] "v"(b1.v[4]),
+        [p5] "v"(b1.v[5]), [p6] "v"(b1.v[6]), [p7] "v"(b1.v[7]), [q0] "v"(b2.v[0]), [q1] "v"(b2.v[1]),
+        [q2] "v"(b2.v[2]), [q3] "v"(b2.v[3]), [q4] "v"(b2.v[4]), [q5] "v"(b2.v[5]), [q6] "v"(b2.v[6]),
+        [q7] "v"(b2.v[7])
+      : "vcc", "scc");
+  d1 = x;
+  d2 = y;
+}
+
 }  // namespace
 
 // V: 0 one chain, 1 two chains, 2 four chains, 3 two chains by fe_mul2,
@@ -82,8 +140,25 @@ __global__ void __launch_bounds__(256) k(fe* x, int n) {
       fe_sq_n<4>(x, x);
       a = x[0]; c = x[1]; e = x[2]; f = x[3];
     }
+    if (V == 11) {
+      fe s, t;
+      fe_add(s, a, b);
+      fe_sub(t, a, b);
+      a = s;
+      b = t;
+    }
+    if (V == 12) fe_addsub(a, b, a, b);
+    if (V == 13) {
+      fe s, t;
+      fe_sub(s, a, b);
+      fe_sub(t, b, c);
+      a = s;
+      b = t;
+    }
+    if (V == 14) fe_sub2(a, a, b, b, b, c);
   }
-  if (V >= 1 && V != 6) {
+  if (V >= 11) fe_add(a, a, b);
+  if (V >= 1 && V != 6 && V < 11) {
     fe_add(a, a, c);
     if (V == 2 || V == 4 || V == 5 || V == 9 || V == 10) {
       fe_add(a, a, e);
@@ -104,17 +179,30 @@ int main() {
       s ^= s << 17;
       h0[i].v[j] = (uint32_t)s;
     }
+  for (int i = 0; i < 8192; i++) {
+    const int kind = i % 8;
+    for (int j = 0; j < 8; j++) {
+      uint32_t v = h0[i].v[j];
+      if (kind == 0) v = 0xffffffffu;
+      if (kind == 1) v = j == 0 ? 0xffffffedu - (i & 31) : (j == 7 ? 0x7fffffffu : 0xffffffffu);
+      if (kind == 2) v = j == 0 ? 0xffffffffu - (i & 63) : 0xffffffffu;
+      if (kind == 3) v = 0;
+      if (kind == 4) v = j == (i / 8) % 8 ? 0xffffffffu : 0;
+      if (kind == 5) v = j < 4 ? 0xffffffffu : v;
+      h0[i].v[j] = v;
+    }
+  }
   fe *d, *ref;
   hipMalloc(&d, sizeof(fe) * nthreads);
   ref = (fe*)malloc(sizeof(fe) * nthreads);
   fe* got = (fe*)malloc(sizeof(fe) * nthreads);
-  const int NV = 11;
-  void (*ks[NV])(fe*, int) = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>, k<6>, k<7>, k<8>, k<9>, k<10>};
+  const int NV = 15;
+  void (*ks[NV])(fe*, int) = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>, k<6>, k<7>, k<8>, k<9>, k<10>, k<11>, k<12>, k<13>, k<14>};
   const char* names[NV] = {"mul 1 chain", "mul 2 chains", "mul 4 chains", "mul 2 by fe_mul2", "mul 4 by 2x fe_mul2",
                            "mul 4 by mul_n<4>", "sq 1 chain", "sq 2 chains", "sq 2 by sq_n<2>", "sq 4 chains",
-                           "sq 4 by sq_n<4>"};
-  const int per[NV] = {1, 2, 4, 2, 4, 4, 1, 2, 2, 4, 4};
-  const int cmp[NV] = {-1, -1, -1, 1, 2, 2, -1, -1, 7, -1, 9};  // variant that must agree
+                           "sq 4 by sq_n<4>", "add+sub", "fe_addsub", "sub+sub", "fe_sub2"};
+  const int per[NV] = {1, 2, 4, 2, 4, 4, 1, 2, 2, 4, 4, 1, 1, 1, 1};
+  const int cmp[NV] = {-1, -1, -1, 1, 2, 2, -1, -1, 7, -1, 9, -1, 11, -1, 13};  // variant that must agree
   // correctness: variants 1/3 and 2/4 must agree with each other
   for (int v = 0; v < NV; v++) {
     hipMemcpy(d, h0, sizeof(fe) * nthreads, hipMemcpyHostToDevice);

@@ -271,6 +271,69 @@ COA_DEV void fe_fold_word(fe& r, uint32_t w) {
       : "vcc");
 }
 
+// s = a + b and d = a - b (mod p, results < 2^256) as two interleaved carry
+// chains: the sum's carries pass through one SGPR pair, the difference's
+// borrows through another (VOP3 forms), so each instruction's carry-in was
+// written two instructions earlier rather than by the one before it, which a
+// wave alone on its SIMD otherwise waits for.  Folds as in fe_add / fe_sub;
+// both second passes run in one out-of-line block, entered when either chain
+// carried (a chain that did not carry propagates zeros there).  The s_or_b64
+// that joins the two carry masks writes SCC, so SCC is declared clobbered: a
+// compiler-held SCC (a loop condition) live across the statement would
+// otherwise be lost -- without it k_verify_main never left its digit loop.
+COA_DEV void fe_addsub(fe& s, fe& d, const fe& a, const fe& b) {
+  fe x = a, y = a;
+  uint32_t t, u;
+  uint64_t cs, cd;
+  asm("v_add_co_u32_e64 %0, %[cs], %0, %[b0]\n\t"
+      "v_sub_co_u32_e64 %8, %[cd], %8, %[b0]\n\t"
+      "v_addc_co_u32_e64 %1, %[cs], %1, %[b1], %[cs]\n\t"
+      "v_subb_co_u32_e64 %9, %[cd], %9, %[b1], %[cd]\n\t"
+      "v_addc_co_u32_e64 %2, %[cs], %2, %[b2], %[cs]\n\t"
+      "v_subb_co_u32_e64 %10, %[cd], %10, %[b2], %[cd]\n\t"
+      "v_addc_co_u32_e64 %3, %[cs], %3, %[b3], %[cs]\n\t"
+      "v_subb_co_u32_e64 %11, %[cd], %11, %[b3], %[cd]\n\t"
+      "v_addc_co_u32_e64 %4, %[cs], %4, %[b4], %[cs]\n\t"
+      "v_subb_co_u32_e64 %12, %[cd], %12, %[b4], %[cd]\n\t"
+      "v_addc_co_u32_e64 %5, %[cs], %5, %[b5], %[cs]\n\t"
+      "v_subb_co_u32_e64 %13, %[cd], %13, %[b5], %[cd]\n\t"
+      "v_addc_co_u32_e64 %6, %[cs], %6, %[b6], %[cs]\n\t"
+      "v_subb_co_u32_e64 %14, %[cd], %14, %[b6], %[cd]\n\t"
+      "v_addc_co_u32_e64 %7, %[cs], %7, %[b7], %[cs]\n\t"
+      "v_subb_co_u32_e64 %15, %[cd], %15, %[b7], %[cd]\n\t"
+      "v_cndmask_b32_e64 %[t], 0, 38, %[cs]\n\t"
+      "v_cndmask_b32_e64 %[u], 0, 38, %[cd]\n\t"
+      "v_add_co_u32_e64 %0, %[cs], %0, %[t]\n\t"
+      "v_sub_co_u32_e64 %8, %[cd], %8, %[u]\n\t"
+      "s_or_b64 vcc, %[cs], %[cd]\n\t"
+      COA_RARE_BEGIN
+      "v_addc_co_u32_e64 %1, %[cs], 0, %1, %[cs]\n\t"
+      "v_subbrev_co_u32_e64 %9, %[cd], 0, %9, %[cd]\n\t"
+      "v_addc_co_u32_e64 %2, %[cs], 0, %2, %[cs]\n\t"
+      "v_subbrev_co_u32_e64 %10, %[cd], 0, %10, %[cd]\n\t"
+      "v_addc_co_u32_e64 %3, %[cs], 0, %3, %[cs]\n\t"
+      "v_subbrev_co_u32_e64 %11, %[cd], 0, %11, %[cd]\n\t"
+      "v_addc_co_u32_e64 %4, %[cs], 0, %4, %[cs]\n\t"
+      "v_subbrev_co_u32_e64 %12, %[cd], 0, %12, %[cd]\n\t"
+      "v_addc_co_u32_e64 %5, %[cs], 0, %5, %[cs]\n\t"
+      "v_subbrev_co_u32_e64 %13, %[cd], 0, %13, %[cd]\n\t"
+      "v_addc_co_u32_e64 %6, %[cs], 0, %6, %[cs]\n\t"
+      "v_subbrev_co_u32_e64 %14, %[cd], 0, %14, %[cd]\n\t"
+      "v_addc_co_u32_e64 %7, %[cs], 0, %7, %[cs]\n\t"
+      "v_subbrev_co_u32_e64 %15, %[cd], 0, %15, %[cd]\n\t"
+      "v_cndmask_b32_e64 %[t], 0, 38, %[cs]\n\t"
+      "v_cndmask_b32_e64 %[u], 0, 38, %[cd]\n\t"
+      "v_add_u32_e32 %0, %0, %[t]\n\t"
+      "v_sub_u32_e32 %8, %8, %[u]\n\t"
+      COA_RARE_END
+      : COA_R8_INOUT(x), COA_R8_INOUT(y), [t] "=&v"(t), [u] "=&v"(u), [cs] "=&s"(cs), [cd] "=&s"(cd)
+      : [b0] "v"(b.v[0]), [b1] "v"(b.v[1]), [b2] "v"(b.v[2]), [b3] "v"(b.v[3]), [b4] "v"(b.v[4]),
+        [b5] "v"(b.v[5]), [b6] "v"(b.v[6]), [b7] "v"(b.v[7])
+      : "vcc", "scc");  // s_or_b64 writes SCC
+  s = x;
+  d = y;
+}
+
 COA_DEV void fe_neg(fe& r, const fe& a) {
   fe z;
   fe_set(z, 0);

@@ -176,24 +176,20 @@ COA_DEV void ge_p2_dbl_il(ge_p1p1& r, const ge_p2& p) {
   fe o[4];
   fe_sq_n<4>(o, s);
   fe_add(o[2], o[2], o[2]);
-  fe_add(r.Y, o[1], o[0]);
-  fe_sub(r.Z, o[1], o[0]);
+  fe_addsub(r.Y, r.Z, o[1], o[0]);
   fe_sub(r.X, o[3], r.Y);
   fe_sub(r.T, o[2], r.Z);
 }
 COA_DEV void ge_add_il(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
   fe a[4], o[4];
-  fe_add(a[0], p.Y, p.X);
-  fe_sub(a[1], p.Y, p.X);
+  fe_addsub(a[0], a[1], p.Y, p.X);
   a[2] = q.T2d;
   a[3] = p.Z;
   const fe b[4] = {q.YplusX, q.YminusX, p.T, q.Z};
   fe_mul_n<4>(o, a, b);
   fe_add(o[3], o[3], o[3]);
-  fe_sub(r.X, o[0], o[1]);
-  fe_add(r.Y, o[0], o[1]);
-  fe_add(r.Z, o[3], o[2]);
-  fe_sub(r.T, o[3], o[2]);
+  fe_addsub(r.Y, r.X, o[0], o[1]);
+  fe_addsub(r.Z, r.T, o[3], o[2]);
 }
 
 // Conditionally negate an addend: -(x, y) = (-x, y) swaps Y+X / Y-X and
