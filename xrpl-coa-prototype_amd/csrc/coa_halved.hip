@@ -443,7 +443,11 @@ __global__ void __launch_bounds__(256, WAVES) k_pre_halve(const uint8_t* __restr
 // Split verification, phase 2: one lane per item (n <= grid), Q = [c](-A) +
 // [|d|](-sign(d) R) from the slab tables (for d < 0 the R digits are negated
 // instead of the table), plus the [e]B point of phase 1.
-template <int WAVES>
+// IL: the point formulas with their independent products interleaved
+// (coa_ge.h *_il; 195 VGPRs) for calls of at most one wave per SIMD, where a
+// lone wave waits on its own dependency chains; larger calls keep the plain
+// formulas (158 VGPRs, three waves per SIMD).
+template <int WAVES, bool IL>
 __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __restrict__ rec,
                                                         const uint8_t* __restrict__ flags, uint32_t n,
                                                         uint8_t* __restrict__ verdicts,
@@ -472,19 +476,39 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
       if (pos != H - 1) {
 #pragma unroll 1
         for (int k = 0; k < 3; k++) {
-          ge_p2_dbl_il(t, acc2);
-          ge_p1p1_to_p2_il(acc2, t);
+          if constexpr (IL) {
+            ge_p2_dbl_il(t, acc2);
+            ge_p1p1_to_p2_il(acc2, t);
+          } else {
+            ge_p2_dbl(t, acc2);
+            ge_p1p1_to_p2(acc2, t);
+          }
         }
-        ge_p2_dbl_il(t, acc2);
-        ge_p1p1_to_p3_il(acc3, t);
+        if constexpr (IL) {
+          ge_p2_dbl_il(t, acc2);
+          ge_p1p1_to_p3_il(acc3, t);
+        } else {
+          ge_p2_dbl(t, acc2);
+          ge_p1p1_to_p3(acc3, t);
+        }
       }
       ge_cached q;
       tab2_select(q, scr, i, 0, dc);
-      ge_add_il(t, acc3, q);
-      ge_p1p1_to_p3_il(acc3, t);
+      if constexpr (IL) {
+        ge_add_il(t, acc3, q);
+        ge_p1p1_to_p3_il(acc3, t);
+      } else {
+        ge_add(t, acc3, q);
+        ge_p1p1_to_p3(acc3, t);
+      }
       tab2_select(q, scr, i, 1, dneg ? -dd : dd);
-      ge_add_il(t, acc3, q);
-      if (pos != 0) ge_p1p1_to_p2_il(acc2, t);
+      if constexpr (IL) {
+        ge_add_il(t, acc3, q);
+        if (pos != 0) ge_p1p1_to_p2_il(acc2, t);
+      } else {
+        ge_add(t, acc3, q);
+        if (pos != 0) ge_p1p1_to_p2(acc2, t);
+      }
     }
     ge_p1p1_to_p3(acc3, t);
     if (!ebp) {  // [e]B here, from the combs
@@ -694,8 +718,16 @@ hipError_t coa_launch_verify_split(const uint8_t* pks, const uint8_t* sigs, cons
                      rec, flags, scratch, ebp, comb, wcomb, blocks, prio);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_verify_main<2>, dim3((n + main_b - 1) / main_b), dim3(main_b), 0, s, rec, flags, n, verdicts,
-                     scratch, ebp, comb, wcomb);
+  // at most one wave per SIMD (the C2 size on 256 CUs): the interleaved
+  // formulas; COA_MAIN_IL=0/1 forces either (A/B runs)
+  const char* il_env = getenv("COA_MAIN_IL");
+  const bool il = il_env ? atoi(il_env) != 0 : n <= 65536u;
+  if (il)
+    hipLaunchKernelGGL((k_verify_main<2, true>), dim3((n + main_b - 1) / main_b), dim3(main_b), 0, s, rec, flags, n,
+                       verdicts, scratch, ebp, comb, wcomb);
+  else
+    hipLaunchKernelGGL((k_verify_main<3, false>), dim3((n + main_b - 1) / main_b), dim3(main_b), 0, s, rec, flags, n,
+                       verdicts, scratch, ebp, comb, wcomb);
   return hipGetLastError();
 }
 
