@@ -481,8 +481,11 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
     const uint64_t o0 = uni64(a.hdr_off[c]), len = uni64(a.hdr_off[c + 1]) - o0;
     const uint8_t* p = a.hdr_data + o0;
     const uint64_t nblk = (len + 17 + 127) / 128;
-    uint64_t st[8];
-    coa_sha::init(st);
+    // the rounds on wave 0, each lane pair running one round's two halves
+    // (coa_sha512.h, compress_kw2); lane 0 ends with the whole state
+    const coa_sha::Lane2 L2 = coa_sha::lane2(lane);
+    uint64_t hs[4];
+    coa_sha::init2(hs, L2);
 #pragma unroll 1
     for (uint64_t b0 = 0; b0 < nblk; b0 += KW_CHUNK) {
       const uint32_t nb = (uint32_t)min<uint64_t>(KW_CHUNK, nblk - b0);
@@ -494,11 +497,13 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
       __syncthreads();
       if (wave == 0) {
 #pragma unroll 1
-        for (uint32_t b = 0; b < nb; b++) coa_sha::compress_kw(st, kw_lds + b * 80);
+        for (uint32_t b = 0; b < nb; b++) coa_sha::compress_kw2(hs, kw_lds + b * 80, L2);
       }
       __syncthreads();
     }
     if (wave) return;
+    uint64_t st[8];
+    coa_sha::gather2(st, hs);
     uint32_t h[16], id[8];
     coa_sha::state_to_le_words(h, st);
     load8u(id, a.ids + (uint64_t)c * 8);

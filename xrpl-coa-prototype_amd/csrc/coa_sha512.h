@@ -414,6 +414,88 @@ COA_DEV void compress_kw(uint64_t st[8], const uint64_t* kw) {
   st[7] += h;
 }
 
+// ------------------------------------------------------------------------
+// One message on two lanes of a wave: the round's two halves in one
+// instruction stream.  Even lanes hold (e, f, g, h) and compute
+//   T1 = h + kw + S1(e) + Ch(e, f, g),
+// odd lanes hold (a, b, c, d) and compute
+//   T2 = S0(a) + Maj(a, b, c) = S0(a) + Ch(a ^ c, b, c),
+// with per-lane operands only: both sums are r3-rotations of
+// x ^ rotr(x, r1) ^ rotr(x, r2) (S1: 14 of 4 and 27; S0: 28 of 6 and 11, so
+// every rotate is a pair of v_alignbit_b32 with a per-lane amount), Ch's first
+// operand is x ^ (s2 & m) (m = 0 on even lanes), and h + kw is masked to 0 on
+// odd lanes.  One DPP swap of adjacent lanes then hands the even lane d and
+// the odd lane T1: the new e = d + T1 and the new a = T1 + T2 are both
+// "received + own".  A lone wave issues one instruction per ~4 cycles, so
+// single-message latency is the round's instruction count: ~22 here against
+// ~28 for the one-lane round.
+struct Lane2 {
+  uint32_t r1, r2, r3, m, km;
+  bool even;
+};
+COA_DEV Lane2 lane2(uint32_t lane) {
+  Lane2 L;
+  L.even = (lane & 1) == 0;
+  L.r1 = L.even ? 4u : 6u;
+  L.r2 = L.even ? 27u : 11u;
+  L.r3 = L.even ? 14u : 28u;
+  L.m = L.even ? 0u : ~0u;
+  L.km = L.even ? ~0u : 0u;
+  return L;
+}
+COA_DEV uint64_t rotr_v(uint64_t x, uint32_t n) {  // 0 < n < 32, per lane
+  const uint32_t l = lo32(x), h = hi32(x);
+  return mk64(__builtin_amdgcn_alignbit(h, l, n), __builtin_amdgcn_alignbit(l, h, n));
+}
+COA_DEV uint64_t swap_adjacent(uint64_t x) {  // lanes 2i <-> 2i + 1 (DPP quad_perm [1,0,3,2])
+  return mk64((uint32_t)__builtin_amdgcn_mov_dpp((int)lo32(x), 0xB1, 0xF, 0xF, false),
+              (uint32_t)__builtin_amdgcn_mov_dpp((int)hi32(x), 0xB1, 0xF, 0xF, false));
+}
+// (s0, s1, s2, s3) -> the lane's new s0, written into s3 (the caller renames).
+COA_DEV void round2(uint64_t s0, uint64_t s1, uint64_t s2, uint64_t& s3, uint64_t kw, const Lane2& L) {
+  const uint64_t in = xor3(s0, rotr_v(s0, L.r1), rotr_v(s0, L.r2));
+  const uint64_t sg = rotr_v(in, L.r3);
+  const uint64_t y = bitop3<0x78>(s0, s2, mk64(L.m, L.m));  // s0 ^ (s2 & m)
+  const uint64_t t = sg + ch(y, s1, s2) + ((s3 + kw) & mk64(L.km, L.km));
+  const uint64_t r = swap_adjacent(L.even ? t : s3);
+  s3 = r + t;
+}
+// One block's 80 rounds on the lane's half state hs (even lanes: state words
+// 4..7, odd lanes: 0..3) from a precomputed kw (LDS, broadcast).
+COA_DEV void compress_kw2(uint64_t hs[4], const uint64_t* kw, const Lane2& L) {
+  uint64_t a = hs[0], b = hs[1], c = hs[2], d = hs[3];
+#pragma unroll 1
+  for (int r = 0; r < 80; r += 16) {
+    const uint64_t* k = kw + r;
+#pragma unroll
+    for (int q = 0; q < 16; q += 4) {
+      round2(a, b, c, d, k[q], L);
+      round2(d, a, b, c, k[q + 1], L);
+      round2(c, d, a, b, k[q + 2], L);
+      round2(b, c, d, a, k[q + 3], L);
+    }
+  }
+  hs[0] += a;
+  hs[1] += b;
+  hs[2] += c;
+  hs[3] += d;
+}
+// The lane's half of the initial state / the full state on even lanes after
+// the last block (odd partners hand over words 0..3).
+COA_DEV void init2(uint64_t hs[4], const Lane2& L) {
+  uint64_t st[8];
+  init(st);
+#pragma unroll
+  for (int i = 0; i < 4; i++) hs[i] = L.even ? st[4 + i] : st[i];
+}
+COA_DEV void gather2(uint64_t st[8], const uint64_t hs[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    st[i] = swap_adjacent(hs[i]);
+    st[4 + i] = hs[i];
+  }
+}
+
 // compress_kw with kw[t] at kw[t * STRIDE] (the shared-schedule kernel's
 // lane-interleaved LDS layout).
 template <int STRIDE>
