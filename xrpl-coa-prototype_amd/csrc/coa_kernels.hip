@@ -304,8 +304,12 @@ __global__ void __launch_bounds__(64) k_sha512_ml(const uint8_t* __restrict__ da
                            (uint32_t)__shfl_xor((int)(uint32_t)maxblk, o, 64);
     maxblk = other > maxblk ? other : maxblk;
   }
-  uint64_t st[8];
-  coa_sha::init(st);
+  // the rounds on lane pairs (q even: state words 4..7, q odd: 0..3; L is
+  // even, so a group's lanes pair up as 2i, 2i + 1): coa_sha512.h,
+  // compress_kw2; lane q = 0 gathers the digest
+  const coa_sha::Lane2 L2 = coa_sha::lane2(q);
+  uint64_t hs[4];
+  coa_sha::init2(hs, L2);
 #pragma unroll 1
   for (uint64_t b0 = 0; b0 < maxblk; b0 += L) {
     if (b0 + q < nblk) {
@@ -316,9 +320,11 @@ __global__ void __launch_bounds__(64) k_sha512_ml(const uint8_t* __restrict__ da
     __syncthreads();
 #pragma unroll 1
     for (int j = 0; j < L; j++)
-      if (b0 + j < nblk) coa_sha::compress_kws<64>(st, kw + j * G + grp);
+      if (b0 + j < nblk) coa_sha::compress_kw2<64>(hs, kw + j * G + grp, L2);
     __syncthreads();
   }
+  uint64_t st[8];
+  coa_sha::gather2(st, hs);
   if (live && q == 0) {
     uint32_t h[16];
     coa_sha::state_to_le_words(h, st);

@@ -461,18 +461,20 @@ COA_DEV void round2(uint64_t s0, uint64_t s1, uint64_t s2, uint64_t& s3, uint64_
   s3 = r + t;
 }
 // One block's 80 rounds on the lane's half state hs (even lanes: state words
-// 4..7, odd lanes: 0..3) from a precomputed kw (LDS, broadcast).
+// 4..7, odd lanes: 0..3) from a precomputed kw[t * STRIDE] (LDS; both lanes
+// of a pair read the same word).
+template <int STRIDE = 1>
 COA_DEV void compress_kw2(uint64_t hs[4], const uint64_t* kw, const Lane2& L) {
   uint64_t a = hs[0], b = hs[1], c = hs[2], d = hs[3];
 #pragma unroll 1
   for (int r = 0; r < 80; r += 16) {
-    const uint64_t* k = kw + r;
+    const uint64_t* k = kw + r * STRIDE;
 #pragma unroll
     for (int q = 0; q < 16; q += 4) {
-      round2(a, b, c, d, k[q], L);
-      round2(d, a, b, c, k[q + 1], L);
-      round2(c, d, a, b, k[q + 2], L);
-      round2(b, c, d, a, k[q + 3], L);
+      round2(a, b, c, d, k[q * STRIDE], L);
+      round2(d, a, b, c, k[(q + 1) * STRIDE], L);
+      round2(c, d, a, b, k[(q + 2) * STRIDE], L);
+      round2(b, c, d, a, k[(q + 3) * STRIDE], L);
     }
   }
   hs[0] += a;
