@@ -59,6 +59,7 @@ def test_adversarial_device_path(engine):
 VERIFY_PATHS = {
     "split": {},                                            # default: k_pre_halve + k_verify_main
     "split/narrow": {"COA_WCOMB": "0"},                     # [e]B from the radix-256 comb
+    "split/plain-main": {"COA_MAIN_IL": "0"},               # k_verify_main without interleaved products
     "single": {"COA_VERIFY_SPLIT": "0"},                    # k_halve + k_verify_halved
     "single/narrow": {"COA_VERIFY_SPLIT": "0", "COA_WCOMB": "0"},
     "full": {"COA_VERIFY_IMPL": "full"},                    # k_hram + k_verify_strict, no halving
