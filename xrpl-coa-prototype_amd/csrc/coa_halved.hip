@@ -64,6 +64,28 @@ COA_DEV void tab2_select(ge_cached& q, const uint32_t* scr, uint32_t lane, int t
   ge_cached_cneg(q, d < 0);
 }
 
+// tab2_select in two halves: the raw entry load (issued early, so a lone
+// wave's doublings cover its latency) and the sign/zero fix-up at the use.
+COA_DEV void tab2_load(ge_cached& q, const uint32_t* scr, uint32_t lane, int tab, int d) {
+  const int m = d < 0 ? -d : d;
+  const int entry = m == 0 ? 0 : m - 1;
+  fe* f[4] = {&q.YplusX, &q.YminusX, &q.Z, &q.T2d};
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint4 v = reinterpret_cast<const uint4*>(scr)[((uint64_t)lane * 16 + tab * 8 + entry) * 8 + c * 2 + h];
+      f[c]->v[4 * h] = v.x;
+      f[c]->v[4 * h + 1] = v.y;
+      f[c]->v[4 * h + 2] = v.z;
+      f[c]->v[4 * h + 3] = v.w;
+    }
+}
+COA_DEV void tab2_fix(ge_cached& q, int d) {
+  if (d == 0) ge_cached_identity(q);
+  ge_cached_cneg(q, d < 0);
+}
+
 COA_DEV void tab2_build(uint32_t* scr, uint32_t lane, int tab, const ge_p3& P) {
   ge_cached c1;
   ge_p3_to_cached(c1, P);
@@ -443,10 +465,12 @@ __global__ void __launch_bounds__(256, WAVES) k_pre_halve(const uint8_t* __restr
 // Split verification, phase 2: one lane per item (n <= grid), Q = [c](-A) +
 // [|d|](-sign(d) R) from the slab tables (for d < 0 the R digits are negated
 // instead of the table), plus the [e]B point of phase 1.
-// IL: the point formulas with their independent products interleaved
-// (coa_ge.h *_il; 195 VGPRs) for calls of at most one wave per SIMD, where a
-// lone wave waits on its own dependency chains; larger calls keep the plain
-// formulas (158 VGPRs, three waves per SIMD).
+// IL: for calls of at most one wave per SIMD, where a lone wave waits on its
+// own dependency chains and memory: the point formulas with their independent
+// products interleaved (coa_ge.h *_il), and both table entries of a digit
+// loaded before its four doublings (launch bound of one wave per SIMD, up to
+// 512 VGPRs); larger calls keep the plain formulas (156 VGPRs, three waves
+// per SIMD).
 template <int WAVES, bool IL>
 __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __restrict__ rec,
                                                         const uint8_t* __restrict__ flags, uint32_t n,
@@ -468,11 +492,24 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
     ge_p2 acc2;
     ge_p1p1 t;
     ge_p3_identity(acc3);
+    uint32_t cw[8], dw[8];  // IL: the digit words in registers, not reloaded per digit
+    if constexpr (IL) {
+      load8_u4(cw, myrec);
+      load8_u4(dw, myrec + 8);
+    }
 #pragma unroll 1
     for (int pos = H - 1; pos >= 0; pos--) {
       const int sh = 4 * (pos & 7);
-      const int dc = (int)((myrec[pos >> 3] >> sh) & 15u) - 8;
-      const int dd = (int)((myrec[8 + (pos >> 3)] >> sh) & 15u) - 8;
+      const uint32_t wc = IL ? cw[pos >> 3] : myrec[pos >> 3];
+      const uint32_t wd = IL ? dw[pos >> 3] : myrec[8 + (pos >> 3)];
+      const int dc = (int)((wc >> sh) & 15u) - 8;
+      const int dd = (int)((wd >> sh) & 15u) - 8;
+      const int dr = dneg ? -dd : dd;
+      ge_cached qa, qr;
+      if constexpr (IL) {  // both entries in flight during the four doublings
+        tab2_load(qa, scr, i, 0, dc);
+        tab2_load(qr, scr, i, 1, dr);
+      }
       if (pos != H - 1) {
 #pragma unroll 1
         for (int k = 0; k < 3; k++) {
@@ -492,21 +529,19 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
           ge_p1p1_to_p3(acc3, t);
         }
       }
-      ge_cached q;
-      tab2_select(q, scr, i, 0, dc);
       if constexpr (IL) {
-        ge_add_il(t, acc3, q);
+        tab2_fix(qa, dc);
+        ge_add_il(t, acc3, qa);
         ge_p1p1_to_p3_il(acc3, t);
-      } else {
-        ge_add(t, acc3, q);
-        ge_p1p1_to_p3(acc3, t);
-      }
-      tab2_select(q, scr, i, 1, dneg ? -dd : dd);
-      if constexpr (IL) {
-        ge_add_il(t, acc3, q);
+        tab2_fix(qr, dr);
+        ge_add_il(t, acc3, qr);
         if (pos != 0) ge_p1p1_to_p2_il(acc2, t);
       } else {
-        ge_add(t, acc3, q);
+        tab2_select(qa, scr, i, 0, dc);
+        ge_add(t, acc3, qa);
+        ge_p1p1_to_p3(acc3, t);
+        tab2_select(qr, scr, i, 1, dr);
+        ge_add(t, acc3, qr);
         if (pos != 0) ge_p1p1_to_p2(acc2, t);
       }
     }
@@ -723,7 +758,7 @@ hipError_t coa_launch_verify_split(const uint8_t* pks, const uint8_t* sigs, cons
   const char* il_env = getenv("COA_MAIN_IL");
   const bool il = il_env ? atoi(il_env) != 0 : n <= 65536u;
   if (il)
-    hipLaunchKernelGGL((k_verify_main<2, true>), dim3((n + main_b - 1) / main_b), dim3(main_b), 0, s, rec, flags, n,
+    hipLaunchKernelGGL((k_verify_main<1, true>), dim3((n + main_b - 1) / main_b), dim3(main_b), 0, s, rec, flags, n,
                        verdicts, scratch, ebp, comb, wcomb);
   else
     hipLaunchKernelGGL((k_verify_main<3, false>), dim3((n + main_b - 1) / main_b), dim3(main_b), 0, s, rec, flags, n,
