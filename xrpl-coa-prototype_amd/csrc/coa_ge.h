@@ -192,6 +192,17 @@ COA_DEV void ge_add_il(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
   fe_addsub(r.Z, r.T, o[3], o[2]);
 }
 
+COA_DEV void ge_madd_il(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
+  fe a[3], o[3], zz;
+  fe_addsub(a[0], a[1], p.Y, p.X);
+  a[2] = q.xy2d;
+  const fe b[3] = {q.yplusx, q.yminusx, p.T};
+  fe_mul_n<3>(o, a, b);
+  fe_add(zz, p.Z, p.Z);
+  fe_addsub(r.Y, r.X, o[0], o[1]);
+  fe_addsub(r.Z, r.T, zz, o[2]);
+}
+
 // Conditionally negate an addend: -(x, y) = (-x, y) swaps Y+X / Y-X and
 // negates the T term.
 COA_DEV void ge_cached_cneg(ge_cached& q, bool neg) {

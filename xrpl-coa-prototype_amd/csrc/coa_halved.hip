@@ -545,13 +545,16 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
         if (pos != 0) ge_p1p1_to_p2(acc2, t);
       }
     }
-    ge_p1p1_to_p3(acc3, t);
+    if constexpr (IL)
+      ge_p1p1_to_p3_il(acc3, t);
+    else
+      ge_p1p1_to_p3(acc3, t);
     if (!ebp) {  // [e]B here, from the combs
       uint32_t e[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) e[j] = myrec[16 + j];
       if (wcomb) {
-        wcomb_accumulate(acc3, e, wcomb);
+        wcomb_accumulate<IL>(acc3, e, wcomb);
       } else {
         add_const_word(e, 0x80808080u);
 #pragma unroll 1

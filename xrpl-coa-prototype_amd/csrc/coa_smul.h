@@ -186,7 +186,7 @@ COA_DEV void wcomb_apply(ge_niels& q, const uint32_t* w, int d) {
 }
 // acc += [x]P from P's wide comb (x < 2^253; a larger x gives some point,
 // never an out-of-range entry).  Entry j+1 is loaded while addition j runs.
-template <int W, int POS>
+template <int W, int POS, bool IL = false>
 COA_DEV void wc_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __restrict__ tab) {
   uint32_t r[9], cur[24], nxt[24];
   wc_recode<W, POS>(r, x);
@@ -200,8 +200,13 @@ COA_DEV void wc_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __rest
     wc_load<W>(nxt, tab, jn, dn);
     ge_niels q;
     wcomb_apply(q, cur, d);
-    ge_madd(t, acc, q);
-    ge_p1p1_to_p3(acc, t);
+    if constexpr (IL) {  // interleaved products (coa_ge.h *_il)
+      ge_madd_il(t, acc, q);
+      ge_p1p1_to_p3_il(acc, t);
+    } else {
+      ge_madd(t, acc, q);
+      ge_p1p1_to_p3(acc, t);
+    }
     d = dn;
 #pragma unroll
     for (int i = 0; i < 24; i++) cur[i] = nxt[i];
@@ -212,8 +217,9 @@ COA_DEV void wc_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __rest
 COA_DEV void wcomb_load(uint32_t* w, const uint32_t* __restrict__ tab, int j, int d) {
   wc_load<COA_WCOMB_W>(w, tab, j, d);
 }
+template <bool IL = false>
 COA_DEV void wcomb_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __restrict__ tab) {
-  wc_accumulate<COA_WCOMB_W, COA_WCOMB_POS>(acc, x, tab);
+  wc_accumulate<COA_WCOMB_W, COA_WCOMB_POS, IL>(acc, x, tab);
 }
 
 COA_DEV uint32_t take_low_byte(uint32_t* x) {
