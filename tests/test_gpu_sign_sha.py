@@ -68,7 +68,7 @@ def test_worker_batch_500kb(engine):
         assert bytes(d) == hashlib.sha512(b).digest()
 
 
-@pytest.mark.parametrize("lanes", ["1", "2", "4", "16", "64", "auto"])
+@pytest.mark.parametrize("lanes", ["1", "2", "4", "8", "16", "32", "64", "auto"])
 def test_sha512_lanes_per_message_ragged(engine, lanes, monkeypatch):
     """SHA-512 with L lanes per message (shared message schedule in LDS):
     ragged lengths around the padding boundaries, multi-block, empty and
