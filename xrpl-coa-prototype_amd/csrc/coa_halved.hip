@@ -22,6 +22,7 @@
 //   k_verify_halved  decompression + small-order checks + Q == O
 #include "coa_halved.h"
 
+#include <atomic>
 #include <cstdlib>
 #include "coa_kernels.h"
 
@@ -728,6 +729,22 @@ hipError_t coa_launch_check_wcomb(const uint32_t* wcomb, uint32_t* bad, hipStrea
   return hipGetLastError();
 }
 
+// Items that fill every SIMD of the current device with one wave (CUs x 4
+// SIMDs x 64 lanes), read once per device.
+static uint32_t one_wave_per_simd_items() {
+  static std::atomic<uint32_t> cache[64];  // per device; the per-device worker threads share it
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 65536u;
+  uint32_t v = cache[dev].load(std::memory_order_relaxed);
+  if (!v) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    v = (uint32_t)cus * 256u;
+    cache[dev].store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+
 static uint32_t block_env(const char* name) {
   const char* e = getenv(name);
   const int b = e ? atoi(e) : COA_VERIFY_BLOCK;
@@ -756,10 +773,10 @@ hipError_t coa_launch_verify_split(const uint8_t* pks, const uint8_t* sigs, cons
                      rec, flags, scratch, ebp, comb, wcomb, blocks, prio);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // at most one wave per SIMD (the C2 size on 256 CUs): the interleaved
-  // formulas; COA_MAIN_IL=0/1 forces either (A/B runs)
+  // at most one wave per SIMD (65,536 items on the 256 CUs of an MI355X, the
+  // C2 size): the interleaved formulas; COA_MAIN_IL=0/1 forces either (A/B)
   const char* il_env = getenv("COA_MAIN_IL");
-  const bool il = il_env ? atoi(il_env) != 0 : n <= 65536u;
+  const bool il = il_env ? atoi(il_env) != 0 : n <= one_wave_per_simd_items();
   if (il)
     hipLaunchKernelGGL((k_verify_main<1, true>), dim3((n + main_b - 1) / main_b), dim3(main_b), 0, s, rec, flags, n,
                        verdicts, scratch, ebp, comb, wcomb);
