@@ -1,4 +1,5 @@
-// SHA-512 (FIPS 180-4) for gfx950, one message per lane.
+// SHA-512 (FIPS 180-4) for gfx950: one message per lane, or per lane pair
+// (round2 / compress_kw2: a round's two halves on two adjacent lanes).
 //
 // Replaces sha2 0.9 `Sha512` at the reference's digest sites
 // (worker/src/processor.rs:38, primary/src/messages.rs:72-82,147-151,
