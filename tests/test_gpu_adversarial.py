@@ -17,8 +17,13 @@ def _pool():
             for v in load_golden("mixed_order_pool.json")]
 
 
-@pytest.mark.parametrize("n,frac", [(4096, 0.25), (262_144, 0.01)])
-def test_adversarial_mix_bit_exact(engine, n, frac):
+@pytest.mark.parametrize("n,frac,il", [(4096, 0.25, None), (65_536, 0.01, None), (262_144, 0.01, None),
+                                        (262_144, 0.01, "1")])
+def test_adversarial_mix_bit_exact(engine, n, frac, il, monkeypatch):
+    """n = 65,536 is the C2 size (the one-wave main kernel by default); 2^18
+    takes the three-wave one by default and the one-wave one forced."""
+    if il is not None:
+        monkeypatch.setenv("COA_MAIN_IL", il)
     from workloads import adversarial_mix, key_seeds, messages
 
     seeds, msgs = key_seeds(n), messages(n)
