@@ -70,6 +70,15 @@ int coa_self_test(int device, uint64_t* bad_entries);
 int coa_fe_rows_check_device(int device, const uint8_t* d_in, size_t n, uint32_t* d_out, void* stream);
 /* Human-readable description of the last error on this thread. */
 const char* coa_last_error(void);
+/* Engine-failure recovery of the host-pointer calls since the library
+ * loaded (no reference counterpart: dalek cannot fail for a reason other
+ * than the input).  A shard whose device work fails (a HIP error or an
+ * allocation failure) has its context rebuilt -- a new stream, per-call
+ * buffers released, in the same process -- and is re-run on the next
+ * contexts in turn; the call returns an error only when every context
+ * failed it.  *contexts_rebuilt / *shards_rerun (either may be NULL) get the
+ * counts.  The aggregation queue counts its own in coa_queue_metrics. */
+int coa_engine_recoveries(uint64_t* contexts_rebuilt, uint64_t* shards_rerun);
 /* Library / ABI version string. */
 const char* coa_version(void);
 
@@ -293,12 +302,15 @@ int coa_ed25519_sign_many_device(int device, const uint8_t* d_seeds, const uint8
  * (when max_batch signatures are pending, when the oldest request is
  * max_delay_us old, or on flush) and replies per request through the
  * callback -- the SignatureService request/oneshot idiom of
- * crypto/src/lib.rs:222-250.  Inputs are copied at submission.  A collector
+ * crypto/src/lib.rs:222-250.  Inputs are copied at submission (into one of
+ * a fixed pool of intake shards, chosen by the calling thread).  A collector
  * thread launches each window on the next of two device slots per GPU
  * (pinned staging, own stream) without waiting for the previous window, and
  * a completion thread answers windows in order: the callback runs there with
  * status (COA_OK or a negative engine error) and the request's verdict
- * byte(s). */
+ * byte(s).  coa_committee_register waits for in-flight windows that read the
+ * committee key cache (certificate windows) and holds new ones back until it
+ * has finished, so registration stays verdict-neutral under load. */
 typedef struct coa_queue coa_queue;
 typedef void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n);
 coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us);
@@ -321,18 +333,23 @@ int coa_queue_submit_certificate(coa_queue* q, const uint8_t* header_data, size_
  * callback receives the 32-byte Digest (n = 32). */
 int coa_queue_submit_digest(coa_queue* q, const uint8_t* data, size_t len, coa_verdict_cb cb, void* user);
 int coa_queue_flush(coa_queue* q);
-/* items = verify requests; groups = vote batches + certificates. */
+/* items = signatures answered (a coa_queue_submit_verify_many request of n
+ * counts n); groups = vote batches + certificates. */
 int coa_queue_stats(coa_queue* q, uint64_t* launches, uint64_t* items, uint64_t* groups);
 int coa_queue_digest_count(coa_queue* q, uint64_t* digests);
 /* Queue metrics since creation.  A window is the set of requests one launch
- * takes; windows are double-buffered (the next window is packed and its
- * copies and kernels enqueued while the previous one runs).  wait_us_* is
- * the time from a request's submission to the start of its callback
- * (percentiles from a log-spaced histogram, +-9 %). */
+ * takes; windows are pipelined (the next window is packed and its copies and
+ * kernels enqueued while the previous one runs).  wait_us_* is the time from
+ * a request's submission to the start of its callback (percentiles from a
+ * log-spaced histogram, +-6 %).
+ * Engine-failure recovery: a window whose launch fails (a HIP error) is
+ * re-run on the recovery context of each device in turn (the failed slot's
+ * stream, event and buffers rebuilt meanwhile, in the same process); its
+ * callbacks get a negative status only when every attempt failed. */
 typedef struct {
   uint64_t requests;      /* requests answered */
   uint64_t windows;       /* launch windows */
-  uint64_t signatures;    /* verify requests */
+  uint64_t signatures;    /* signatures answered (verify requests x their n) */
   uint64_t batches;       /* vote-batch requests */
   uint64_t certificates;  /* certificate requests */
   uint64_t digests;       /* digest requests */
@@ -340,6 +357,9 @@ typedef struct {
   uint64_t max_in_flight; /* most windows launched and not yet answered at once */
   uint64_t max_pending;   /* most items waiting for a window at once */
   double wait_us_mean, wait_us_p50, wait_us_p99, wait_us_max;
+  uint64_t retried_windows;   /* windows whose launch failed and were re-run */
+  uint64_t recovered_windows; /* ... of which a re-run succeeded */
+  uint64_t failed_windows;    /* windows answered with an engine error */
 } coa_queue_metrics_t;
 int coa_queue_metrics(coa_queue* q, coa_queue_metrics_t* out);
 int coa_queue_destroy(coa_queue* q);

@@ -52,6 +52,9 @@ pub struct CoaQueueMetrics {
     pub wait_us_p50: f64,
     pub wait_us_p99: f64,
     pub wait_us_max: f64,
+    pub retried_windows: u64,
+    pub recovered_windows: u64,
+    pub failed_windows: u64,
 }
 
 /// void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n)
@@ -69,6 +72,7 @@ extern "C" {
     pub fn coa_fe_rows_check_device(device: c_int, d_in: *const u8, n: usize, d_out: *mut u32,
                                     stream: *mut c_void) -> c_int;
     pub fn coa_last_error() -> *const c_char;
+    pub fn coa_engine_recoveries(contexts_rebuilt: *mut u64, shards_rerun: *mut u64) -> c_int;
     pub fn coa_version() -> *const c_char;
 
     // -------------------------------------------------- Signature::verify

@@ -24,9 +24,15 @@
 
 // ------------------------------------------------------------ stub backend
 // Two slots like the HIP backend: launch() blocks while both are busy and
-// returns at once; complete() "runs" the window (a short sleep) and writes the
-// outputs.  Verdicts are pure functions of the request bytes.
-static std::atomic<long> g_engine_calls{0};
+// returns at once; complete() "runs" the launch (a short sleep) and writes
+// every part's outputs.  Verdicts are pure functions of the request bytes.
+// Fault injection (argv[3] = k): every k-th launch fails in complete() (no
+// outputs, COA_EHIP), as a HIP error would; the queue must then re-run it
+// through retry(), which succeeds -- unless argv[4] = 1, when every retry
+// fails too and the callbacks must get the engine error.
+static std::atomic<long> g_engine_calls{0}, g_injected{0};
+static unsigned long g_fault_every = 0;
+static bool g_fault_all = false;
 static uint8_t v_single(const uint8_t* msg, const uint8_t* sig) { return (uint8_t)((msg[0] ^ sig[0]) & 1u); }
 static uint8_t v_group(const uint8_t* msg, size_t nvotes) { return (uint8_t)((msg[1] + nvotes) & 1u); }
 static uint8_t v_cert(const uint8_t* id, size_t nvotes) { return (uint8_t)((id[2] + nvotes) & 7u); }
@@ -35,39 +41,63 @@ static uint8_t v_digest(const uint8_t* data, size_t len, int j) {
 }
 
 namespace {
-class StubBackend : public coa_q::Backend {
- public:
-  int slots() const override { return 2; }
-  void launch(coa_q::Window& w) override {
-    std::unique_lock<std::mutex> l(m_);
-    const int k = (int)(next_++ % 2);
-    cv_.wait(l, [&] { return !busy_[k]; });
-    busy_[k] = true;
-    w.slot = k;
-    w.v_out.assign(w.nv, 1);
-    w.g_out.assign(w.ng, 1);
-    w.c_out.assign(w.nc, 7);
-    w.d_out.assign(w.nd * 32, 0);
-  }
-  void complete(coa_q::Window& w) override {
-    g_engine_calls++;
-    std::this_thread::sleep_for(std::chrono::microseconds(50));
+void run_launch(coa_q::Launch& L) {
+  for (coa_q::Window* wp : L.parts) {
+    coa_q::Window& w = *wp;
     for (size_t i = 0; i < w.nv; i++) w.v_out[i] = v_single(&w.v_msgs[i * 32], &w.v_sigs[i * 64]);
     for (size_t g = 0; g < w.ng; g++) w.g_out[g] = v_group(&w.g_msgs[g * 32], w.g_offs[g + 1] - w.g_offs[g]);
     for (size_t c = 0; c < w.nc; c++) w.c_out[c] = v_cert(&w.c_ids[c * 32], w.c_voff[c + 1] - w.c_voff[c]);
     for (size_t i = 0; i < w.nd; i++)
       for (int j = 0; j < 32; j++)
         w.d_out[i * 32 + j] = v_digest(w.d_data.data() + w.d_offs[i], w.d_offs[i + 1] - w.d_offs[i], j);
-    w.rc = COA_OK;
+  }
+  L.rc = COA_OK;
+}
+
+class StubBackend : public coa_q::Backend {
+ public:
+  int slots() const override { return 2; }
+  int devices() const override { return 2; }
+  void launch(coa_q::Launch& L) override {
+    std::unique_lock<std::mutex> l(m_);
+    const int k = (int)(next_++ % 2);
+    cv_.wait(l, [&] { return !busy_[k]; });
+    busy_[k] = true;
+    L.slot = k;
+    fail_[k] = g_fault_every && next_ % g_fault_every == 0;
+  }
+  void complete(coa_q::Launch& L) override {
+    g_engine_calls++;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+    bool failed;
+    {
+      std::lock_guard<std::mutex> l(m_);
+      failed = fail_[L.slot];
+    }
+    if (failed) {
+      g_injected++;
+      L.rc = COA_EHIP;  // outputs stay at their "failed" values
+    } else {
+      run_launch(L);
+    }
     std::lock_guard<std::mutex> l(m_);
-    busy_[w.slot] = false;
+    busy_[L.slot] = false;
     cv_.notify_all();
+  }
+  void retry(coa_q::Launch& L, int attempt) override {
+    if (attempt < 1 || attempt > devices()) std::abort();
+    if (g_fault_all) {
+      L.rc = COA_EHIP;
+      return;
+    }
+    run_launch(L);
   }
 
  private:
   std::mutex m_;
   std::condition_variable cv_;
   bool busy_[2] = {false, false};
+  bool fail_[2] = {false, false};
   unsigned long next_ = 0;
 };
 }  // namespace
@@ -82,15 +112,23 @@ struct Req {
   std::atomic<int> bad{0};
 };
 
+static std::atomic<long> g_engine_errors{0};
 static void check_cb(void* user, int status, const uint8_t* verdicts, size_t n) {
   Req* r = static_cast<Req*>(user);
-  if (status != COA_OK || n != r->n_expect || std::memcmp(verdicts, r->expect, n) != 0) r->bad++;
+  if (status == COA_EHIP) {
+    g_engine_errors++;
+    if (!g_fault_all) r->bad++;
+  } else if (status != COA_OK || n != r->n_expect || std::memcmp(verdicts, r->expect, n) != 0) {
+    r->bad++;
+  }
   r->done++;
 }
 
 int main(int argc, char** argv) {
   const int producers = argc > 1 ? std::atoi(argv[1]) : 8;
   const int per = argc > 2 ? std::atoi(argv[2]) : 400;
+  g_fault_every = argc > 3 ? std::strtoul(argv[3], nullptr, 10) : 0;
+  g_fault_all = argc > 4 && std::atoi(argv[4]) == 1;
   coa_queue* q = coa_queue_create(64, 200);
   std::vector<std::vector<Req>> reqs(producers);
   for (auto& v : reqs) v = std::vector<Req>(per);
@@ -165,10 +203,18 @@ int main(int argc, char** argv) {
   coa_queue_destroy(q);
   const long total = (long)producers * per;
   std::printf("queue tsan: %ld/%ld answered, %ld wrong, %llu launches, %ld windows completed, max in flight %llu, "
-              "wait p50 %.0f us p99 %.0f us\n",
+              "wait p50 %.0f us p99 %.0f us, injected %ld, retried %llu, recovered %llu, failed %llu, engine errors %ld\n",
               done, total, bad, (unsigned long long)launches, g_engine_calls.load(),
-              (unsigned long long)m.max_in_flight, m.wait_us_p50, m.wait_us_p99);
-  const bool metrics_ok = m.requests == (uint64_t)total && m.signatures + m.batches + m.certificates + m.digests ==
-                                                               (uint64_t)total && m.windows == launches;
+              (unsigned long long)m.max_in_flight, m.wait_us_p50, m.wait_us_p99, g_injected.load(),
+              (unsigned long long)m.retried_windows, (unsigned long long)m.recovered_windows,
+              (unsigned long long)m.failed_windows, g_engine_errors.load());
+  // every injected failure was retried; retries succeed unless told not to
+  const bool recovery_ok =
+      m.retried_windows == (uint64_t)g_injected.load() &&
+      (g_fault_all ? (m.recovered_windows == 0 && m.failed_windows == m.retried_windows &&
+                      (g_injected.load() == 0 || g_engine_errors.load() > 0))
+                   : (m.recovered_windows == m.retried_windows && m.failed_windows == 0 && g_engine_errors.load() == 0));
+  const bool metrics_ok = m.requests == (uint64_t)total && m.batches + m.certificates + m.digests <= (uint64_t)total &&
+                          m.windows == launches && recovery_ok;
   return (done == total && bad == 0 && items + groups + digests == (uint64_t)total && metrics_ok) ? 0 : 1;
 }

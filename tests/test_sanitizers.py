@@ -11,7 +11,9 @@
   pthread_cond_clockwait and reports false double locks) and, separately,
   ASan + UBSan, with a deterministic stub in place of its HIP launch backend
   (same two-slot double buffering), with 16 producer threads submitting
-  every request kind while they also flush and read the stats and metrics.
+  every request kind while they also flush and read the stats and metrics,
+  and with injected launch failures (engine-failure recovery: re-run and
+  exact, or reported to every callback when every attempt fails).
 No device code is involved (GPU sanitizers are not available on the pool)."""
 import os
 import subprocess
@@ -64,12 +66,21 @@ def test_queue_many_producers_tsan():
                  ["-fsanitize=thread"], cxx=CLANG)
     out = _run([exe, "16", "500"], {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"})
     assert "8000/8000 answered, 0 wrong" in out
+    # engine-failure recovery: every 7th launch fails; each is re-run and
+    # every callback still gets its exact verdict (the binary checks that
+    # retried == recovered == injected and no callback saw an engine error)
+    out = _run([exe, "16", "500", "7"], {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"})
+    assert "8000/8000 answered, 0 wrong" in out and "injected 0," not in out, out
 
 
 def test_queue_many_producers_asan_ubsan():
     exe = _build(os.path.join(ROOT, "tests", "sanitize", "_build", "queue_asan"),
                  [os.path.join(CSRC, "coa_queue.cpp"), os.path.join(ROOT, "tests", "sanitize", "queue_tsan.cpp")],
                  ["-fsanitize=address,undefined", "-fno-sanitize-recover=all"])
-    out = _run([exe, "16", "500"], {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1",
-                                    "UBSAN_OPTIONS": "halt_on_error=1"})
+    env = {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1", "UBSAN_OPTIONS": "halt_on_error=1"}
+    out = _run([exe, "16", "500"], env)
     assert "8000/8000 answered, 0 wrong" in out
+    # every 5th launch fails and so does every retry: those windows' callbacks
+    # get the engine error (counted as failed windows), the rest are exact
+    out = _run([exe, "8", "300", "5", "1"], env)
+    assert "2400/2400 answered, 0 wrong" in out and "recovered 0" in out and "engine errors 0" not in out, out

@@ -38,7 +38,8 @@ def _compile(src):
         return obj, False
     cmd = [HIPCC] + COMMON + ["-c", path, "-o", obj]
     if src.endswith(".cpp"):
-        cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", "-I" + os.path.join(ROOT, "include"), "-c", path, "-o", obj]
+        cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include"), "-c",
+                   path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")

@@ -54,7 +54,8 @@ class QueueMetrics(ctypes.Structure):
     """coa_queue_metrics_t (include/coa_verify.h)."""
     _fields_ = [(n, ctypes.c_uint64) for n in ("requests", "windows", "signatures", "batches", "certificates",
                                                "digests", "max_window", "max_in_flight", "max_pending")] + \
-               [(n, ctypes.c_double) for n in ("wait_us_mean", "wait_us_p50", "wait_us_p99", "wait_us_max")]
+               [(n, ctypes.c_double) for n in ("wait_us_mean", "wait_us_p50", "wait_us_p99", "wait_us_max")] + \
+               [(n, ctypes.c_uint64) for n in ("retried_windows", "recovered_windows", "failed_windows")]
 
 
 # void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n)
@@ -89,6 +90,7 @@ def lib():
         "coa_self_test": ([ctypes.c_int, P64], ctypes.c_int),
         "coa_fe_rows_check_device": ([ctypes.c_int, vp, sz, vp, vp], ctypes.c_int),
         "coa_last_error": ([], ctypes.c_char_p),
+        "coa_engine_recoveries": ([P64, P64], ctypes.c_int),
         "coa_version": ([], ctypes.c_char_p),
         "coa_ed25519_verify_strict": ([P8, P8, P8], ctypes.c_int),
         "coa_ed25519_verify_strict_many": ([P8, sz, P8, P8, sz, P8], ctypes.c_int),
@@ -306,6 +308,14 @@ def device_ids():
 def shutdown():
     """Release every context (the next call re-initialises lazily)."""
     return _check(lib().coa_shutdown())
+
+
+def engine_recoveries():
+    """coa_engine_recoveries: contexts rebuilt and shards re-run after device
+    failures of host-pointer calls since the library loaded."""
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().coa_engine_recoveries(ctypes.byref(a), ctypes.byref(b)))
+    return {"contexts_rebuilt": a.value, "shards_rerun": b.value}
 
 
 def self_test(device=0):

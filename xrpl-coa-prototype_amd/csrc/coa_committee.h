@@ -72,6 +72,15 @@ struct CertInl {
 };
 hipError_t coa_launch_cert_verify_inl(const CertInl& ci, hipStream_t s);
 
+// Key-cache read gate of HIP device `device` (coa_runtime.cpp).  The
+// aggregation queue holds it from a certificate window's launch to that
+// window's completion (the kernels read the key tables asynchronously);
+// coa_committee_register waits until no window holds it and keeps new
+// windows out until the tables are rebuilt.  Release may come from another
+// thread than the acquire.
+extern "C" void coa_keycache_read_acquire(int device);
+extern "C" void coa_keycache_read_release(int device);
+
 hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s);
 hipError_t coa_launch_key_tables(const uint32_t* keys, uint32_t nk, uint32_t* tabs, hipStream_t s);
 // wide combs from the radix-256 key combs (tabs already built)

@@ -6,34 +6,41 @@
 // and launches them as a few large GPU calls.  Modelled on the reference's
 // SignatureService (crypto/src/lib.rs:222-250): a request channel in, a
 // per-request reply (here a C callback, which the Rust side maps onto a
-// oneshot channel).
+// oneshot channel: rust/crypto/src/service.rs).
 //
-// Pipeline (double buffering):
-//   producers   copy each request into their own intake shard (one per
-//               producer thread and queue, packed by kind: the arrays the
-//               engine's batched entry points take), under that shard's lock
-//               only -- with one shared window, eight producers contended
-//               down to ~1 M requests/s against ~4 M/s for one
-//               (tools/queue_probe.c)
+// Pipeline:
+//   producers   copy each request into an intake shard under that shard's
+//               lock only.  A queue has a fixed pool of kShards shards; a
+//               thread always uses shard (thread ordinal mod kShards), so
+//               memory is bounded whatever the number of threads or queues.
+//               The queue-wide pending count is told in steps (a shard's
+//               first item, then every kReport items), so producers do not
+//               share a written cache line per request
 //   collector   closes the window when `max_batch` items are pending, when
 //               the oldest request is `max_delay_us` old, or on flush, takes
-//               every shard's requests into it (the first by swapping, the
-//               others appended with their indices rebased) and hands it to
-//               the backend, which stages it in a free device
-//               slot and enqueues its copies and kernels on that slot's
-//               stream -- WITHOUT waiting for them; it then collects the next
-//               window, which is packed and launched while the previous one
-//               is still on the GPU
-//   completer   waits for the windows in launch order and answers every
-//               request of a window through its callback
-// The backend (coa_queue.h) is the HIP one (coa_queue_hip.cpp, two slots
-// per opened GPU) or, in the ThreadSanitizer build, a stub.
+//               every non-empty shard's window (a swap per shard -- the
+//               parts are never merged on the host: the backend packs them
+//               straight into its pinned staging) and hands the parts to the
+//               backend, which enqueues their copies and kernels on a free
+//               device slot's stream WITHOUT waiting; it then collects the
+//               next window, which is packed and launched while the previous
+//               one is still on the GPU
+//   completer   waits for the launches in order and answers every request
+//               through its callback.  A failed launch is retried on the
+//               backend's recovery context of each device in turn (its slot
+//               rebuilt meanwhile); only when every attempt failed do the
+//               callbacks get the engine error -- the reference's verify
+//               never fails for a reason other than the signature, and
+//               Core::run logs every error and continues
+//               (primary/src/core.rs:390-398).
+// The backend (coa_queue.h) is the HIP one (coa_queue_hip.cpp) or, in the
+// sanitizer and CPU tests, a stub.
 //
 // Metrics (coa_queue_metrics): per-kind request counts, window sizes,
-// windows in flight, pending depth, and the submit -> callback wait time of
-// every request (mean, max, p50/p99 from a log-spaced histogram) -- the
-// numbers needed to tune max_batch / max_delay_us against the serial
-// Core::run.
+// windows in flight, pending depth, retried / recovered / failed windows and
+// the submit -> callback wait time of every request (mean, max, p50/p99 from
+// a log-spaced histogram) -- the numbers needed to tune max_batch /
+// max_delay_us against the serial Core::run.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -50,84 +57,76 @@
 
 namespace {
 
-using clock_t_ = std::chrono::steady_clock;
+using coa_q::Launch;
+using coa_q::Window;
 
 enum Kind : uint8_t { K_VERIFY, K_BATCH, K_CERT, K_DIGEST };
 
+inline int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 struct Req {
-  Kind kind;
-  uint32_t idx;  // index among the window's requests of this kind
   coa_verdict_cb cb;
   void* user;
-  clock_t_::time_point t0;
-  uint32_t n = 1;  // K_VERIFY: consecutive signatures of the request
+  int64_t t0;      // submission time, ns
+  uint32_t idx;    // index among the part's requests of this kind
+  uint32_t n;      // K_VERIFY: consecutive signatures of the request
+  Kind kind;
+};
+
+constexpr size_t kShards = 64;  // intake shards per queue
+constexpr size_t kReport = 64;  // a shard tells the pending count every kReport items
+
+// One intake shard.  `reported` is the part of `items` already added to the
+// queue's pending count.
+struct alignas(64) Shard {
+  std::mutex mu;
+  std::unique_ptr<Window> w;
+  std::vector<Req> reqs;
+  size_t items = 0, reported = 0;
+  // a recycled window and request vector for the next take (capacity kept)
+  std::unique_ptr<Window> spare;
+  std::vector<Req> spare_reqs;
+};
+
+// One shard's requests inside a launch.
+struct Part {
+  std::unique_ptr<Window> w;
+  std::vector<Req> reqs;
+  uint32_t shard;
 };
 
 struct Flight {
-  std::unique_ptr<coa_q::Window> w;
-  std::vector<Req> reqs;
+  std::vector<Part> parts;
+  Launch L;
 };
-
-// One producer thread's intake for one queue.
-struct Shard {
-  std::mutex mu;
-  std::unique_ptr<coa_q::Window> w{new coa_q::Window()};
-  std::unique_ptr<coa_q::Window> next;  // a reset window for the next swap
-  std::vector<Req> reqs;
-  size_t items = 0;
-  Shard() { w->reset(); }
-};
-
-template <class T>
-void append(std::vector<T>& dst, const std::vector<T>& src) {
-  dst.insert(dst.end(), src.begin(), src.end());
-}
-// offsets array src (starting at 0) appended after dst's last entry
-void append_offs(std::vector<uint64_t>& dst, const std::vector<uint64_t>& src) {
-  const uint64_t base = dst.back();
-  for (size_t i = 1; i < src.size(); i++) dst.push_back(base + src[i]);
-}
-
-// Window `src` with requests `reqs` joins window `dst` with requests `dreqs`.
-void merge(coa_q::Window& dst, std::vector<Req>& dreqs, const coa_q::Window& src, const std::vector<Req>& reqs) {
-  const uint32_t bv = (uint32_t)dst.nv, bg = (uint32_t)dst.ng, bc = (uint32_t)dst.nc, bd = (uint32_t)dst.nd;
-  append(dst.v_msgs, src.v_msgs);
-  append(dst.v_pks, src.v_pks);
-  append(dst.v_sigs, src.v_sigs);
-  append(dst.g_msgs, src.g_msgs);
-  append(dst.g_pks, src.g_pks);
-  append(dst.g_sigs, src.g_sigs);
-  append_offs(dst.g_offs, src.g_offs);
-  append(dst.c_hdata, src.c_hdata);
-  append_offs(dst.c_hoff, src.c_hoff);
-  append(dst.c_ids, src.c_ids);
-  append(dst.c_origins, src.c_origins);
-  append(dst.c_hsigs, src.c_hsigs);
-  append(dst.c_rounds, src.c_rounds);
-  append(dst.c_pks, src.c_pks);
-  append(dst.c_sigs, src.c_sigs);
-  append_offs(dst.c_voff, src.c_voff);
-  append(dst.d_data, src.d_data);
-  append_offs(dst.d_offs, src.d_offs);
-  dst.nv += src.nv;
-  dst.ng += src.ng;
-  dst.nc += src.nc;
-  dst.nd += src.nd;
-  for (Req r : reqs) {
-    r.idx += r.kind == K_VERIFY ? bv : r.kind == K_BATCH ? bg : r.kind == K_CERT ? bc : bd;
-    dreqs.push_back(r);
-  }
-}
 
 std::atomic<uint64_t> g_queue_ids{1};
+std::atomic<uint32_t> g_thread_ord{0};
 
-// Wait-time histogram: bucket b covers [2^(b/8), 2^((b+1)/8)) microseconds.
+uint32_t thread_ordinal() {
+  static thread_local const uint32_t ord = g_thread_ord.fetch_add(1, std::memory_order_relaxed);
+  return ord;
+}
+
+// Wait-time histogram: bucket 0 is < 1 us; bucket 8e + m + 1 covers
+// [2^e (1 + m/8), 2^e (1 + (m+1)/8)) microseconds (the exponent and the top
+// three mantissa bits of the double: no log per request).
 constexpr int HB = 8 * 40;
 int wait_bucket(double us) {
-  if (us < 1.0) return 0;
-  return std::min(HB - 1, (int)(8.0 * std::log2(us)) + 1);
+  if (!(us >= 1.0)) return 0;
+  uint64_t bits;
+  std::memcpy(&bits, &us, 8);
+  const int e = (int)((bits >> 52) & 0x7ff) - 1023, m = (int)((bits >> 49) & 7);
+  return std::min(HB - 1, 8 * e + m + 1);
 }
-double bucket_mid(int b) { return b == 0 ? 0.5 : std::exp2((b - 0.5) / 8.0); }
+double bucket_mid(int b) {
+  if (b == 0) return 0.5;
+  const int e = (b - 1) / 8, m = (b - 1) % 8;
+  return std::ldexp(1.0 + (m + 0.5) / 8.0, e);
+}
 
 }  // namespace
 
@@ -136,55 +135,45 @@ struct coa_queue {
   std::chrono::microseconds max_delay{500};
   std::unique_ptr<coa_q::Backend> be;
   const uint64_t id = g_queue_ids.fetch_add(1);
+  std::unique_ptr<Shard[]> shards{new Shard[kShards]};
 
   std::mutex mu;
   std::condition_variable cv;         // collector: requests arrived / flush / stop
   std::condition_variable flight_cv;  // completer: a window was launched / stop
   std::condition_variable idle_cv;    // flush: everything answered
-  std::vector<std::unique_ptr<coa_q::Window>> spare;  // answered windows, recycled (capacity kept)
-  std::atomic<int64_t> pend{0};  // items submitted and not yet taken (briefly < 0 while a take races an arrival)
+  std::atomic<int64_t> pend{0};  // reported items not yet taken (briefly < 0 while a take races a report)
   std::atomic<bool> stop{false};
-  clock_t_::time_point oldest;
+  std::chrono::steady_clock::time_point oldest;
   std::deque<Flight> flight;  // launched, not yet answered (launch order)
   size_t busy = 0;            // windows taken by the collector and not yet answered
   bool flush = false, collector_done = false;
 
-  std::mutex shards_mu;
-  std::vector<std::unique_ptr<Shard>> shards;
-
   // metrics (under mu, except m_max_pending)
   uint64_t m_requests = 0, m_windows = 0, m_sig = 0, m_batch = 0, m_cert = 0, m_dig = 0;
   uint64_t m_max_window = 0, m_max_in_flight = 0;
+  uint64_t m_retried = 0, m_recovered = 0, m_failed = 0;
   std::atomic<int64_t> m_max_pending{0};
   double m_wait_sum = 0.0, m_wait_max = 0.0;
   uint64_t m_hist[HB] = {};
 
   std::thread collector, completer;
 
+  coa_queue() {
+    for (size_t i = 0; i < kShards; i++) {
+      shards[i].w.reset(new Window());
+      shards[i].w->reset();
+    }
+  }
+
   void start() {
     collector = std::thread([this] { collect(); });
     completer = std::thread([this] { answer(); });
   }
 
-  // The calling thread's shard (created on its first submission).
-  Shard* my_shard() {
-    struct Entry {
-      uint64_t qid;
-      Shard* sh;
-    };
-    thread_local Entry cache[4] = {};
-    thread_local unsigned next_slot = 0;
-    for (const Entry& e : cache)
-      if (e.qid == id) return e.sh;
-    std::lock_guard<std::mutex> l(shards_mu);
-    shards.emplace_back(new Shard());
-    Shard* sh = shards.back().get();
-    cache[next_slot++ & 3] = {id, sh};
-    return sh;
-  }
+  Shard& my_shard() { return shards[thread_ordinal() % kShards]; }
 
-  // A request of `items` items joined a shard (its lock released).  Wakes the
-  // collector only on the two edges it waits for: the first pending item
+  // `items` more items were reported by a shard (its lock released).  Wakes
+  // the collector only on the two edges it waits for: the first pending item
   // (arms the deadline) and max_batch reached.
   void arrived(size_t items) {
     const int64_t old = pend.fetch_add((int64_t)items), now_pend = old + (int64_t)items;
@@ -195,55 +184,48 @@ struct coa_queue {
     const bool crossed = old < (int64_t)max_batch && now_pend >= (int64_t)max_batch;
     if (first || crossed) {
       std::lock_guard<std::mutex> l(mu);
-      if (first) oldest = clock_t_::now();
+      if (first) oldest = std::chrono::steady_clock::now();
       cv.notify_one();
     }
   }
 
-  // Shards' pending requests into f (the collector, no queue lock): whole
+  // Non-empty shards' windows into f (the collector, no queue lock): whole
   // shards, starting one shard further each window, until f holds max_batch
   // items; the rest waits for the next window (which the collector then
   // closes at once: pend is still >= max_batch).
   size_t rr = 0;
   void gather(Flight& f) {
-    std::vector<Shard*> snap;
-    {
-      std::lock_guard<std::mutex> l(shards_mu);
-      for (auto& s : shards) snap.push_back(s.get());
-    }
-    const size_t ns = snap.size(), start = ns ? rr++ % ns : 0;
+    const size_t start = rr++ % kShards;
     size_t taken = 0;
-    for (size_t k = 0; k < ns && taken < max_batch; k++) {
-      Shard* sh = snap[(start + k) % ns];
-      std::unique_ptr<coa_q::Window> w;
-      std::vector<Req> reqs;
-      size_t items;
+    for (size_t k = 0; k < kShards && taken < max_batch; k++) {
+      const uint32_t si = (uint32_t)((start + k) % kShards);
+      Shard& sh = shards[si];
+      Part p;
+      size_t items, rep;
       {
-        std::lock_guard<std::mutex> l(sh->mu);
-        if (sh->items == 0) continue;
-        w = std::move(sh->w);
-        if (sh->next) {
-          sh->w = std::move(sh->next);
+        std::lock_guard<std::mutex> l(sh.mu);
+        if (sh.items == 0) continue;
+        p.w = std::move(sh.w);
+        p.reqs.swap(sh.reqs);
+        if (sh.spare) {
+          sh.w = std::move(sh.spare);
         } else {
-          sh->w.reset(new coa_q::Window());
-          sh->w->reset();
+          sh.w.reset(new Window());
+          sh.w->reset();
         }
-        reqs.swap(sh->reqs);
-        items = sh->items;
-        sh->items = 0;
+        sh.reqs.swap(sh.spare_reqs);
+        items = sh.items;
+        rep = sh.reported;
+        sh.items = sh.reported = 0;
       }
-      pend.fetch_sub((int64_t)items);
+      pend.fetch_sub((int64_t)rep);
       taken += items;
-      if (f.reqs.empty()) {  // the first shard's window becomes the launch window
-        std::swap(f.w, w);
-        f.reqs.swap(reqs);
-      } else {
-        merge(*f.w, f.reqs, *w, reqs);
-      }
-      w->reset();
-      std::lock_guard<std::mutex> l(sh->mu);
-      if (!sh->next) sh->next = std::move(w);
+      p.shard = si;
+      f.parts.push_back(std::move(p));
     }
+    f.L.parts.clear();
+    for (Part& p : f.parts) f.L.parts.push_back(p.w.get());
+    f.L.tally();
   }
 
   void collect() {
@@ -258,25 +240,19 @@ struct coa_queue {
       flush = false;
       busy++;  // before the take: flush must not see pend == 0 and busy == 0 meanwhile
       Flight f;
-      if (spare.empty()) {
-        f.w.reset(new coa_q::Window());
-      } else {
-        f.w = std::move(spare.back());
-        spare.pop_back();
-      }
-      f.w->reset();
       l.unlock();
       gather(f);
       l.lock();
-      if (f.reqs.empty()) {  // every pending item was taken by an earlier window
+      if (f.parts.empty()) {  // every pending item was taken by an earlier window
         busy--;
-        spare.push_back(std::move(f.w));
         if (busy == 0 && pend.load() <= 0) idle_cv.notify_all();
         continue;
       }
-      m_max_window = std::max<uint64_t>(m_max_window, f.w->nv + f.w->c_voff.back() + f.w->g_offs.back() + f.w->nd);
+      m_max_window = std::max<uint64_t>(m_max_window, f.L.items());
       l.unlock();
-      be->launch(*f.w);  // stages and enqueues; blocks only while every slot is busy
+      f.L.reset_outputs();
+      f.L.attempts = 1;
+      be->launch(f.L);  // stages and enqueues; blocks only while every slot is busy
       l.lock();
       m_windows++;
       flight.push_back(std::move(f));
@@ -287,6 +263,20 @@ struct coa_queue {
     flight_cv.notify_one();
   }
 
+  // A launch that failed on the device (a HIP error or an allocation
+  // failure; not "no device" or bad arguments): retried on the recovery
+  // context of each device in turn (the first retry on the next device),
+  // until one succeeds.
+  static bool recoverable(int rc) { return rc == COA_EHIP || rc == COA_ENOMEM; }
+  void recover(Launch& L) {
+    const int n = std::max(1, be->devices());
+    for (int a = 1; a <= n && recoverable(L.rc); a++) {
+      L.reset_outputs();
+      L.attempts++;
+      be->retry(L, a);
+    }
+  }
+
   void answer() {
     std::unique_lock<std::mutex> l(mu);
     for (;;) {
@@ -295,32 +285,55 @@ struct coa_queue {
       Flight f = std::move(flight.front());
       flight.pop_front();
       l.unlock();
-      be->complete(*f.w);
-      const coa_q::Window& w = *f.w;
-      std::vector<double> waits;
-      waits.reserve(f.reqs.size());
-      for (const Req& r : f.reqs) {
-        const auto now = clock_t_::now();
-        waits.push_back(std::chrono::duration<double, std::micro>(now - r.t0).count());
-        switch (r.kind) {
-          case K_VERIFY: r.cb(r.user, w.rc, w.v_out.data() + r.idx, r.n); break;
-          case K_BATCH: r.cb(r.user, w.rc, w.g_out.data() + r.idx, 1); break;
-          case K_CERT: r.cb(r.user, w.rc, w.c_out.data() + r.idx, 1); break;
-          case K_DIGEST: r.cb(r.user, w.rc, w.d_out.data() + (size_t)r.idx * 32, 32); break;
+      be->complete(f.L);
+      const bool retried = recoverable(f.L.rc);
+      if (retried) recover(f.L);
+      const int rc = f.L.rc;
+      // callbacks; wait times from a clock read every 32 requests
+      uint64_t hist[HB] = {};
+      double wsum = 0.0, wmax = 0.0;
+      uint64_t nreq = 0;
+      int64_t tnow = now_ns();
+      for (const Part& p : f.parts) {
+        const Window& w = *p.w;
+        for (const Req& r : p.reqs) {
+          if ((nreq & 31) == 31) tnow = now_ns();
+          nreq++;
+          const double us = (double)(tnow - r.t0) * 1e-3;
+          wsum += us;
+          wmax = std::max(wmax, us);
+          hist[wait_bucket(us)]++;
+          switch (r.kind) {
+            case K_VERIFY: r.cb(r.user, rc, w.v_out.data() + r.idx, r.n); break;
+            case K_BATCH: r.cb(r.user, rc, w.g_out.data() + r.idx, 1); break;
+            case K_CERT: r.cb(r.user, rc, w.c_out.data() + r.idx, 1); break;
+            case K_DIGEST: r.cb(r.user, rc, w.d_out.data() + (size_t)r.idx * 32, 32); break;
+          }
         }
       }
-      l.lock();
-      for (double us : waits) {
-        m_wait_sum += us;
-        m_wait_max = std::max(m_wait_max, us);
-        m_hist[wait_bucket(us)]++;
+      // recycle each part's window and request vector into its shard
+      for (Part& p : f.parts) {
+        p.w->reset();
+        p.reqs.clear();
+        Shard& sh = shards[p.shard];
+        std::lock_guard<std::mutex> g(sh.mu);
+        if (!sh.spare) sh.spare = std::move(p.w);
+        if (sh.spare_reqs.capacity() < p.reqs.capacity()) sh.spare_reqs.swap(p.reqs);
       }
-      m_requests += f.reqs.size();
-      m_sig += w.nv;
-      m_batch += w.ng;
-      m_cert += w.nc;
-      m_dig += w.nd;
-      if (spare.size() < 8) spare.push_back(std::move(f.w));
+      l.lock();
+      for (int b = 0; b < HB; b++) m_hist[b] += hist[b];
+      m_wait_sum += wsum;
+      m_wait_max = std::max(m_wait_max, wmax);
+      m_requests += nreq;
+      m_sig += f.L.nv;
+      m_batch += f.L.ng;
+      m_cert += f.L.nc;
+      m_dig += f.L.nd;
+      if (retried) {
+        m_retried++;
+        if (rc == COA_OK) m_recovered++;
+      }
+      if (rc != COA_OK) m_failed++;
       busy--;
       if (busy == 0 && pend.load() <= 0) idle_cv.notify_all();
     }
@@ -340,6 +353,28 @@ struct coa_queue {
   }
 };
 
+namespace {
+void submitted(coa_queue* q, Shard& sh, std::unique_lock<std::mutex>& sl, Kind kind, uint32_t idx, uint32_t n,
+               coa_verdict_cb cb, void* user, size_t items) {
+  sh.reqs.push_back(Req{cb, user, now_ns(), idx, n, kind});
+  sh.items += items;
+  size_t delta = 0;
+  if (sh.reported == 0 || sh.items - sh.reported >= kReport) {
+    delta = sh.items - sh.reported;
+    sh.reported = sh.items;
+  }
+  sl.unlock();
+  if (delta) q->arrived(delta);
+}
+
+template <size_t N>
+inline void put(std::vector<uint8_t>& v, const uint8_t* src) {
+  const size_t at = v.size();
+  v.resize(at + N);
+  std::memcpy(v.data() + at, src, N);
+}
+}  // namespace
+
 extern "C" {
 
 coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
@@ -354,30 +389,21 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
 // The submissions: the request goes into the calling thread's shard under
 // that shard's lock; then the queue's pending count (and, on an edge, the
 // collector) learns of it.
-#define COA_Q_INTAKE(q)                         \
-  Shard* sh = (q)->my_shard();                  \
-  std::unique_lock<std::mutex> sl(sh->mu);      \
-  if ((q)->stop.load()) return COA_EINVAL;      \
-  coa_q::Window& w = *sh->w;
+#define COA_Q_INTAKE(q)                        \
+  Shard& sh = (q)->my_shard();                 \
+  std::unique_lock<std::mutex> sl(sh.mu);      \
+  if ((q)->stop.load()) return COA_EINVAL;     \
+  Window& w = *sh.w;
 
-namespace {
-void submitted(coa_queue* q, Shard* sh, std::unique_lock<std::mutex>& sl, Req r, size_t items) {
-  r.t0 = clock_t_::now();
-  sh->reqs.push_back(r);
-  sh->items += items;
-  sl.unlock();
-  q->arrived(items);
-}
-}  // namespace
 
 int coa_queue_submit_verify(coa_queue* q, const uint8_t msg[32], const uint8_t pk[32], const uint8_t sig[64],
                             coa_verdict_cb cb, void* user) {
   if (!q || !msg || !pk || !sig || !cb) return COA_EINVAL;
   COA_Q_INTAKE(q)
-  w.v_msgs.insert(w.v_msgs.end(), msg, msg + 32);
-  w.v_pks.insert(w.v_pks.end(), pk, pk + 32);
-  w.v_sigs.insert(w.v_sigs.end(), sig, sig + 64);
-  submitted(q, sh, sl, {K_VERIFY, (uint32_t)w.nv++, cb, user, {}}, 1);
+  put<32>(w.v_msgs, msg);
+  put<32>(w.v_pks, pk);
+  put<64>(w.v_sigs, sig);
+  submitted(q, sh, sl, K_VERIFY, (uint32_t)w.nv++, 1, cb, user, 1);
   return COA_OK;
 }
 
@@ -388,10 +414,9 @@ int coa_queue_submit_verify_many(coa_queue* q, const uint8_t* msgs, const uint8_
   w.v_msgs.insert(w.v_msgs.end(), msgs, msgs + n * 32);
   w.v_pks.insert(w.v_pks.end(), pks, pks + n * 32);
   w.v_sigs.insert(w.v_sigs.end(), sigs, sigs + n * 64);
-  Req r{K_VERIFY, (uint32_t)w.nv, cb, user, {}};
-  r.n = (uint32_t)n;
+  const uint32_t idx = (uint32_t)w.nv;
   w.nv += n;
-  submitted(q, sh, sl, r, n);
+  submitted(q, sh, sl, K_VERIFY, idx, (uint32_t)n, cb, user, n);
   return COA_OK;
 }
 
@@ -399,13 +424,13 @@ int coa_queue_submit_batch(coa_queue* q, const uint8_t msg[32], const uint8_t* p
                            coa_verdict_cb cb, void* user) {
   if (!q || !msg || (n && (!pks || !sigs)) || !cb) return COA_EINVAL;
   COA_Q_INTAKE(q)
-  w.g_msgs.insert(w.g_msgs.end(), msg, msg + 32);
+  put<32>(w.g_msgs, msg);
   if (n) {
     w.g_pks.insert(w.g_pks.end(), pks, pks + n * 32);
     w.g_sigs.insert(w.g_sigs.end(), sigs, sigs + n * 64);
   }
   w.g_offs.push_back(w.g_offs.back() + n);
-  submitted(q, sh, sl, {K_BATCH, (uint32_t)w.ng++, cb, user, {}}, n ? n : 1);
+  submitted(q, sh, sl, K_BATCH, (uint32_t)w.ng++, 1, cb, user, n ? n : 1);
   return COA_OK;
 }
 
@@ -419,16 +444,16 @@ int coa_queue_submit_certificate(coa_queue* q, const uint8_t* header_data, size_
   COA_Q_INTAKE(q)
   if (header_len) w.c_hdata.insert(w.c_hdata.end(), header_data, header_data + header_len);
   w.c_hoff.push_back(w.c_hdata.size());
-  w.c_ids.insert(w.c_ids.end(), id, id + 32);
-  w.c_origins.insert(w.c_origins.end(), origin, origin + 32);
-  w.c_hsigs.insert(w.c_hsigs.end(), header_sig, header_sig + 64);
+  put<32>(w.c_ids, id);
+  put<32>(w.c_origins, origin);
+  put<64>(w.c_hsigs, header_sig);
   w.c_rounds.push_back(round);
   if (n_votes) {
     w.c_pks.insert(w.c_pks.end(), vote_pks, vote_pks + n_votes * 32);
     w.c_sigs.insert(w.c_sigs.end(), vote_sigs, vote_sigs + n_votes * 64);
   }
   w.c_voff.push_back(w.c_voff.back() + n_votes);
-  submitted(q, sh, sl, {K_CERT, (uint32_t)w.nc++, cb, user, {}}, 1 + n_votes);
+  submitted(q, sh, sl, K_CERT, (uint32_t)w.nc++, 1, cb, user, 1 + n_votes);
   return COA_OK;
 }
 
@@ -437,7 +462,7 @@ int coa_queue_submit_digest(coa_queue* q, const uint8_t* data, size_t len, coa_v
   COA_Q_INTAKE(q)
   if (len) w.d_data.insert(w.d_data.end(), data, data + len);
   w.d_offs.push_back(w.d_data.size());
-  submitted(q, sh, sl, {K_DIGEST, (uint32_t)w.nd++, cb, user, {}}, 1);
+  submitted(q, sh, sl, K_DIGEST, (uint32_t)w.nd++, 1, cb, user, 1);
   return COA_OK;
 }
 
@@ -485,6 +510,9 @@ int coa_queue_metrics(coa_queue* q, coa_queue_metrics_t* out) {
   out->wait_us_p50 = q->percentile(0.50);
   out->wait_us_p99 = q->percentile(0.99);
   out->wait_us_max = q->m_wait_max;
+  out->retried_windows = q->m_retried;
+  out->recovered_windows = q->m_recovered;
+  out->failed_windows = q->m_failed;
   return COA_OK;
 }
 

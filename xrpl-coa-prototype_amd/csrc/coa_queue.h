@@ -1,8 +1,8 @@
 // Internal interface between the aggregation queue (coa_queue.cpp: request
-// intake, windows, callbacks, metrics; no HIP) and its launch backend
-// (coa_queue_hip.cpp: pinned staging, HIP streams and events over the
-// device-resident entry points; a test build links a stub instead,
-// tests/sanitize/queue_tsan.cpp).
+// intake, windows, callbacks, metrics, recovery; no HIP) and its launch
+// backend (coa_queue_hip.cpp: pinned staging, HIP streams and events over the
+// device-resident entry points; the sanitizer and CPU tests link a stub
+// instead, tests/sanitize/queue_tsan.cpp).
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
@@ -13,8 +13,11 @@
 
 namespace coa_q {
 
-// One launch window: every request the collector took in one go, packed
-// contiguously by kind.  The backend fills the outputs and `rc`.
+// One intake shard's requests, packed contiguously by kind (the arrays the
+// engine's batched entry points take).  A launch takes the windows of every
+// shard that had requests (its "parts") and the backend packs them straight
+// into its pinned staging block -- the parts are never merged on the host.
+// The backend fills each part's outputs.
 struct Window {
   // header / vote signatures (coa_ed25519_verify_strict semantics)
   size_t nv = 0;
@@ -35,10 +38,17 @@ struct Window {
   std::vector<uint8_t> d_data;
   std::vector<uint64_t> d_offs;  // nd + 1
   std::vector<uint8_t> d_out;    // nd x 32
-  int rc = COA_OK;               // engine status of the window (negative = failure)
-  int slot = -1;                 // backend slot the window ran on
 
-  // Empty again for the next window, keeping every vector's capacity (the
+  size_t items() const { return nv + nd + nc + (c_voff.empty() ? 0 : c_voff.back()) + g_offs.back(); }
+  // Outputs sized and set to "failed" (verdict Err, all certificate bits,
+  // zero digests) before a launch or a retry.
+  void reset_outputs() {
+    v_out.assign(nv, 1);
+    g_out.assign(ng, 1);
+    c_out.assign(nc, 7);
+    d_out.assign(nd * 32, 0);
+  }
+  // Empty again for the next intake, keeping every vector's capacity (the
   // queue recycles answered windows, so a window fills without reallocating
   // under the intake lock).
   void reset() {
@@ -51,21 +61,62 @@ struct Window {
     c_hoff.push_back(0);
     c_voff.push_back(0);
     d_offs.push_back(0);
+  }
+};
+
+// The parts one launch takes, with their totals.
+struct Launch {
+  std::vector<Window*> parts;
+  size_t nv = 0, ng = 0, nc = 0, nd = 0;
+  size_t nvotes = 0;   // certificate votes
+  size_t hbytes = 0;   // certificate header bytes
+  size_t dbytes = 0;   // digest input bytes
+  size_t gvotes = 0;   // bare-batch votes
+  int rc = COA_OK;     // engine status (negative = failure), set by the backend
+  int slot = -1;       // backend slot the launch ran on
+  int attempts = 0;    // launches of this window (1 + retries)
+  void tally() {
+    nv = ng = nc = nd = nvotes = hbytes = dbytes = gvotes = 0;
+    for (const Window* w : parts) {
+      nv += w->nv;
+      ng += w->ng;
+      nc += w->nc;
+      nd += w->nd;
+      nvotes += w->c_voff.back();
+      hbytes += w->c_hdata.size();
+      dbytes += w->d_data.size();
+      gvotes += w->g_offs.back();
+    }
+  }
+  size_t items() const { return nv + nd + nc + nvotes + gvotes; }
+  void reset_outputs() {
+    for (Window* w : parts) w->reset_outputs();
     rc = COA_OK;
-    slot = -1;
   }
 };
 
 class Backend {
  public:
   virtual ~Backend() {}
-  // Copies the window's inputs to a free slot and enqueues its device work;
-  // blocks while every slot is still busy with an earlier window (the
-  // double buffering: at most `slots()` windows in flight).
-  virtual void launch(Window& w) = 0;
-  // Waits for the window's work and fills its outputs; frees its slot.
-  virtual void complete(Window& w) = 0;
+  // Copies the launch's inputs to a free slot and enqueues its device work;
+  // blocks while every slot is still busy with an earlier launch (at most
+  // `slots()` launches in flight).  Sets l.slot and, on a failure already
+  // known at enqueue time, l.rc.
+  virtual void launch(Launch& l) = 0;
+  // Waits for the launch's work and fills its outputs (and l.rc); frees its
+  // slot.  On a failure the slot's device work has drained and the slot has
+  // been rebuilt (a new stream and event, its buffers freed and regrown on
+  // demand -- in the same process, never an exec) before it is freed.
+  virtual void complete(Launch& l) = 0;
+  // Engine-failure recovery, called by the completion thread after a failed
+  // launch (l.slot = the slot it failed on): re-runs the launch synchronously
+  // on the recovery context of the device `attempt` places after the failed
+  // one -- its own stream and buffers, used only here, so a retry never waits
+  // for a slot that a later launch holds.  Sets l.rc.
+  virtual void retry(Launch& l, int attempt) = 0;
   virtual int slots() const = 0;
+  // Number of device contexts retries can go to (at least 1).
+  virtual int devices() const = 0;
 };
 
 // The HIP backend (coa_queue_hip.cpp), or a test stub.

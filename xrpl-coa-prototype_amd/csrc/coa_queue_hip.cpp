@@ -1,12 +1,14 @@
-// HIP launch backend of the aggregation queue (coa_queue.h): two device
-// slots per opened GPU context, each with its own non-blocking stream, event,
-// page-locked staging and device buffers.  launch() packs a window into one
-// pinned block, issues ONE host-to-device copy, the engine's device-resident
-// entry points (asynchronous with an explicit workspace, no engine lock) and
-// ONE device-to-host copy on the slot's stream, records an event and returns;
-// complete() waits for the event.  So while window N runs on slot A, window
-// N + 1 is packed and enqueued on slot B, and the copies of one window overlap
-// the kernels of the other.
+// HIP launch backend of the aggregation queue (coa_queue.h): device slots
+// (two per opened GPU context by default), each with its own non-blocking
+// stream, event, page-locked staging and device buffers.  launch() packs the
+// launch's parts (one per intake shard) straight into one pinned block --
+// the parts are never merged first -- issues ONE host-to-device copy, the
+// engine's device-resident entry points (asynchronous with an explicit
+// workspace, no engine lock) and ONE device-to-host copy on the slot's
+// stream, records an event and returns; complete() waits for the event and
+// scatters the outputs back to the parts.  So while window N runs on slot A,
+// window N + 1 is packed and enqueued on slot B, and the copies of one window
+// overlap the kernels of the other.
 //
 // Per kind:
 //   signatures    coa_ed25519_verify_strict_many_device (Signature::verify)
@@ -15,12 +17,24 @@
 //                 the exact random-linear-combination check or carry a key
 //                 outside the registered committee are re-decided in
 //                 complete() through coa_certificate_verify_many, as the
-//                 host-pointer entry point does
+//                 host-pointer entry point does.  A window with certificates
+//                 holds its device's key-cache read gate from launch to
+//                 completion, so coa_committee_register never rewrites the
+//                 key tables under a running window
 //   digests       coa_sha512_many_device (worker/src/processor.rs:38)
 //   vote batches  coa_ed25519_verify_batch_groups in complete() (host
 //                 pointers; bare batches are rare next to whole certificates)
+//
+// Engine-failure recovery: a failed launch drains its stream (the error code
+// kept), its slot is rebuilt (new stream and event, device buffers freed and
+// regrown on demand) and freed; the queue then re-runs the window through
+// retry() on the recovery context of another device (one per device, used
+// only by retries).  COA_QUEUE_FAULT=<k> makes every k-th window's launch
+// fail after its input copy is enqueued (fault injection for the recovery
+// tests; never set in production).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -48,8 +62,9 @@ struct Slot {
   void* ws = nullptr;    // device workspace (verify + certificates)
   size_t cap_hin = 0, cap_hout = 0, cap_din = 0, cap_dout = 0, cap_ws = 0;
   bool busy = false;
-  bool launched = false;  // device work was enqueued (else complete() skips the wait)
-  // output offsets of the current window
+  bool launched = false;  // device work was enqueued (complete() must drain it)
+  bool gate = false;      // holds the device's key-cache read gate
+  // output offsets of the current launch
   size_t o_v = 0, o_c = 0, o_d = 0;
 };
 
@@ -74,68 +89,103 @@ hipError_t grow_dev(void*& p, size_t& cap, size_t want) {
   return e;
 }
 
+// New stream and event for a slot; its device buffers are freed (regrown by
+// the next launch).  The pinned host blocks are kept.
+int make_stream(Slot& sl) {
+  if (hipSetDevice(sl.dev) != hipSuccess) return COA_EHIP;
+  if (sl.s) {
+    (void)hipStreamSynchronize(sl.s);
+    (void)hipStreamDestroy(sl.s);
+    sl.s = nullptr;
+  }
+  if (sl.ev) {
+    (void)hipEventDestroy(sl.ev);
+    sl.ev = nullptr;
+  }
+  for (void** p : {&sl.din, &sl.dout, &sl.ws})
+    if (*p) {
+      (void)hipFree(*p);
+      *p = nullptr;
+    }
+  sl.cap_din = sl.cap_dout = sl.cap_ws = 0;
+  (void)hipGetLastError();  // a failed launch's error is not sticky for the new stream
+  if (hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess)
+    return COA_EHIP;
+  return COA_OK;
+}
+
+void free_slot(Slot& sl) {
+  if (sl.dev < 0) return;
+  (void)hipSetDevice(sl.dev);
+  if (sl.s) (void)hipStreamSynchronize(sl.s);
+  if (sl.hin) (void)hipHostFree(sl.hin);
+  if (sl.hout) (void)hipHostFree(sl.hout);
+  if (sl.din) (void)hipFree(sl.din);
+  if (sl.dout) (void)hipFree(sl.dout);
+  if (sl.ws) (void)hipFree(sl.ws);
+  if (sl.ev) (void)hipEventDestroy(sl.ev);
+  if (sl.s) (void)hipStreamDestroy(sl.s);
+}
+
 class HipBackend : public coa_q::Backend {
  public:
   ~HipBackend() override {
-    for (Slot& sl : slots_) {
-      if (sl.dev < 0) continue;
-      (void)hipSetDevice(sl.dev);
-      if (sl.s) (void)hipStreamSynchronize(sl.s);
-      if (sl.hin) (void)hipHostFree(sl.hin);
-      if (sl.hout) (void)hipHostFree(sl.hout);
-      if (sl.din) (void)hipFree(sl.din);
-      if (sl.dout) (void)hipFree(sl.dout);
-      if (sl.ws) (void)hipFree(sl.ws);
-      if (sl.ev) (void)hipEventDestroy(sl.ev);
-      if (sl.s) (void)hipStreamDestroy(sl.s);
-    }
+    for (Slot& sl : slots_) free_slot(sl);
+    for (Slot& sl : rescue_) free_slot(sl);
   }
 
   int slots() const override { return (int)slots_.size(); }
+  int devices() const override { return std::max<int>(1, (int)devs_.size()); }
 
-  void launch(coa_q::Window& w) override {
-    w.v_out.assign(w.nv, 1);
-    w.g_out.assign(w.ng, 1);
-    w.c_out.assign(w.nc, 7);
-    w.d_out.assign(w.nd * 32, 0);
+  void launch(coa_q::Launch& L) override {
     if (!ready()) {
-      w.rc = init_rc_;
+      L.rc = init_rc_;
       return;
     }
     Slot* sl;
+    bool inject = false;
     {
       std::unique_lock<std::mutex> l(m_);
       const size_t k = next_++ % slots_.size();
       cv_.wait(l, [&] { return !slots_[k].busy; });
       slots_[k].busy = true;
-      w.slot = (int)k;
+      L.slot = (int)k;
       sl = &slots_[k];
+      inject = fault_every_ && ++launches_ % fault_every_ == 0;
     }
     sl->launched = false;
-    w.rc = enqueue(*sl, w);
+    L.rc = enqueue(*sl, L, inject);
   }
 
-  void complete(coa_q::Window& w) override {
-    if (w.slot < 0) return;  // never staged (no device)
-    Slot& sl = slots_[w.slot];
-    if (w.rc == COA_OK && sl.launched) {
-      const hipError_t e = hipEventSynchronize(sl.ev);
-      if (e != hipSuccess) w.rc = COA_EHIP;
-    }
-    if (w.rc == COA_OK) {
-      const uint8_t* h = static_cast<const uint8_t*>(sl.hout);
-      if (w.nv) std::memcpy(w.v_out.data(), h + sl.o_v, w.nv);
-      if (w.nd) {
-        for (size_t i = 0; i < w.nd; i++) std::memcpy(&w.d_out[i * 32], h + sl.o_d + i * 64, 32);
-      }
-      if (w.nc) w.rc = resolve_certs(w, reinterpret_cast<const uint32_t*>(h + sl.o_c));
-      if (w.rc == COA_OK && w.ng)
-        w.rc = coa_ed25519_verify_batch_groups(w.g_msgs.data(), w.g_pks.data(), w.g_sigs.data(), w.g_offs.data(),
-                                               w.ng, w.g_out.data(), 0);
-    }
+  void complete(coa_q::Launch& L) override {
+    if (L.slot < 0) return;  // never staged (no device)
+    Slot& sl = slots_[L.slot];
+    finish(sl, L);
+    if (L.rc != COA_OK) (void)make_stream(sl);  // rebuilt before reuse
     std::lock_guard<std::mutex> l(m_);
     sl.busy = false;
     cv_.notify_all();
+  }
+
+  void retry(coa_q::Launch& L, int attempt) override {
+    if (!ready() || devs_.empty()) {
+      L.rc = init_rc_ != COA_OK ? init_rc_ : COA_ENODEVICE;
+      return;
+    }
+    size_t pos = 0;
+    if (L.slot >= 0)
+      for (size_t i = 0; i < devs_.size(); i++)
+        if (devs_[i] == slots_[L.slot].dev) pos = i;
+    Slot& sl = rescue_[(pos + (size_t)attempt) % devs_.size()];
+    if (!sl.s && make_stream(sl) != COA_OK) {
+      L.rc = COA_EHIP;
+      return;
+    }
+    sl.launched = false;
+    L.rc = enqueue(sl, L, false);
+    finish(sl, L);
+    if (L.rc != COA_OK) (void)make_stream(sl);
   }
 
  private:
@@ -149,100 +199,159 @@ class HipBackend : public coa_q::Backend {
       init_rc_ = n < 0 ? n : COA_ENODEVICE;
       return false;
     }
-    // device slots per GPU: windows in flight at once (COA_QUEUE_SLOTS,
+    const int nctx = std::min(n, 64);
+    // device slots per context: windows in flight at once (COA_QUEUE_SLOTS,
     // 1..8; tools/queue_probe.c measures the choice)
     size_t per = COA_QUEUE_SLOTS_DEFAULT;
     if (const char* e = getenv("COA_QUEUE_SLOTS")) {
       const int v = atoi(e);
       if (v >= 1 && v <= 8) per = (size_t)v;
     }
-    slots_.resize(per * (size_t)std::min(n, 64));
+    if (const char* e = getenv("COA_QUEUE_FAULT")) fault_every_ = strtoull(e, nullptr, 10);
+    slots_.resize(per * (size_t)nctx);
     for (size_t k = 0; k < slots_.size(); k++) {
-      Slot& sl = slots_[k];
-      sl.dev = ids[k % (size_t)std::min(n, 64)];
-      if (hipSetDevice(sl.dev) != hipSuccess || hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) != hipSuccess ||
-          hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) {
+      slots_[k].dev = ids[k % (size_t)nctx];
+      if (make_stream(slots_[k]) != COA_OK) {
         init_rc_ = COA_EHIP;
         return false;
       }
     }
+    for (int i = 0; i < nctx; i++)
+      if (std::find(devs_.begin(), devs_.end(), ids[i]) == devs_.end()) devs_.push_back(ids[i]);
+    rescue_.resize(devs_.size());
+    for (size_t i = 0; i < devs_.size(); i++) rescue_[i].dev = devs_[i];
     return true;
   }
 
   // Input block: verify msgs | pks | sigs, certificate arrays, digest data |
-  // offsets (256-byte aligned sections).  Output block: verdicts | status
-  // words | 64-byte digests.
-  int enqueue(Slot& sl, coa_q::Window& w) {
+  // offsets (256-byte aligned sections), each section the parts' arrays one
+  // after another (offsets rebased).  Output block: verdicts | status words |
+  // 64-byte digests.
+  int enqueue(Slot& sl, coa_q::Launch& L, bool inject) {
     if (hipSetDevice(sl.dev) != hipSuccess) return COA_EHIP;
-    const size_t nvotes = w.nc ? w.c_voff.back() : 0;
     size_t o = 0;
     auto take = [&](size_t bytes) {
       const size_t at = o;
       o = al256(o + bytes);
       return at;
     };
-    const size_t i_vm = take(w.nv * 32), i_vp = take(w.nv * 32), i_vs = take(w.nv * 64);
-    const size_t i_ch = take(w.c_hdata.size() + 16), i_cho = take((w.nc + 1) * 8), i_cid = take(w.nc * 32),
-                 i_cor = take(w.nc * 32), i_chs = take(w.nc * 64), i_crd = take(w.nc * 8),
-                 i_cvp = take(nvotes * 32), i_cvs = take(nvotes * 64), i_cvo = take((w.nc + 1) * 8);
-    const size_t i_dd = take(w.d_data.size() + 16), i_do = take((w.nd + 1) * 8);
+    const size_t i_vm = take(L.nv * 32), i_vp = take(L.nv * 32), i_vs = take(L.nv * 64);
+    const size_t i_ch = take(L.hbytes + 16), i_cho = take((L.nc + 1) * 8), i_cid = take(L.nc * 32),
+                 i_cor = take(L.nc * 32), i_chs = take(L.nc * 64), i_crd = take(L.nc * 8),
+                 i_cvp = take(L.nvotes * 32), i_cvs = take(L.nvotes * 64), i_cvo = take((L.nc + 1) * 8);
+    const size_t i_dd = take(L.dbytes + 16), i_do = take((L.nd + 1) * 8);
     const size_t in_bytes = o;
     o = 0;
-    sl.o_v = take(w.nv);
-    sl.o_c = take(w.nc * 4);
-    sl.o_d = take(w.nd * 64);
+    sl.o_v = take(L.nv);
+    sl.o_c = take(L.nc * 4);
+    sl.o_d = take(L.nd * 64);
     const size_t out_bytes = o;
-    const size_t ws_v = w.nv ? coa_verify_workspace_bytes(w.nv) : 0;
-    const size_t ws_c = w.nc ? coa_certificate_workspace_bytes(w.nc, nvotes) : 0;
+    const size_t ws_v = L.nv ? coa_verify_workspace_bytes(L.nv) : 0;
+    const size_t ws_c = L.nc ? coa_certificate_workspace_bytes(L.nc, L.nvotes) : 0;
     if (grow_pinned(sl.hin, sl.cap_hin, in_bytes) != hipSuccess ||
         grow_pinned(sl.hout, sl.cap_hout, out_bytes) != hipSuccess ||
         grow_dev(sl.din, sl.cap_din, in_bytes) != hipSuccess || grow_dev(sl.dout, sl.cap_dout, out_bytes) != hipSuccess ||
         grow_dev(sl.ws, sl.cap_ws, std::max(ws_v, ws_c) + 256) != hipSuccess)
       return COA_ENOMEM;
     uint8_t* h = static_cast<uint8_t*>(sl.hin);
-    auto put = [&](size_t at, const void* src, size_t bytes) {
-      if (bytes) std::memcpy(h + at, src, bytes);
-    };
-    put(i_vm, w.v_msgs.data(), w.v_msgs.size());
-    put(i_vp, w.v_pks.data(), w.v_pks.size());
-    put(i_vs, w.v_sigs.data(), w.v_sigs.size());
-    if (w.nc) {
-      put(i_ch, w.c_hdata.data(), w.c_hdata.size());
-      put(i_cho, w.c_hoff.data(), (w.nc + 1) * 8);
-      put(i_cid, w.c_ids.data(), w.nc * 32);
-      put(i_cor, w.c_origins.data(), w.nc * 32);
-      put(i_chs, w.c_hsigs.data(), w.nc * 64);
-      put(i_crd, w.c_rounds.data(), w.nc * 8);
-      put(i_cvp, w.c_pks.data(), nvotes * 32);
-      put(i_cvs, w.c_sigs.data(), nvotes * 64);
-      put(i_cvo, w.c_voff.data(), (w.nc + 1) * 8);
+    size_t v = 0, c = 0, cv = 0, hb = 0, dn = 0, db = 0;
+    uint64_t* cho = reinterpret_cast<uint64_t*>(h + i_cho);
+    uint64_t* cvo = reinterpret_cast<uint64_t*>(h + i_cvo);
+    uint64_t* dof = reinterpret_cast<uint64_t*>(h + i_do);
+    cho[0] = cvo[0] = dof[0] = 0;
+    for (const coa_q::Window* w : L.parts) {
+      if (w->nv) {
+        std::memcpy(h + i_vm + v * 32, w->v_msgs.data(), w->nv * 32);
+        std::memcpy(h + i_vp + v * 32, w->v_pks.data(), w->nv * 32);
+        std::memcpy(h + i_vs + v * 64, w->v_sigs.data(), w->nv * 64);
+        v += w->nv;
+      }
+      if (w->nc) {
+        const size_t nvt = w->c_voff.back();
+        if (!w->c_hdata.empty()) std::memcpy(h + i_ch + hb, w->c_hdata.data(), w->c_hdata.size());
+        for (size_t i = 1; i <= w->nc; i++) {
+          cho[c + i] = hb + w->c_hoff[i];
+          cvo[c + i] = cv + w->c_voff[i];
+        }
+        std::memcpy(h + i_cid + c * 32, w->c_ids.data(), w->nc * 32);
+        std::memcpy(h + i_cor + c * 32, w->c_origins.data(), w->nc * 32);
+        std::memcpy(h + i_chs + c * 64, w->c_hsigs.data(), w->nc * 64);
+        std::memcpy(h + i_crd + c * 8, w->c_rounds.data(), w->nc * 8);
+        if (nvt) {
+          std::memcpy(h + i_cvp + cv * 32, w->c_pks.data(), nvt * 32);
+          std::memcpy(h + i_cvs + cv * 64, w->c_sigs.data(), nvt * 64);
+        }
+        c += w->nc;
+        cv += nvt;
+        hb += w->c_hdata.size();
+      }
+      if (w->nd) {
+        if (!w->d_data.empty()) std::memcpy(h + i_dd + db, w->d_data.data(), w->d_data.size());
+        for (size_t i = 1; i <= w->nd; i++) dof[dn + i] = db + w->d_offs[i];
+        dn += w->nd;
+        db += w->d_data.size();
+      }
     }
-    if (w.nd) {
-      put(i_dd, w.d_data.data(), w.d_data.size());
-      put(i_do, w.d_offs.data(), (w.nd + 1) * 8);
-    }
-    if (w.nv + w.nc + w.nd == 0) return COA_OK;  // bare vote batches only: done in complete()
+    if (L.nv + L.nc + L.nd == 0) return COA_OK;  // bare vote batches only: done in complete()
     uint8_t* d = static_cast<uint8_t*>(sl.din);
     uint8_t* dout = static_cast<uint8_t*>(sl.dout);
     if (hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, sl.s) != hipSuccess) return COA_EHIP;
     sl.launched = true;
+    if (inject) return COA_EHIP;  // fault injection: the copy is in flight, the kernels never run
     int rc = COA_OK;
-    if (w.nv)
-      rc = coa_ed25519_verify_strict_many_device(sl.dev, d + i_vm, 32, d + i_vp, d + i_vs, w.nv, dout + sl.o_v, sl.ws,
+    if (L.nv)
+      rc = coa_ed25519_verify_strict_many_device(sl.dev, d + i_vm, 32, d + i_vp, d + i_vs, L.nv, dout + sl.o_v, sl.ws,
                                                  sl.s);
-    if (rc == COA_OK && w.nc)
+    if (rc == COA_OK && L.nc) {
+      coa_keycache_read_acquire(sl.dev);
+      sl.gate = true;
       rc = coa_certificate_verify_many_device(
           sl.dev, d + i_ch, reinterpret_cast<const uint64_t*>(d + i_cho), d + i_cid, d + i_cor, d + i_chs,
           reinterpret_cast<const uint64_t*>(d + i_crd), d + i_cvp, d + i_cvs,
-          reinterpret_cast<const uint64_t*>(d + i_cvo), w.nc, nvotes, reinterpret_cast<uint32_t*>(dout + sl.o_c),
+          reinterpret_cast<const uint64_t*>(d + i_cvo), L.nc, L.nvotes, reinterpret_cast<uint32_t*>(dout + sl.o_c),
           sl.ws, sl.s);
-    if (rc == COA_OK && w.nd)
-      rc = coa_sha512_many_device(sl.dev, d + i_dd, reinterpret_cast<const uint64_t*>(d + i_do), w.nd, dout + sl.o_d,
+    }
+    if (rc == COA_OK && L.nd)
+      rc = coa_sha512_many_device(sl.dev, d + i_dd, reinterpret_cast<const uint64_t*>(d + i_do), L.nd, dout + sl.o_d,
                                   sl.s);
     if (rc != COA_OK) return rc;
     if (hipMemcpyAsync(sl.hout, dout, out_bytes, hipMemcpyDeviceToHost, sl.s) != hipSuccess) return COA_EHIP;
     if (hipEventRecord(sl.ev, sl.s) != hipSuccess) return COA_EHIP;
     return COA_OK;
+  }
+
+  // Waits for the slot's work (a failed enqueue drains its stream, keeping
+  // the error), then scatters the outputs to the parts.
+  void finish(Slot& sl, coa_q::Launch& L) {
+    if (sl.launched) {
+      (void)hipSetDevice(sl.dev);
+      if (L.rc == COA_OK) {
+        if (hipEventSynchronize(sl.ev) != hipSuccess) L.rc = COA_EHIP;
+      } else {
+        (void)hipStreamSynchronize(sl.s);  // nothing may still read the staging when the slot is reused
+      }
+      sl.launched = false;
+    }
+    if (L.rc == COA_OK) {
+      const uint8_t* h = static_cast<const uint8_t*>(sl.hout);
+      size_t v = 0, c = 0, dn = 0;
+      for (coa_q::Window* w : L.parts) {
+        if (w->nv) std::memcpy(w->v_out.data(), h + sl.o_v + v, w->nv);
+        for (size_t i = 0; i < w->nd; i++) std::memcpy(&w->d_out[i * 32], h + sl.o_d + (dn + i) * 64, 32);
+        if (w->nc && L.rc == COA_OK)
+          L.rc = resolve_certs(*w, reinterpret_cast<const uint32_t*>(h + sl.o_c) + c);
+        if (w->ng && L.rc == COA_OK)
+          L.rc = coa_ed25519_verify_batch_groups(w->g_msgs.data(), w->g_pks.data(), w->g_sigs.data(),
+                                                 w->g_offs.data(), w->ng, w->g_out.data(), 0);
+        v += w->nv;
+        c += w->nc;
+        dn += w->nd;
+      }
+    }
+    if (sl.gate) {
+      coa_keycache_read_release(sl.dev);
+      sl.gate = false;
+    }
   }
 
   // Raw certificate status words -> COA_CERT_* bits; certificates the fused
@@ -277,11 +386,14 @@ class HipBackend : public coa_q::Backend {
   }
 
   std::vector<Slot> slots_;
+  std::vector<Slot> rescue_;  // one recovery context per device, used only by retry()
+  std::vector<int> devs_;     // distinct device ids
   size_t next_ = 0;
   std::mutex m_;
   std::condition_variable cv_;
   bool inited_ = false;
   int init_rc_ = COA_OK;
+  unsigned long long fault_every_ = 0, launches_ = 0;
 };
 
 }  // namespace

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -214,6 +215,36 @@ std::mutex g_init_mu;
 std::vector<std::unique_ptr<Dev>> g_devs;
 bool g_inited = false;
 
+// Engine-failure recovery counters (coa_engine_recoveries).
+std::atomic<uint64_t> g_ctx_rebuilt{0}, g_shards_rerun{0};
+
+// Key-cache gate per HIP device id (coa_committee.h): readers are the
+// aggregation queue's in-flight certificate windows, the writer is
+// coa_committee_register.  A waiting writer holds new readers back.
+struct KeyGate {
+  std::mutex mu;
+  std::condition_variable cv;
+  int readers = 0;
+  bool writer = false;
+};
+constexpr int kMaxDevIds = 64;
+KeyGate g_kgate[kMaxDevIds];
+KeyGate& kgate(int device) { return g_kgate[(unsigned)device % kMaxDevIds]; }
+
+void kgate_write_lock(int device) {
+  KeyGate& g = kgate(device);
+  std::unique_lock<std::mutex> l(g.mu);
+  g.cv.wait(l, [&] { return !g.writer; });
+  g.writer = true;
+  g.cv.wait(l, [&] { return g.readers == 0; });
+}
+void kgate_write_unlock(int device) {
+  KeyGate& g = kgate(device);
+  std::lock_guard<std::mutex> l(g.mu);
+  g.writer = false;
+  g.cv.notify_all();
+}
+
 int open_device(int d) {
   auto dev = std::make_unique<Dev>();
   dev->id = d;
@@ -404,13 +435,38 @@ int lat_res_prepare(Dev& d, size_t n, uint32_t& tag) {
     d.lat_res_cap = 0;
     const size_t cap = std::max<size_t>(n, 64);
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.lat_res), cap * 4, hipHostMallocCoherent));
-    std::memset(d.lat_res, 0, cap * 4);
     d.lat_res_cap = cap;
   }
+  // the words this call waits for start at 0, which no tag matches: a word
+  // left over from an earlier call can never pass for this call's result,
+  // however the 24-bit tag wraps
+  std::memset(d.lat_res, 0, n * 4);
   d.lat_tag = (d.lat_tag + 1) & 0xffffffu;
   if (d.lat_tag == 0) d.lat_tag = 1;
   tag = d.lat_tag;
   return COA_OK;
+}
+
+// The context a latency call runs on: the first idle one (its lock free),
+// starting one further on each call; when every context is busy, the next
+// one in turn (the call then waits for its lock).  Concurrent one-message
+// calls (Core and the two Processors) thus spread over every opened context
+// instead of queueing on the first.
+std::atomic<uint32_t> g_lat_rr{0};
+Dev& lat_dev(std::unique_lock<std::mutex>& lk) {
+  const size_t n = g_devs.size();
+  const size_t start = g_lat_rr.fetch_add(1, std::memory_order_relaxed) % n;
+  for (size_t k = 0; k < n; k++) {
+    Dev& d = *g_devs[(start + k) % n];
+    std::unique_lock<std::mutex> l(d.mu, std::try_to_lock);
+    if (l.owns_lock()) {
+      lk = std::move(l);
+      return d;
+    }
+  }
+  Dev& d = *g_devs[start];
+  lk = std::unique_lock<std::mutex>(d.mu);
+  return d;
 }
 
 // Waits until the n result words carry `tag` (written by the kernel just
@@ -515,23 +571,84 @@ int run_tasks(std::vector<std::pair<Dev*, std::function<int()>>>& tasks) {
   return rc;
 }
 
+// COA_FAULT_SHARD=<k>: every k-th shard of a sharded call fails with
+// COA_EHIP after its work has run (fault injection for the recovery tests;
+// never set in production).  Read per call.
+bool inject_shard_fault() {
+  static std::atomic<unsigned long long> count{0};
+  const char* e = getenv("COA_FAULT_SHARD");
+  const unsigned long long every = e ? strtoull(e, nullptr, 10) : 0ull;
+  return every && (count.fetch_add(1) + 1) % every == 0;
+}
+
+// Rebuilds a context after a HIP failure (its lock held): drains and
+// replaces its stream and releases its per-call buffers (they regrow on
+// demand).  The fixed-base and committee tables are kept: they were built
+// and checked before and no call writes them.  Same process, no exec.
+int rebuild_context(Dev& d) {
+  (void)hipSetDevice(d.id);
+  (void)hipStreamSynchronize(d.stream);
+  (void)hipStreamDestroy(d.stream);
+  d.stream = nullptr;
+  for (DevBuf* b : {&d.msgs, &d.pks, &d.sigs, &d.kbuf, &d.rec, &d.verdicts, &d.scratch, &d.aux, &d.rbuf, &d.seeds,
+                    &d.offs, &d.data, &d.out, &d.idx, &d.zs, &d.terms, &d.flags, &d.cert, &d.cscr, &d.msm, &d.lat})
+    b->release();
+  (void)hipGetLastError();
+  HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  g_ctx_rebuilt++;
+  return COA_OK;
+}
+
 // Run `body` for every shard with its context's lock held, then drain the
 // context's stream.  body(Dev&, lo, hi) enqueues work and returns COA_OK or an
 // error.  The shards run concurrently, one per context worker.
+// Engine-failure recovery: a shard that fails with a device error
+// (COA_EHIP / COA_ENOMEM) has its context rebuilt and is re-run on the next
+// contexts in turn (the rebuilt one last); the call fails only when every
+// context failed it.  body must therefore be re-runnable for its range: it
+// writes only its own slice of the caller's outputs.
 template <class F>
 int for_shards(size_t n, F body) {
   std::vector<std::pair<Dev*, std::function<int()>>> tasks;
-  for (const Range& r : shard(n)) {
-    tasks.emplace_back(r.dev, [r, &body]() -> int {
-      std::lock_guard<std::mutex> l(r.dev->mu);
-      if (hipSetDevice(r.dev->id) != hipSuccess) return fail(COA_EHIP, "hipSetDevice failed");
-      int rc = body(*r.dev, r.lo, r.hi);
-      const hipError_t e = hipStreamSynchronize(r.dev->stream);
-      if (e != hipSuccess && rc == COA_OK) rc = fail(COA_EHIP, std::string("stream sync: ") + hipGetErrorString(e));
-      return rc;
+  const std::vector<Range> ranges = shard(n);
+  std::vector<int> rcs(ranges.size(), COA_OK);
+  std::vector<std::string> msgs(ranges.size());
+  auto run_on = [&body](Dev& d, size_t lo, size_t hi, bool inject) -> int {
+    std::lock_guard<std::mutex> l(d.mu);
+    if (hipSetDevice(d.id) != hipSuccess) return fail(COA_EHIP, "hipSetDevice failed");
+    int rc = body(d, lo, hi);
+    const hipError_t e = hipStreamSynchronize(d.stream);
+    if (e != hipSuccess && rc == COA_OK) rc = fail(COA_EHIP, std::string("stream sync: ") + hipGetErrorString(e));
+    if (rc == COA_OK && inject) rc = fail(COA_EHIP, "injected shard fault (COA_FAULT_SHARD)");
+    if (rc == COA_EHIP || rc == COA_ENOMEM) (void)rebuild_context(d);
+    return rc;
+  };
+  for (size_t i = 0; i < ranges.size(); i++) {
+    const Range r = ranges[i];
+    const bool inject = inject_shard_fault();
+    tasks.emplace_back(r.dev, [r, inject, i, &rcs, &msgs, &run_on]() -> int {
+      rcs[i] = run_on(*r.dev, r.lo, r.hi, inject);
+      if (rcs[i] != COA_OK) msgs[i] = g_err;
+      // recoverable failures are re-run below, so the other shards finish
+      return (rcs[i] == COA_EHIP || rcs[i] == COA_ENOMEM) ? COA_OK : rcs[i];
     });
   }
-  return run_tasks(tasks);
+  int rc = run_tasks(tasks);
+  if (rc != COA_OK) return rc;
+  for (size_t i = 0; i < ranges.size(); i++) {
+    if (rcs[i] == COA_OK) continue;
+    size_t at = 0;
+    for (size_t g = 0; g < g_devs.size(); g++)
+      if (g_devs[g].get() == ranges[i].dev) at = g;
+    int r = rcs[i];
+    const std::string first = msgs[i];
+    for (size_t k = 1; k <= g_devs.size() && (r == COA_EHIP || r == COA_ENOMEM); k++) {
+      r = run_on(*g_devs[(at + k) % g_devs.size()], ranges[i].lo, ranges[i].hi, false);
+      g_shards_rerun++;
+    }
+    if (r != COA_OK) return fail(r, "shard failed on every context: " + first + " / " + g_err);
+  }
+  return COA_OK;
 }
 
 uint64_t os_entropy_seed() {
@@ -988,9 +1105,9 @@ int certificates_impl(const CertIn& in, size_t n, uint64_t rng_seed, uint8_t* st
   if (check_n(n + in.voff[n]) != COA_OK) return COA_EINVAL;
   std::vector<uint32_t> st(n, 0);
   int rc;
-  if (g_devs.size() == 1 && cert_lanes(n + in.voff[n]) == 64) {  // latency path: one device, no stream sync
-    Dev& d = *g_devs[0];
-    std::lock_guard<std::mutex> l(d.mu);
+  if (cert_lanes(n + in.voff[n]) == 64) {  // latency path: one idle context, no stream sync
+    std::unique_lock<std::mutex> l;
+    Dev& d = lat_dev(l);
     HIP_TRY(hipSetDevice(d.id));
     rc = cert_shard(d, in, 0, n, st.data(), true);
   } else {
@@ -1134,9 +1251,9 @@ int coa_ed25519_verify_strict_many(const uint8_t* msgs, size_t msg_len, const ui
   if (n == 0) return COA_OK;
   if ((!msgs && msg_len) || !pks || !sigs || !verdicts_out) return fail(COA_EINVAL, "null argument");
   if (check_n(n) != COA_OK) return COA_EINVAL;
-  if (msg_len == 32 && n <= lat_max()) {  // few signatures: the latency kernel, first device
-    Dev& d = *g_devs[0];
-    std::lock_guard<std::mutex> l(d.mu);
+  if (msg_len == 32 && n <= lat_max()) {  // few signatures: the latency kernel on an idle context
+    std::unique_lock<std::mutex> l;
+    Dev& d = lat_dev(l);
     HIP_TRY(hipSetDevice(d.id));
     return lat_verify(d, msgs, pks, sigs, n, verdicts_out);
   }
@@ -1447,9 +1564,37 @@ int coa_committee_register(const uint8_t* pks, size_t n) {
       return COA_OK;
     });
   }
+  // the aggregation queue's in-flight certificate windows read these tables
+  // asynchronously: wait for them and hold new ones back (coa_committee.h)
+  std::vector<int> ids;
+  for (auto& dp : g_devs)
+    if (std::find(ids.begin(), ids.end(), dp->id) == ids.end()) ids.push_back(dp->id);
+  std::sort(ids.begin(), ids.end());
+  for (int id : ids) kgate_write_lock(id);
   rc = run_tasks(tasks);
+  for (int id : ids) kgate_write_unlock(id);
   if (rc != COA_OK) return rc;
   return (int)nk;
+}
+
+void coa_keycache_read_acquire(int device) {
+  KeyGate& g = kgate(device);
+  std::unique_lock<std::mutex> l(g.mu);
+  g.cv.wait(l, [&] { return !g.writer; });
+  g.readers++;
+}
+
+void coa_keycache_read_release(int device) {
+  KeyGate& g = kgate(device);
+  std::lock_guard<std::mutex> l(g.mu);
+  g.readers--;
+  g.cv.notify_all();
+}
+
+int coa_engine_recoveries(uint64_t* contexts_rebuilt, uint64_t* shards_rerun) {
+  if (contexts_rebuilt) *contexts_rebuilt = g_ctx_rebuilt.load();
+  if (shards_rerun) *shards_rerun = g_shards_rerun.load();
+  return COA_OK;
 }
 
 int coa_committee_key_flags(uint32_t* flags_out, size_t cap) {
