@@ -70,6 +70,8 @@ int main(int argc, char** argv) {
   CHECK(coa_self_test(0, &bad_entries) == dev_rc, "coa_self_test");
   CHECK(!gpu || bad_entries == 0, "coa_self_test entries");
   CHECK(coa_fe_rows_check_device(0, NULL, 0, NULL, NULL) == dev_rc, "coa_fe_rows_check_device");
+  uint64_t rebuilt = 9, rerun = 9;
+  CHECK(coa_engine_recoveries(&rebuilt, &rerun) == COA_OK && rebuilt == 0 && rerun == 0, "coa_engine_recoveries");
 
   /* Signature::verify */
   CHECK(coa_ed25519_verify_strict(msg, pk, sig) == (gpu ? COA_OK : COA_ENODEVICE), "verify_strict ok");
@@ -182,7 +184,8 @@ int main(int argc, char** argv) {
   CHECK(coa_queue_digest_count(q, &digests) == COA_OK && digests == 1, "queue_digest_count");
   coa_queue_metrics_t qm;
   CHECK(coa_queue_metrics(q, &qm) == COA_OK && qm.requests == 5 && qm.signatures == 2 && qm.batches == 1 &&
-            qm.certificates == 1 && qm.digests == 1 && qm.wait_us_max >= qm.wait_us_mean,
+            qm.certificates == 1 && qm.digests == 1 && qm.wait_us_max >= qm.wait_us_mean &&
+            qm.retried_windows == qm.recovered_windows && qm.failed_windows == (gpu ? 0u : qm.windows),
         "queue_metrics");
   CHECK(coa_queue_destroy(q) == COA_OK, "queue_destroy");
 

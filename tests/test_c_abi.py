@@ -3,8 +3,14 @@
 ABI, so the header's prototypes -- not only the exported symbol names -- are
 checked; run without a GPU it checks that every device call refuses with
 COA_ENODEVICE (no CPU fallback) and that the host-only calls behave.  The GPU
-form of the same harness runs in tests/test_gpu_c_abi.py."""
+form of the same harness runs in tests/test_gpu_c_abi.py.
+
+The multi-producer queue harness (tests/c_abi/queue_harness.c, the way the
+Rust VerifyService drives the queue) is compiled the same way; without a GPU
+every one of its requests must still be answered, with the engine error."""
+import json
 import os
+import struct
 import subprocess
 
 import pytest
@@ -29,6 +35,66 @@ def build_harness():
     subprocess.run(cmd, check=True, capture_output=True, text=True)
     os.replace(tmp, OUT)
     return OUT
+
+
+QSRC = os.path.join(ROOT, "tests", "c_abi", "queue_harness.c")
+QOUT = os.path.join(ROOT, "tests", "c_abi", "queue_harness")
+
+
+def build_queue_harness():
+    import build
+
+    lib = build.build()
+    libdir = os.path.dirname(lib)
+    tmp = f"{QOUT}.{os.getpid()}"
+    cmd = ["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"),
+           QSRC, "-o", tmp, "-L", libdir, "-lcoa_verify", f"-Wl,-rpath,{libdir}", "-L/opt/rocm/lib",
+           "-Wl,-rpath,/opt/rocm/lib"]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    os.replace(tmp, QOUT)
+    return QOUT
+
+
+def write_queue_vectors(path):
+    """The golden verify vectors with 32-byte messages (crypto API), the
+    golden batch groups (z-independent verdicts) and SHA-512 vectors, in the
+    queue harness's binary format; returns (n_verify, n_batch, n_digest)."""
+    gold = os.path.join(ROOT, "tests", "golden")
+    vv = [v for v in json.load(open(os.path.join(gold, "verify_vectors.json"))) if len(v["msg"]) == 64]
+    bv = json.load(open(os.path.join(gold, "batch_vectors.json")))
+    dv = json.load(open(os.path.join(gold, "sha512_vectors.json")))
+    out = [struct.pack("<4I", 0x51414F43, len(vv), len(bv), len(dv))]
+    for v in vv:
+        out.append(bytes.fromhex(v["msg"]) + bytes.fromhex(v["pk"]) + bytes.fromhex(v["sig"]) +
+                   bytes([0 if v["expect"] else 1]))
+    for g in bv:
+        out.append(bytes.fromhex(g["msg"]) + struct.pack("<I", len(g["pks"])) + bytes([0 if g["expect"] else 1]))
+        for pk, sg in zip(g["pks"], g["sigs"]):
+            out.append(bytes.fromhex(pk) + bytes.fromhex(sg))
+    for d in dv:
+        data = bytes.fromhex(d["msg"])
+        out.append(struct.pack("<I", len(data)) + data + bytes.fromhex(d["sha512"])[:32])
+    with open(path, "wb") as f:
+        f.write(b"".join(out))
+    return len(vv), len(bv), len(dv)
+
+
+def test_queue_harness_cpu_mode(tmp_path):
+    """No GPU: every request of 4 producers is answered exactly once, each
+    with the engine error (the harness then exits 1)."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: tests/test_gpu_queue_harness.py runs it")
+    exe = build_queue_harness()
+    vec = str(tmp_path / "vectors.bin")
+    nv, nb, nd = write_queue_vectors(vec)
+    r = subprocess.run([exe, vec, "4", "1"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1, r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    n = 4 * (nv + nb + nd)
+    assert res["submitted"] == n and res["answered"] == n and res["bad_status"] == n, res
+    assert res["retried_windows"] == 0  # "no device" is not a recoverable failure
 
 
 def test_harness_compiles_against_header():

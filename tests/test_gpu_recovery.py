@@ -1,0 +1,165 @@
+"""GPU: engine-failure recovery, concurrency of the latency route and
+registration under load.
+
+* Host-pointer calls (coa_runtime.cpp for_shards): with COA_FAULT_SHARD a
+  shard's work is declared failed after it ran; its context is rebuilt (new
+  stream, per-call buffers released) and the shard re-run on the next
+  context -- verdicts stay bit-exact against the C oracle and
+  coa_engine_recoveries counts it.  The reference's verify never fails for a
+  reason other than the input, and Core::run logs and continues
+  (primary/src/core.rs:390-398), so a device hiccup must not become a verdict.
+* One-message calls (Header::verify / Vote::verify,
+  primary/src/messages.rs:64-66,139-141) from 8 threads over 8 contexts: each
+  call takes an idle context (no longer always the first), every verdict
+  equals the golden expectation.
+* coa_committee_register while the aggregation queue is saturated with
+  certificate windows: registration waits for in-flight windows
+  and holds new ones back, so every certificate verdict stays exact whether
+  the committee is registered, re-registered or cleared meanwhile."""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import coa_oracle as co
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _vec32():
+    return [v for v in load_golden("verify_vectors.json") if len(v["msg"]) == 64]
+
+
+def _tiled(n):
+    vecs = _vec32()
+    rows = [vecs[i % len(vecs)] for i in range(n)]
+    msgs = np.array([list(bytes.fromhex(v["msg"])) for v in rows], np.uint8)
+    pks = np.array([list(bytes.fromhex(v["pk"])) for v in rows], np.uint8)
+    sigs = np.array([list(bytes.fromhex(v["sig"])) for v in rows], np.uint8)
+    exp = np.array([0 if v["expect"] else 1 for v in rows], np.uint8)
+    return msgs, pks, sigs, exp
+
+
+@pytest.fixture
+def contexts(engine):
+    """Re-open the engine with k contexts on device 0 (k index-range shards,
+    as k GPUs of a node); back to the default afterwards."""
+    opened = []
+
+    def open_k(k):
+        engine.shutdown()
+        engine.init_devices([0] * k)
+        opened.append(k)
+        return engine
+
+    yield open_k
+    if opened:
+        engine.shutdown()
+        engine.init(0)
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_shard_failure_rebuilds_context_and_reruns(engine, contexts, monkeypatch, k):
+    from workloads import adversarial_mix, key_seeds, messages
+
+    contexts(k)
+    n = 12_000  # above COA_LAT_MAX: the sharded throughput path
+    pks, sigs = engine.sign_many(key_seeds(n, 7000), messages(n, 7000))
+    msgs, pks, sigs, cls = adversarial_mix(messages(n, 7000), pks, sigs, frac=0.1, seed=77)
+    exp = co.verify_strict_many(msgs, pks, sigs, min(16, os.cpu_count() or 1))
+    before = engine.engine_recoveries()
+    monkeypatch.setenv("COA_FAULT_SHARD", "2")  # every 2nd shard "fails"
+    got = engine.verify_strict_many(msgs, pks, sigs)
+    got2 = engine.verify_strict_many(msgs, pks, sigs)
+    monkeypatch.delenv("COA_FAULT_SHARD")
+    after = engine.engine_recoveries()
+    assert (got == exp).all() and (got2 == exp).all()
+    assert after["contexts_rebuilt"] > before["contexts_rebuilt"]
+    assert after["shards_rerun"] > before["shards_rerun"]
+    # the rebuilt contexts keep working: SHA-512 and the golden tiles
+    m2, p2, s2, e2 = _tiled(5000)
+    assert (engine.verify_strict_many(m2, p2, s2) == e2).all()
+
+
+def test_single_verifies_from_eight_threads_over_eight_contexts(engine, contexts):
+    contexts(8)
+    vecs = _vec32()
+    engine.committee_register(np.array([list(bytes.fromhex(v["pk"])) for v in vecs[:40]], np.uint8))
+    errors = []
+
+    def worker(t):
+        try:
+            for r in range(3):
+                for i in range(t, len(vecs), 8):
+                    v = vecs[i]
+                    sig = engine.Signature.from_bytes(bytes.fromhex(v["sig"]))
+                    try:
+                        sig.verify(bytes.fromhex(v["msg"]), bytes.fromhex(v["pk"]))
+                        got = True
+                    except engine.CryptoError:
+                        got = False
+                    if got != v["expect"]:
+                        errors.append((t, r, v["class"], v["note"]))
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=240)
+    engine.committee_register(np.zeros((0, 32), np.uint8))
+    assert not any(x.is_alive() for x in th)
+    assert not errors, errors[:10]
+
+
+def test_register_while_queue_saturated_with_certificates(engine):
+    import certificates as C
+
+    committee, batch = C.synth_certificates(48, committee_size=12, n_payload=3, seed=31)
+    batch.vote_sigs[int(batch.offsets[5]) + 1, 44] ^= 1   # certificate 5: bad vote
+    batch.header_sigs[9, 20] ^= 1                          # certificate 9: bad header signature
+    committee.register()
+    want_bits = {5: engine.CERT_BAD_VOTES, 9: engine.CERT_BAD_HEADER_SIG}
+    stop = threading.Event()
+    regs = [0]
+
+    def registrar():
+        while not stop.is_set():
+            engine.committee_register(np.zeros((0, 32), np.uint8))   # cleared: uncached host path
+            committee.register()                                      # back: cached fused kernel
+            regs[0] += 1
+
+    results = []
+    lock = threading.Lock()
+    with engine.AggregationQueue(max_batch=512, max_delay_us=300) as q:
+        def producer(t):
+            out = []
+            for rnd in range(6):
+                for c in range(t, len(batch), 4):
+                    lo, hi = int(batch.offsets[c]), int(batch.offsets[c + 1])
+                    votes = [(engine.PublicKey(bytes(batch.vote_pks[j])),
+                              engine.Signature.from_bytes(bytes(batch.vote_sigs[j]))) for j in range(lo, hi)]
+                    out.append((c, q.submit_certificate(batch.header_inputs[c], bytes(batch.ids[c]),
+                                                        bytes(batch.authors[c]), bytes(batch.header_sigs[c]),
+                                                        batch.round, votes)))
+            with lock:
+                results.extend(out)
+
+        reg = threading.Thread(target=registrar)
+        reg.start()
+        th = [threading.Thread(target=producer, args=(t,)) for t in range(4)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        q.flush()
+        stop.set()
+        reg.join()
+        for c, f in results:
+            assert f.result(timeout=120) == want_bits.get(c, 0), c
+        m = q.metrics()
+    committee.register()
+    assert regs[0] >= 1 and m["certificates"] == len(results) and m["failed_windows"] == 0
