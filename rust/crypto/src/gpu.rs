@@ -17,12 +17,19 @@
 //!     }
 //! `ed25519-dalek` stays a dependency for signing (`Signature::new`,
 //! `generate_keypair`, `SignatureService`), which is not on the hot path.
+//!
+//! Also in crypto/src/lib.rs: `pub mod service; pub mod verified;` -- the
+//! tokio-side aggregation stage (`service::VerifyService`) and the verdicts
+//! it computed ahead of these synchronous calls (`verified`), which
+//! `verify` consults first.
 use crate::coa_ffi as ffi;
 use crate::{CryptoError, Digest, PublicKey};
 
 /// Ok / Err as the engine returned it; a negative code is an engine failure
-/// (no GPU, HIP error, bad arguments), which must never turn into a verdict:
-/// there is no CPU fallback, so it panics with the engine's message.
+/// (no GPU, bad arguments, or a HIP error that persisted after the engine
+/// rebuilt the failing context and re-ran the work on every other context,
+/// coa_engine_recoveries), which must never turn into a verdict: there is no
+/// CPU fallback, so it panics with the engine's message.
 fn verdict(rc: i32) -> Result<(), CryptoError> {
     match rc {
         ffi::COA_OK => Ok(()),
@@ -37,9 +44,14 @@ fn engine_ok(rc: i32) -> i32 {
 }
 
 /// Signature::verify (crypto/src/lib.rs:200-204): dalek 1.0.1 verify_strict
-/// of the 64-byte signature R || s over the 32-byte digest.  One message per
-/// call takes the engine's single-signature latency kernel.
+/// of the 64-byte signature R || s over the 32-byte digest.  A triple the
+/// pre-verification stage already verified Ok (in a coalesced launch) is
+/// answered from `verified`; any other takes the engine's single-signature
+/// latency kernel on an idle device context.
 pub fn verify(signature: &[u8; 64], digest: &Digest, public_key: &PublicKey) -> Result<(), CryptoError> {
+    if crate::verified::take_signature(digest, public_key, signature) {
+        return Ok(());
+    }
     verdict(unsafe { ffi::coa_ed25519_verify_strict(digest.0.as_ptr(), public_key.0.as_ptr(), signature.as_ptr()) })
 }
 
@@ -60,8 +72,12 @@ where
     })
 }
 
-/// Digest(Sha512(bytes)[..32]) on the device (worker/src/processor.rs:38):
-///     let digest = crypto::gpu::sha512_digest(&batch);
+/// Digest(Sha512(bytes)[..32]) of ONE message on the device.  One 508 KB
+/// worker batch per launch is a serial chain of 3,970 compressions (~14 ms,
+/// against ~1 ms on a CPU core): the worker's `Processor` must not call this
+/// per batch -- it streams its batches through `service::VerifyService::
+/// digest` instead (rust/worker/src/processor.rs), whose windows hash many
+/// batches per launch.
 pub fn sha512_digest(bytes: &[u8]) -> Digest {
     let offsets = [0u64, bytes.len() as u64];
     let mut out = [0u8; 32];

@@ -1,0 +1,351 @@
+//! The tokio-side aggregation stage over the engine's native queue
+//! (`coa_queue_*`, include/coa_verify.h): `VerifyService`, modelled on the
+//! reference's `SignatureService` (crypto/src/lib.rs:222-250) -- an mpsc
+//! request channel in, a `oneshot` reply per request.  Where
+//! `SignatureService` signs one digest per request, this service hands every
+//! request it has received to the engine's queue, which coalesces the
+//! requests of all tasks into a few large launches:
+//!
+//!   * `Signature::verify` triples (Header::verify, Vote::verify,
+//!     primary/src/messages.rs:64-66,139-141): whatever the service task
+//!     drains from its channel at once goes to the queue as ONE
+//!     `coa_queue_submit_verify_many` request whose callback fans the
+//!     verdicts out to the requests' oneshot senders;
+//!   * vote batches (`Signature::verify_batch`, :206-219), whole certificates
+//!     (the fused `Certificate::verify` crypto, messages.rs:189-215) and
+//!     worker batch digests (worker/src/processor.rs:38) go one request each.
+//!
+//! The engine answers on its completion thread through the `extern "C"`
+//! callbacks below; each one takes back the boxed sender(s) it was given and
+//! completes them.  `oneshot::Sender::send` does not block and needs no
+//! runtime, so the callbacks never touch tokio's threads.  A callback never
+//! panics (that would unwind across the FFI boundary): an engine failure --
+//! reported only after the queue re-ran the window on every device context
+//! (coa_queue_metrics' retried/recovered/failed counters) -- travels to the
+//! awaiting task as `Err(status)`, and the task panics there with the
+//! engine's message, as the synchronous calls in `gpu.rs` do.  There is no
+//! CPU fallback.
+//!
+//! Wiring (crypto/src/lib.rs): `pub mod service;`.  One service per process,
+//! created once the committee is registered (node/src/main.rs):
+//!     let verifier = crypto::service::VerifyService::new(65_536, 500);
+use crate::coa_ffi as ffi;
+use crate::{CryptoError, Digest, PublicKey};
+use std::os::raw::{c_int, c_void};
+use tokio::sync::mpsc::{channel, Receiver, Sender};
+use tokio::sync::oneshot;
+
+/// A verdict as the crate reports it, or the engine's failure status.
+type Verdict = Result<Result<(), CryptoError>, c_int>;
+
+/// The crypto of one `Certificate::verify` in the engine's terms (the
+/// `primary` crate builds it: rust/primary/src/gpu_certificate.rs).
+pub struct CertificateCrypto {
+    /// the bytes `Header::digest` hashes (primary/src/messages.rs:70-84)
+    pub header_input: Vec<u8>,
+    pub id: Digest,
+    pub origin: PublicKey,
+    pub header_signature: [u8; 64],
+    pub round: u64,
+    /// the votes: 32-byte keys and 64-byte signatures, concatenated
+    pub vote_keys: Vec<u8>,
+    pub vote_signatures: Vec<u8>,
+}
+
+impl CertificateCrypto {
+    /// Every byte the certificate's crypto verdict depends on, length-framed
+    /// (the key of `verified::remember_certificate`).
+    pub fn key_bytes(&self) -> Vec<u8> {
+        let mut k = Vec::with_capacity(
+            8 + self.header_input.len() + 32 + 32 + 64 + 8 + 8 + self.vote_keys.len() + self.vote_signatures.len(),
+        );
+        k.extend_from_slice(&(self.header_input.len() as u64).to_le_bytes());
+        k.extend_from_slice(&self.header_input);
+        k.extend_from_slice(&self.id.0);
+        k.extend_from_slice(&self.origin.0);
+        k.extend_from_slice(&self.header_signature);
+        k.extend_from_slice(&self.round.to_le_bytes());
+        k.extend_from_slice(&((self.vote_keys.len() / 32) as u64).to_le_bytes());
+        k.extend_from_slice(&self.vote_keys);
+        k.extend_from_slice(&self.vote_signatures);
+        k
+    }
+}
+
+/// A worker batch on its way through the engine, handed back with its digest
+/// (the batch is then stored, worker/src/processor.rs:41).
+type DigestReply = Result<(Digest, Vec<u8>), c_int>;
+
+enum Request {
+    Verify(Digest, PublicKey, [u8; 64], oneshot::Sender<Verdict>),
+    Batch(Digest, Vec<(PublicKey, [u8; 64])>, oneshot::Sender<Verdict>),
+    Certificate(CertificateCrypto, oneshot::Sender<Result<u8, c_int>>),
+    Digest(Vec<u8>, oneshot::Sender<DigestReply>),
+}
+
+/// The engine queue, shared by the service task and the callbacks.  The C
+/// queue is thread-safe (per-thread intake shards, its own threads).
+struct Queue(*mut ffi::CoaQueue);
+unsafe impl Send for Queue {}
+unsafe impl Sync for Queue {}
+
+/// Most requests the service task drains from its channel per turn.
+const DRAIN: usize = 4096;
+
+#[derive(Clone)]
+pub struct VerifyService {
+    channel: Sender<Request>,
+}
+
+impl VerifyService {
+    /// `max_batch`: signatures per GPU launch window (the queue closes a
+    /// window when this many are pending); `max_delay_us`: the longest a
+    /// request waits for its window to close.
+    pub fn new(max_batch: usize, max_delay_us: u32) -> Self {
+        let queue = unsafe { ffi::coa_queue_create(max_batch, max_delay_us) };
+        assert!(!queue.is_null(), "MI355X verification engine: coa_queue_create failed: {}", ffi::last_error());
+        let queue = Queue(queue);
+        let (tx, rx): (Sender<Request>, Receiver<Request>) = channel(DRAIN);
+        tokio::spawn(Self::run(queue, rx));
+        Self { channel: tx }
+    }
+
+    async fn run(queue: Queue, mut rx: Receiver<Request>) {
+        while let Some(first) = rx.recv().await {
+            let mut window = vec![first];
+            while window.len() < DRAIN {
+                match rx.try_recv() {
+                    Ok(request) => window.push(request),
+                    Err(_) => break,
+                }
+            }
+            submit_window(&queue, window);
+        }
+        // every handle dropped: answer what is in flight, then free the queue
+        // (both block, so off the async workers)
+        let _ = tokio::task::spawn_blocking(move || unsafe {
+            ffi::coa_queue_flush(queue.0);
+            ffi::coa_queue_destroy(queue.0);
+        })
+        .await;
+    }
+
+    async fn send(&self, request: Request) {
+        if let Err(e) = self.channel.send(request).await {
+            panic!("Failed to send request to the Verify Service: {}", e);
+        }
+    }
+
+    /// `Signature::verify(digest, key)` (crypto/src/lib.rs:200-204) through
+    /// the queue: coalesced with every other pending request.
+    pub async fn verify(&self, digest: &Digest, key: &PublicKey, signature: [u8; 64]) -> Result<(), CryptoError> {
+        let (sender, receiver) = oneshot::channel();
+        self.send(Request::Verify(digest.clone(), *key, signature, sender)).await;
+        match receiver.await.expect("Failed to receive verdict from Verify Service") {
+            Ok(verdict) => verdict,
+            Err(status) => panic!("MI355X verification engine failure {} (every context failed)", status),
+        }
+    }
+
+    /// `Signature::verify_batch(digest, votes)` (crypto/src/lib.rs:206-219).
+    pub async fn verify_batch(&self, digest: &Digest, votes: Vec<(PublicKey, [u8; 64])>) -> Result<(), CryptoError> {
+        let (sender, receiver) = oneshot::channel();
+        self.send(Request::Batch(digest.clone(), votes, sender)).await;
+        match receiver.await.expect("Failed to receive verdict from Verify Service") {
+            Ok(verdict) => verdict,
+            Err(status) => panic!("MI355X verification engine failure {} (every context failed)", status),
+        }
+    }
+
+    /// The crypto of `Certificate::verify` (primary/src/messages.rs:189-215):
+    /// the COA_CERT_* bits, 0 = every crypto check Ok.
+    pub async fn certificate(&self, crypto: CertificateCrypto) -> u8 {
+        let (sender, receiver) = oneshot::channel();
+        self.send(Request::Certificate(crypto, sender)).await;
+        match receiver.await.expect("Failed to receive status from Verify Service") {
+            Ok(bits) => bits,
+            Err(status) => panic!("MI355X verification engine failure {} (every context failed)", status),
+        }
+    }
+
+    /// `Digest(Sha512(bytes)[..32])` (worker/src/processor.rs:38), with the
+    /// bytes handed back (the queue copies them at submission; no clone).
+    pub async fn digest(&self, bytes: Vec<u8>) -> (Digest, Vec<u8>) {
+        let (sender, receiver) = oneshot::channel();
+        self.send(Request::Digest(bytes, sender)).await;
+        match receiver.await.expect("Failed to receive digest from Verify Service") {
+            Ok(reply) => reply,
+            Err(status) => panic!("MI355X verification engine failure {} (every context failed)", status),
+        }
+    }
+}
+
+fn verdict_of(byte: u8) -> Result<(), CryptoError> {
+    if byte == 0 {
+        Ok(())
+    } else {
+        Err(CryptoError::new())
+    }
+}
+
+/// One drained window of requests into the engine queue.
+fn submit_window(queue: &Queue, window: Vec<Request>) {
+    let mut senders: Vec<oneshot::Sender<Verdict>> = Vec::new();
+    let (mut msgs, mut keys, mut sigs) = (Vec::new(), Vec::new(), Vec::new());
+    for request in window {
+        match request {
+            Request::Verify(digest, key, signature, sender) => {
+                msgs.extend_from_slice(&digest.0);
+                keys.extend_from_slice(&key.0);
+                sigs.extend_from_slice(&signature);
+                senders.push(sender);
+            }
+            Request::Batch(digest, votes, sender) => submit_batch(queue, &digest, &votes, sender),
+            Request::Certificate(crypto, sender) => submit_certificate(queue, &crypto, sender),
+            Request::Digest(bytes, sender) => submit_digest(queue, bytes, sender),
+        }
+    }
+    if senders.is_empty() {
+        return;
+    }
+    let n = senders.len();
+    let user = Box::into_raw(Box::new(senders)) as *mut c_void;
+    let rc = unsafe {
+        ffi::coa_queue_submit_verify_many(queue.0, msgs.as_ptr(), keys.as_ptr(), sigs.as_ptr(), n,
+                                          Some(on_verdicts), user)
+    };
+    if rc != ffi::COA_OK {
+        // not queued: the callback will never run, so answer here
+        let senders = unsafe { Box::from_raw(user as *mut Vec<oneshot::Sender<Verdict>>) };
+        for sender in *senders {
+            let _ = sender.send(Err(rc));
+        }
+    }
+}
+
+fn submit_batch(queue: &Queue, digest: &Digest, votes: &[(PublicKey, [u8; 64])], sender: oneshot::Sender<Verdict>) {
+    let (mut keys, mut sigs) = (Vec::with_capacity(32 * votes.len()), Vec::with_capacity(64 * votes.len()));
+    for (key, signature) in votes {
+        keys.extend_from_slice(&key.0);
+        sigs.extend_from_slice(signature);
+    }
+    let user = Box::into_raw(Box::new(sender)) as *mut c_void;
+    let rc = unsafe {
+        ffi::coa_queue_submit_batch(queue.0, digest.0.as_ptr(), keys.as_ptr(), sigs.as_ptr(), votes.len(),
+                                    Some(on_verdict), user)
+    };
+    if rc != ffi::COA_OK {
+        let sender = unsafe { Box::from_raw(user as *mut oneshot::Sender<Verdict>) };
+        let _ = sender.send(Err(rc));
+    }
+}
+
+fn submit_certificate(queue: &Queue, c: &CertificateCrypto, sender: oneshot::Sender<Result<u8, c_int>>) {
+    let n_votes = c.vote_keys.len() / 32;
+    assert_eq!(c.vote_signatures.len(), 64 * n_votes, "64-byte signature per vote key");
+    let user = Box::into_raw(Box::new(sender)) as *mut c_void;
+    let rc = unsafe {
+        ffi::coa_queue_submit_certificate(queue.0, c.header_input.as_ptr(), c.header_input.len(), c.id.0.as_ptr(),
+                                          c.origin.0.as_ptr(), c.header_signature.as_ptr(), c.round,
+                                          c.vote_keys.as_ptr(), c.vote_signatures.as_ptr(), n_votes,
+                                          Some(on_status), user)
+    };
+    if rc != ffi::COA_OK {
+        let sender = unsafe { Box::from_raw(user as *mut oneshot::Sender<Result<u8, c_int>>) };
+        let _ = sender.send(Err(rc));
+    }
+}
+
+fn submit_digest(queue: &Queue, bytes: Vec<u8>, sender: oneshot::Sender<DigestReply>) {
+    // the bytes ride along with the sender and come back with the digest
+    let user = Box::into_raw(Box::new((sender, bytes))) as *mut c_void;
+    let (ptr, len) = unsafe {
+        let pair = &*(user as *const (oneshot::Sender<DigestReply>, Vec<u8>));
+        (pair.1.as_ptr(), pair.1.len())
+    };
+    let rc = unsafe { ffi::coa_queue_submit_digest(queue.0, ptr, len, Some(on_digest), user) };
+    if rc != ffi::COA_OK {
+        let pair = unsafe { Box::from_raw(user as *mut (oneshot::Sender<DigestReply>, Vec<u8>)) };
+        let (sender, _) = *pair;
+        let _ = sender.send(Err(rc));
+    }
+}
+
+// ------------------------------------------------------------- callbacks
+// coa_verdict_cb: void (*)(void* user, int status, const uint8_t* verdicts,
+// size_t n).  Each runs exactly once per queued request, on the engine's
+// completion thread; `user` is the boxed sender(s) given at submission.
+
+/// A coalesced window of `Signature::verify` requests: n verdict bytes, in
+/// the order of the senders.
+unsafe extern "C" fn on_verdicts(user: *mut c_void, status: c_int, verdicts: *const u8, n: usize) {
+    let senders = Box::from_raw(user as *mut Vec<oneshot::Sender<Verdict>>);
+    if status != ffi::COA_OK || verdicts.is_null() || n != senders.len() {
+        let failure = if status != ffi::COA_OK { status } else { ffi::COA_EINVAL };
+        for sender in *senders {
+            let _ = sender.send(Err(failure));
+        }
+        return;
+    }
+    let bytes = std::slice::from_raw_parts(verdicts, n);
+    for (sender, &byte) in senders.into_iter().zip(bytes) {
+        let _ = sender.send(Ok(verdict_of(byte)));
+    }
+}
+
+/// One vote batch: one verdict byte.
+unsafe extern "C" fn on_verdict(user: *mut c_void, status: c_int, verdicts: *const u8, n: usize) {
+    let sender = Box::from_raw(user as *mut oneshot::Sender<Verdict>);
+    let reply = if status != ffi::COA_OK {
+        Err(status)
+    } else if verdicts.is_null() || n != 1 {
+        Err(ffi::COA_EINVAL)
+    } else {
+        Ok(verdict_of(*verdicts))
+    };
+    let _ = sender.send(reply);
+}
+
+/// One certificate: one status byte of COA_CERT_* bits.
+unsafe extern "C" fn on_status(user: *mut c_void, status: c_int, verdicts: *const u8, n: usize) {
+    let sender = Box::from_raw(user as *mut oneshot::Sender<Result<u8, c_int>>);
+    let reply = if status != ffi::COA_OK {
+        Err(status)
+    } else if verdicts.is_null() || n != 1 {
+        Err(ffi::COA_EINVAL)
+    } else {
+        Ok(*verdicts)
+    };
+    let _ = sender.send(reply);
+}
+
+/// One worker batch: the 32-byte Digest, and the batch handed back.
+unsafe extern "C" fn on_digest(user: *mut c_void, status: c_int, verdicts: *const u8, n: usize) {
+    let pair = Box::from_raw(user as *mut (oneshot::Sender<DigestReply>, Vec<u8>));
+    let (sender, bytes) = *pair;
+    let reply = if status != ffi::COA_OK {
+        Err(status)
+    } else if verdicts.is_null() || n != 32 {
+        Err(ffi::COA_EINVAL)
+    } else {
+        let mut digest = [0u8; 32];
+        digest.copy_from_slice(std::slice::from_raw_parts(verdicts, 32));
+        Ok((Digest(digest), bytes))
+    };
+    let _ = sender.send(reply);
+}
+
+/// The process's service (created on first use, inside the tokio runtime):
+/// for callers whose constructors take no service handle -- the worker's
+/// `Processor::spawn` keeps the reference's signature this way.
+/// COA_SERVICE_MAX_BATCH / COA_SERVICE_MAX_DELAY_US tune it.
+pub fn global() -> VerifyService {
+    static SERVICE: std::sync::OnceLock<VerifyService> = std::sync::OnceLock::new();
+    SERVICE
+        .get_or_init(|| {
+            let batch = std::env::var("COA_SERVICE_MAX_BATCH").ok().and_then(|v| v.parse().ok()).unwrap_or(65_536);
+            let delay = std::env::var("COA_SERVICE_MAX_DELAY_US").ok().and_then(|v| v.parse().ok()).unwrap_or(500);
+            VerifyService::new(batch, delay)
+        })
+        .clone()
+}

@@ -18,9 +18,15 @@
 //!     crypto::gpu::register_committee(committee.authorities.keys());
 //! `primary/Cargo.toml` needs nothing new (crypto is already a dependency;
 //! the FFI lives in crypto's `coa_ffi`, re-exported below).
+//!
+//! A certificate the pre-verification stage (pre_verify.rs) already ran
+//! through the engine in a coalesced launch is answered from
+//! `crypto::verified` (keyed by every byte of its crypto input), so `Core`'s
+//! one-at-a-time call costs a lookup instead of a launch.
 use crate::error::{DagError, DagResult};
 use crate::messages::{Certificate, Header};
 use config::Committee;
+use crypto::service::CertificateCrypto;
 use crypto::{CryptoError, PublicKey};
 use std::collections::HashSet;
 use std::os::raw::c_int;
@@ -67,7 +73,7 @@ pub fn header_digest_input(h: &Header) -> Vec<u8> {
 /// The 64-byte R || s of a crypto::Signature through its serde form
 /// (the fields are private; bincode writes part1 then part2, 32 bytes each,
 /// with no length prefix for fixed arrays).
-fn signature_bytes(sig: &crypto::Signature) -> [u8; 64] {
+pub(crate) fn signature_bytes(sig: &crypto::Signature) -> [u8; 64] {
     let v = bincode::serialize(sig).expect("Signature serializes");
     let mut out = [0u8; 64];
     out.copy_from_slice(&v[..64]);
@@ -81,6 +87,22 @@ fn votes_flat(cert: &Certificate) -> (Vec<u8>, Vec<u8>) {
         sigs.extend_from_slice(&signature_bytes(sig));
     }
     (pks, sigs)
+}
+
+/// The crypto input of Certificate::verify in the engine's terms (the
+/// request `VerifyService::certificate` and `coa_certificate_verify` take).
+pub(crate) fn certificate_crypto(cert: &Certificate) -> CertificateCrypto {
+    let h = &cert.header;
+    let (vote_keys, vote_signatures) = votes_flat(cert);
+    CertificateCrypto {
+        header_input: header_digest_input(h),
+        id: h.id.clone(),
+        origin: h.author,
+        header_signature: signature_bytes(&h.signature),
+        round: h.round,
+        vote_keys,
+        vote_signatures,
+    }
 }
 
 /// The checks of Certificate::verify in the reference's order, the crypto
@@ -112,20 +134,22 @@ fn checks_in_order(cert: &Certificate, committee: &Committee, st: c_int) -> DagR
     Ok(())
 }
 
-/// Certificate::verify, one certificate (the engine's latency path: one
-/// H2D, one launch, one D2H).
+/// Certificate::verify, one certificate: the bits the pre-verification
+/// stage computed for exactly these bytes, or the engine's latency path (one
+/// launch with the certificate in its arguments, on an idle device context).
 pub fn verify(cert: &Certificate, committee: &Committee) -> DagResult<()> {
     // Genesis certificates are always valid (:191-193).
     if Certificate::genesis(committee).contains(cert) {
         return Ok(());
     }
-    let h = &cert.header;
-    let bytes = header_digest_input(h);
-    let (pks, sigs) = votes_flat(cert);
-    let hsig = signature_bytes(&h.signature);
+    let c = certificate_crypto(cert);
+    if let Some(bits) = crypto::verified::take_certificate(&c.key_bytes()) {
+        return checks_in_order(cert, committee, bits as c_int);
+    }
     let st = unsafe {
-        coa_certificate_verify(bytes.as_ptr(), bytes.len(), h.id.0.as_ptr(), h.author.0.as_ptr(), hsig.as_ptr(),
-                               h.round, pks.as_ptr(), sigs.as_ptr(), cert.votes.len(), 0)
+        coa_certificate_verify(c.header_input.as_ptr(), c.header_input.len(), c.id.0.as_ptr(), c.origin.0.as_ptr(),
+                               c.header_signature.as_ptr(), c.round, c.vote_keys.as_ptr(),
+                               c.vote_signatures.as_ptr(), cert.votes.len(), 0)
     };
     if st < 0 {
         engine_failure(st);

@@ -88,10 +88,71 @@ def test_no_placeholders_and_helpers_defined():
     # every free function called is defined in the shim, taken from the FFI,
     # or a std / reference crate API (method calls excluded)
     defined = set(re.findall(r"\bfn\s+(\w+)", text))
+    # names brought in by `use` (e.g. tokio's mpsc::channel) count as defined
+    for group in re.findall(r"\buse\s+[\w:]+::\{([^}]*)\}", text):
+        defined |= {n.strip().split(" as ")[-1].strip() for n in group.split(",") if n.strip()}
+    defined |= set(re.findall(r"\buse\s+[\w:]+::(\w+)\s*;", text))
     called = set(re.findall(r"(?<![\w.:!])([a-z_][a-z0-9_]*)\s*\(", text))
     keywords = {"if", "for", "while", "match", "assert", "assert_eq", "panic", "vec", "fn", "return", "Some", "Ok",
-                "Err", "ensure", "println", "loop", "in", "as", "unsafe", "move", "Box", "format", "mod", "let"}
+                "Err", "ensure", "println", "loop", "in", "as", "unsafe", "move", "Box", "format", "mod", "let",
+                "const", "mut", "pub"}
     unknown = sorted(called - defined - keywords)
     assert not unknown, unknown
     assert "header_digest_input" in defined
     assert os.path.exists(os.path.join(RUST, "crypto", "build.rs"))
+
+
+def _verdict_cb_params():
+    """Parameter kinds of the header's coa_verdict_cb typedef."""
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    m = re.search(r"typedef\s+void\s*\(\*\s*coa_verdict_cb\s*\)\s*\(([^)]*)\)\s*;", text)
+    assert m, "coa_verdict_cb typedef not found"
+    return [_c_kind(a.rsplit(" ", 1)[0]) for a in m.group(1).split(",")]
+
+
+def test_service_callbacks_match_coa_verdict_cb():
+    """rust/crypto/src/service.rs (the VerifyService over the queue): every
+    extern "C" callback has coa_verdict_cb's parameter kinds and returns
+    nothing, every coa_queue_submit_* call passes one of them, and each boxed
+    user pointer handed to the engine is taken back on every path (the
+    callback, and the submit-failure branch)."""
+    src = open(os.path.join(RUST, "crypto", "src", "service.rs")).read()
+    want = _verdict_cb_params()
+    assert want == ["ptr", "int", "ptr", "usize"]
+    # the FFI alias of the callback type agrees too
+    ffi = open(os.path.join(RUST, "crypto", "src", "coa_ffi.rs")).read()
+    m = re.search(r"type\s+CoaVerdictCb\s*=\s*Option<unsafe extern \"C\" fn\((.*?)\)>", ffi, flags=re.S)
+    assert m and [_r_kind(a.split(":", 1)[1]) for a in m.group(1).split(",") if a.strip()] == want
+    cbs = re.findall(r'unsafe extern "C" fn\s+(\w+)\s*\((.*?)\)\s*(->\s*[^{]+)?\{', src, flags=re.S)
+    assert len(cbs) >= 4
+    for name, args, ret in cbs:
+        assert not ret, (name, ret)
+        assert [_r_kind(a.split(":", 1)[1]) for a in args.split(",") if a.strip()] == want, name
+    names = {n for n, _, _ in cbs}
+    submits = re.findall(r"ffi::(coa_queue_submit_\w+)\((.*?)\)\s*\}?;", src, flags=re.S)
+    assert {s for s, _ in submits} >= {"coa_queue_submit_verify_many", "coa_queue_submit_batch",
+                                       "coa_queue_submit_certificate", "coa_queue_submit_digest"}
+    for fn_name, args in submits:
+        cb = re.search(r"Some\((\w+)\)", args)
+        assert cb and cb.group(1) in names, fn_name
+    # Box::into_raw / Box::from_raw balance per boxed type: each callback and
+    # each submit-failure branch takes back what the submit gave away
+    given = re.findall(r"Box::into_raw\(Box::new\(", src)
+    taken = re.findall(r"Box::from_raw\(user as \*mut ", src)
+    assert len(given) == 4 and len(taken) == 8, (len(given), len(taken))
+    assert "panic!" not in "".join(re.findall(r'unsafe extern "C" fn.*?\n\}', src, flags=re.S))
+
+
+def test_pre_verification_stage_and_processor_use_the_service():
+    """The stage in front of Core and the worker's Processor go through the
+    service (coalesced launches), and the synchronous drop-in calls consult
+    the verdicts the stage computed."""
+    pre = open(os.path.join(RUST, "primary", "src", "pre_verify.rs")).read()
+    assert "FuturesOrdered" in pre and "service.verify(" in pre and "service.certificate(" in pre
+    assert "remember_signature" in pre and "remember_certificate" in pre
+    proc_ = open(os.path.join(RUST, "worker", "src", "processor.rs")).read()
+    assert "service.digest(" in proc_ and "FuturesOrdered" in proc_ and "sha512_digest" not in proc_
+    gpu = open(os.path.join(RUST, "crypto", "src", "gpu.rs")).read()
+    assert "verified::take_signature" in gpu
+    cert = open(os.path.join(RUST, "primary", "src", "gpu_certificate.rs")).read()
+    assert "verified::take_certificate" in cert
