@@ -69,6 +69,8 @@ def parse():
                     help="A/B only: a timing event pair around every timed call (round-1 method)")
     ap.add_argument("--c3-certs", type=int, default=10000, help="C3 certificates per round")
     ap.add_argument("--c4-batches", type=str, default="1024,16384")
+    ap.add_argument("--sections", type=str, default="",
+                    help="comma list: run only these secondary sections (A/B runs; default all)")
     return ap.parse_args()
 
 
@@ -453,9 +455,30 @@ def c4_sha512(local, dev, stream, counts, steps, cpu_threads):
                                 "batches_per_s": round(nb / (ms * 1e-3), 1)}
         del data, dig
         torch.cuda.empty_cache()
-    # CPU: the C SHA-512 over host copies, all threads
+    # one batch per call through the host-pointer C ABI (what a per-batch
+    # drop-in of worker/src/processor.rs:38 would pay), and one CPU core
+    one = workloads.worker_batch(0)
+    one_a = np.frombuffer(one, np.uint8)
+    lat = []
+    for i in range(23):
+        t0 = time.perf_counter()
+        dg = coa_crypto.digest_many([one])
+        lat.append(time.perf_counter() - t0)
+    assert bytes(dg[0]) == hashlib.sha512(one).digest()[:32]
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coa_oracle
+
+    cl = []
+    for i in range(23):
+        t0 = time.perf_counter()
+        coa_oracle.sha512_many(one_a, np.array([0, len(one)], np.uint64), 1)
+        cl.append(time.perf_counter() - t0)
+    out["single_batch"] = {"gpu_p50_ms": round(float(np.percentile(np.array(lat[3:]) * 1e3, 50)), 3),
+                           "cpu_one_core_p50_ms": round(float(np.percentile(np.array(cl[3:]) * 1e3, 50)), 3),
+                           "note": "one 508 KB batch per call: a serial chain of 3,970 compressions, slower on "
+                                   "a GPU lane pair than on a CPU core; the worker streams batches through the "
+                                   "queue instead (c4_stream)"}
+    # CPU: the C SHA-512 over host copies, all threads
 
     nbc = 4 * cpu_threads  # 64 distinct batches, tiled (the digest work does not depend on the bytes)
     host = np.tile(np.frombuffer(b"".join(workloads.worker_batch(b) for b in range(64)), np.uint8),
@@ -467,6 +490,187 @@ def c4_sha512(local, dev, stream, counts, steps, cpu_threads):
     out["cpu_baseline"] = {"GBps": round(host.size / el / 1e9, 3), "cores": cpu_threads, "kind": "port",
                            "sample": f"{nbc} batches, {cpu_threads} threads (every usable CPU)"}
     return out
+
+
+def _latc_paced_lib():
+    import ctypes
+
+    lib = _latc()
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    # max_batch, max_delay_us, n; arrive, kind, item; 4 verify, 10
+    # certificate and 3 digest arrays; lat_us, elapsed_s, metrics
+    lib.latc_paced.argtypes = [sz, ctypes.c_uint, sz] + [vp] * 3 + [vp] * 17 + [vp] * 3
+    lib.latc_paced.restype = ctypes.c_int
+    return lib
+
+
+def paced_queue(arrive_s, kind, item, vm=None, vp=None, vs=None, vexp=None, certs=None, cexp=None, ddata=None,
+                doff=None, dexp=None, max_batch=65536, max_delay_us=500):
+    """One paced run through the aggregation queue (tools/latc.c latc_paced):
+    requests arrive at arrive_s (seconds), each answer is checked against its
+    expectation; returns the latencies (ms, from the scheduled arrival to the
+    callback), the wall time and the queue metrics."""
+    import ctypes
+
+    import numpy as np
+
+    import coa_crypto
+
+    lib = _latc_paced_lib()
+    n = len(arrive_s)
+    z8, z64 = np.zeros(64, np.uint8), np.zeros(2, np.uint64)
+    A = lambda a, dt=np.uint8: np.ascontiguousarray(a, dtype=dt) if a is not None else (z8 if dt == np.uint8 else z64)  # noqa: E731,E501
+    arrive = np.ascontiguousarray(arrive_s, np.float64)
+    kind_a, item_a = np.ascontiguousarray(kind, np.int32), np.ascontiguousarray(item, np.uint32)
+    if certs is not None:
+        hd = np.frombuffer(b"".join(certs.header_inputs) + bytes(16), np.uint8)
+        hoff = np.zeros(len(certs) + 1, np.uint64)
+        hoff[1:] = np.cumsum([len(h) for h in certs.header_inputs])
+        c_arrs = [hd, hoff, certs.ids, certs.authors, certs.header_sigs,
+                  np.full(len(certs), certs.round, np.uint64), certs.vote_pks, certs.vote_sigs, certs.offsets]
+        c_arrs = [np.ascontiguousarray(a) for a in c_arrs]
+    else:
+        c_arrs = [z8, z64, z8, z8, z8, z64, z8, z8, z64]
+    keep = [A(vm), A(vp), A(vs), A(vexp)] + c_arrs + [A(cexp), A(ddata), A(doff, np.uint64), A(dexp)]
+    lat = np.zeros(max(n, 1), np.float64)
+    el = ctypes.c_double()
+    m = coa_crypto.QueueMetrics()
+    wrong = lib.latc_paced(max_batch, max_delay_us, n, arrive.ctypes.data, kind_a.ctypes.data, item_a.ctypes.data,
+                           *[a.ctypes.data for a in keep], lat.ctypes.data, ctypes.addressof(el),
+                           ctypes.addressof(m))
+    assert wrong == 0, f"paced queue run: {wrong} wrong answers"
+    met = {name: getattr(m, name) for name, _ in coa_crypto.QueueMetrics._fields_}
+    return lat[:n] * 1e-3, el.value, met
+
+
+def c4_stream(cpu_p50_batch_ms, rates=(1000, 4000), seconds=1.5):
+    """C4 as the worker streams it (rust/worker/src/processor.rs): 508 KB
+    batches arriving at a fixed rate (1,000/s = BASELINE C4's 1M tx/s of
+    512 B), each submitted to the aggregation queue as it arrives
+    (coa_queue_submit_digest); the queue's windows hash every batch that
+    arrived during the previous launch in one launch.  Per-batch latency =
+    scheduled arrival -> digest callback; every digest is checked against
+    hashlib.  Beside it: one CPU core's p50 for one batch (the reference's
+    serial Processor loop), whose reciprocal is the rate one core sustains."""
+    import hashlib
+
+    import numpy as np
+
+    import workloads
+
+    nb = 32
+    blobs = [workloads.worker_batch(b) for b in range(nb)]
+    data = np.frombuffer(b"".join(blobs) + bytes(16), np.uint8)
+    offs = np.zeros(nb + 1, np.uint64)
+    offs[1:] = np.cumsum([len(b) for b in blobs])
+    dexp = np.frombuffer(b"".join(hashlib.sha512(b).digest()[:32] for b in blobs), np.uint8)
+    out = {"workload": "C4 streamed: 508,052-byte worker batches arriving at a fixed rate, one "
+                       "coa_queue_submit_digest each (the streamed Processor), digests checked",
+           "queue": {"max_batch": 65536, "max_delay_us": 500}}
+    for rate in rates:
+        n = int(rate * seconds)
+        arrive = np.arange(n) / rate
+        lat, el, met = paced_queue(arrive, np.full(n, 2), np.arange(n) % nb, ddata=data, doff=offs, dexp=dexp)
+        out[f"rate_{rate}"] = {"batches": n, "achieved_batches_per_s": round(n / el, 1),
+                               "p50_ms": round(float(np.percentile(lat, 50)), 3),
+                               "p99_ms": round(float(np.percentile(lat, 99)), 3),
+                               "windows": met["windows"], "mean_batches_per_window": round(n / max(1, met["windows"]), 1),
+                               "retried_windows": met["retried_windows"]}
+    if cpu_p50_batch_ms:
+        out["cpu_one_core"] = {"p50_ms_per_batch": cpu_p50_batch_ms,
+                               "max_batches_per_s": round(1e3 / cpu_p50_batch_ms, 1),
+                               "note": "the reference's Processor hashes serially on one task: it sustains at most "
+                                       "1 / p50 batches/s per Processor"}
+    return out
+
+
+def queue_round_mix(rates=(5, 10, 100, 300, 1000), seconds=0.6, committee_size=100, n_payload=32):
+    """The aggregation queue at committee-100 arrival rates: each round
+    brings 100 certificates (67 votes each, fused Certificate::verify crypto)
+    and 200 header/vote signatures (Signature::verify, committee keys),
+    spread evenly over the round's period; rounds arrive at `rate` per second.
+    Per-request latency = scheduled arrival -> callback, by kind.  Beside it
+    the reference's Core::run, which verifies the same messages one at a time
+    on ONE task (primary/src/core.rs:349-389): a single FIFO server whose
+    service times are the single-core CPU restatement's measured p50s
+    (simulated queue; above ~9 rounds/s it cannot keep up)."""
+    import numpy as np
+
+    import certificates as C
+    import coa_crypto
+    import workloads
+
+    committee, certs = C.synth_certificates(committee_size, committee_size=committee_size, n_payload=n_payload,
+                                            seed=11)
+    committee.register()
+    seeds = workloads.key_seeds(committee_size)
+    ns = 2 * committee_size
+    idx = np.arange(ns) % committee_size
+    msgs = workloads.messages(ns, start=70_000)
+    pks, sigs = coa_crypto.sign_many(seeds[idx], msgs)
+    per_round = committee_size + ns
+    # certificate and signature requests interleaved over the round
+    kinds = np.array([1 if j % 3 == 0 else 0 for j in range(per_round)], np.int32)
+    items = np.zeros(per_round, np.uint32)
+    items[kinds == 1] = np.arange(committee_size)
+    items[kinds == 0] = np.arange(ns)
+    res = {"workload": f"committee {committee_size}: per round {committee_size} certificates "
+                       f"({committee.quorum_threshold()} votes) + {ns} header/vote signatures, evenly spread",
+           "queue": {"max_batch": 65536, "max_delay_us": 200}, "rates": {}}
+    # CPU service times (one core, the C restatement of dalek): measured
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import random
+
+    import coa_oracle
+
+    rnd = random.Random(5)
+    ct = []
+    for c in range(min(40, committee_size)):
+        lo, hi = int(certs.offsets[c]), int(certs.offsets[c + 1])
+        zs = [rnd.getrandbits(128) for _ in range(hi - lo)]
+        t1 = time.perf_counter()
+        assert coa_oracle.certificate_verify(certs.header_inputs[c], certs.ids[c], certs.authors[c],
+                                             certs.header_sigs[c], certs.round, certs.vote_pks[lo:hi],
+                                             certs.vote_sigs[lo:hi], zs)
+        ct.append(time.perf_counter() - t1)
+    t1 = time.perf_counter()
+    v = coa_oracle.verify_strict_many(msgs, pks, sigs, 1)
+    st_single = (time.perf_counter() - t1) / ns
+    assert int(v.sum()) == 0
+    st_cert = float(np.percentile(ct[5:], 50))
+    res["cpu_service_ms"] = {"certificate": round(st_cert * 1e3, 4), "signature": round(st_single * 1e3, 4),
+                             "round": round((committee_size * st_cert + ns * st_single) * 1e3, 2),
+                             "max_rounds_per_s": round(1.0 / (committee_size * st_cert + ns * st_single), 2)}
+    for rate in rates:
+        rounds = max(3, int(rate * seconds))
+        n = rounds * per_round
+        arrive = (np.arange(n) // per_round + (np.arange(n) % per_round) / per_round) / rate
+        kind = np.tile(kinds, rounds)
+        item = np.tile(items, rounds)
+        lat, el, met = paced_queue(arrive, kind, item, vm=msgs, vp=pks, vs=sigs, vexp=np.zeros(ns, np.uint8),
+                                   certs=certs, cexp=np.zeros(committee_size, np.uint8), max_delay_us=200)
+        # the reference: one FIFO server, deterministic service times
+        svc = np.where(kind == 1, st_cert, st_single)
+        done = np.empty(n)
+        t = 0.0
+        for i in range(n):
+            t = max(t, arrive[i]) + svc[i]
+            done[i] = t
+        cpu_lat = (done - arrive) * 1e3
+        row = {"rounds": rounds, "requests": n, "achieved_requests_per_s": round(n / el, 1),
+               "windows": met["windows"], "mean_requests_per_window": round(n / max(1, met["windows"]), 1)}
+        for k, name in ((1, "certificate"), (0, "signature")):
+            sel = kind == k
+            row[name] = {"p50_ms": round(float(np.percentile(lat[sel], 50)), 3),
+                         "p99_ms": round(float(np.percentile(lat[sel], 99)), 3),
+                         "cpu_core_run_p50_ms": round(float(np.percentile(cpu_lat[sel], 50)), 3),
+                         "cpu_core_run_p99_ms": round(float(np.percentile(cpu_lat[sel], 99)), 3)}
+        row["queue_wait_us_p50"] = round(met["wait_us_p50"], 1)
+        row["queue_wait_us_p99"] = round(met["wait_us_p99"], 1)
+        row["cpu_saturated"] = bool(rate > res["cpu_service_ms"]["max_rounds_per_s"])
+        res["rates"][str(rate)] = row
+    coa_crypto.committee_register(np.zeros((0, 32), np.uint8))
+    return res
 
 
 def certificate_config(n_certs, latency_samples, cpu_threads, dev, stream, committee_size=100, n_payload=32,
@@ -864,17 +1068,30 @@ def main():
         threads = usable_cpus()
         del ws
         torch.cuda.empty_cache()
-        secondary = {
-            "verify_single": verify_single(local, cpu["single_verify_p50_ms"] if cpu else None),
-            "c5_shard": c5_shard(local, dev, stream),
-            "verify_batch": verify_batch_config(local, dev, stream),
-            "c4_sha512": c4_sha512(local, dev, stream, [int(x) for x in args.c4_batches.split(",") if x], 2,
-                                   threads),
-            "c3_certificate_verify": certificate_config(args.c3_certs, 1000, threads, dev, stream,
-                                                        cpu_thread_seconds=args.cpu_thread_seconds),
-            "c1_certificate_verify": certificate_config(2000, 1000, threads, dev, stream, committee_size=4,
-                                                        n_payload=1, cpu_thread_seconds=args.cpu_thread_seconds),
-        }
+        want = set(x for x in args.sections.split(",") if x)
+        on = lambda name: not want or name in want  # noqa: E731
+        secondary = {}
+        if on("verify_single"):
+            secondary["verify_single"] = verify_single(local, cpu["single_verify_p50_ms"] if cpu else None)
+        if on("c5_shard"):
+            secondary["c5_shard"] = c5_shard(local, dev, stream)
+        if on("verify_batch"):
+            secondary["verify_batch"] = verify_batch_config(local, dev, stream)
+        if on("c4_sha512"):
+            secondary["c4_sha512"] = c4_sha512(local, dev, stream, [int(x) for x in args.c4_batches.split(",") if x],
+                                               2, threads)
+        if on("c3_certificate_verify"):
+            secondary["c3_certificate_verify"] = certificate_config(args.c3_certs, 1000, threads, dev, stream,
+                                                                    cpu_thread_seconds=args.cpu_thread_seconds)
+        if on("c1_certificate_verify"):
+            secondary["c1_certificate_verify"] = certificate_config(2000, 1000, threads, dev, stream,
+                                                                    committee_size=4, n_payload=1,
+                                                                    cpu_thread_seconds=args.cpu_thread_seconds)
+        if on("c4_stream"):
+            c4 = secondary.get("c4_sha512", {})
+            secondary["c4_stream"] = c4_stream(c4.get("single_batch", {}).get("cpu_one_core_p50_ms"))
+        if on("queue_round_mix"):
+            secondary["queue_round_mix"] = queue_round_mix()
 
     if rank == 0:
         line = {

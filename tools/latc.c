@@ -48,3 +48,97 @@ int latc_verify(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, in
   }
   return 0;
 }
+
+/* ------------------------------------------------------------------------
+ * Paced arrivals through the aggregation queue (coa_queue_*): request i is
+ * due arrive_s[i] seconds after the start; this thread sleeps until it is due
+ * and submits it (a late request goes at once: its latency is measured from
+ * the SCHEDULED arrival, so a producer or queue that falls behind shows up as
+ * latency, not as a quietly lower rate).  kind[i]:
+ *   0  Signature::verify of triple item[i] (vmsgs / vpks / vsigs)
+ *   1  Certificate::verify of certificate item[i] (c_* arrays: header bytes
+ *      with c_hoff offsets, ids, origins, header signatures, rounds, votes
+ *      with c_voff offsets)
+ *   2  Sha512 digest of message item[i] (d_data with d_off offsets)
+ * Expected answers: v_expect[item] verdict byte, c_expect[item] status byte,
+ * d_expect[32 * item] digest.  lat_us[i] = callback time - scheduled arrival.
+ * Returns the number of wrong or failed answers (>= 0); queue metrics into
+ * *m, wall time from the first arrival to the last answer into *elapsed_s. */
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct {
+  double due_us;
+  double* out;
+  const uint8_t* expect;
+  size_t n_expect;
+  atomic_int* wrong;
+} PacedReq;
+
+static double g_paced_t0;
+
+static void paced_cb(void* user, int status, const uint8_t* v, size_t n) {
+  PacedReq* r = (PacedReq*)user;
+  *r->out = now_us() - g_paced_t0 - r->due_us;
+  if (status != COA_OK || n != r->n_expect || memcmp(v, r->expect, n) != 0) atomic_fetch_add(r->wrong, 1);
+}
+
+static void sleep_until_us(double t_us) {
+  for (;;) {
+    const double left = t_us - (now_us() - g_paced_t0);
+    if (left <= 0) return;
+    if (left > 300.0) {
+      struct timespec ts = {0, (long)((left - 150.0) * 1e3)};
+      nanosleep(&ts, NULL);
+    }
+  }
+}
+
+int latc_paced(size_t max_batch, unsigned max_delay_us, size_t n, const double* arrive_s, const int* kind,
+               const uint32_t* item, const uint8_t* vmsgs, const uint8_t* vpks, const uint8_t* vsigs,
+               const uint8_t* v_expect, const uint8_t* c_hdata, const uint64_t* c_hoff, const uint8_t* c_ids,
+               const uint8_t* c_origins, const uint8_t* c_hsigs, const uint64_t* c_rounds, const uint8_t* c_vpks,
+               const uint8_t* c_vsigs, const uint64_t* c_voff, const uint8_t* c_expect, const uint8_t* d_data,
+               const uint64_t* d_off, const uint8_t* d_expect, double* lat_us, double* elapsed_s,
+               coa_queue_metrics_t* m) {
+  coa_queue* q = coa_queue_create(max_batch, max_delay_us);
+  if (!q) return -1;
+  PacedReq* reqs = (PacedReq*)calloc(n ? n : 1, sizeof(PacedReq));
+  atomic_int wrong = 0;
+  g_paced_t0 = now_us();
+  for (size_t i = 0; i < n; i++) {
+    PacedReq* r = &reqs[i];
+    r->due_us = arrive_s[i] * 1e6;
+    r->out = &lat_us[i];
+    r->wrong = &wrong;
+    const size_t k = item[i];
+    sleep_until_us(r->due_us);
+    int rc;
+    if (kind[i] == 0) {
+      r->expect = v_expect + k;
+      r->n_expect = 1;
+      rc = coa_queue_submit_verify(q, vmsgs + 32 * k, vpks + 32 * k, vsigs + 64 * k, paced_cb, r);
+    } else if (kind[i] == 1) {
+      r->expect = c_expect + k;
+      r->n_expect = 1;
+      rc = coa_queue_submit_certificate(q, c_hdata + c_hoff[k], c_hoff[k + 1] - c_hoff[k], c_ids + 32 * k,
+                                        c_origins + 32 * k, c_hsigs + 64 * k, c_rounds[k], c_vpks + 32 * c_voff[k],
+                                        c_vsigs + 64 * c_voff[k], c_voff[k + 1] - c_voff[k], paced_cb, r);
+    } else {
+      r->expect = d_expect + 32 * k;
+      r->n_expect = 32;
+      rc = coa_queue_submit_digest(q, d_data + d_off[k], d_off[k + 1] - d_off[k], paced_cb, r);
+    }
+    if (rc != COA_OK) {
+      lat_us[i] = -1.0;
+      atomic_fetch_add(&wrong, 1);
+    }
+  }
+  coa_queue_flush(q);
+  *elapsed_s = (now_us() - g_paced_t0) * 1e-6;
+  coa_queue_metrics(q, m);
+  coa_queue_destroy(q);
+  free(reqs);
+  return atomic_load(&wrong);
+}

@@ -25,3 +25,14 @@ struct LatArgs {
 
 // One 256-thread workgroup (four waves) per signature.
 hipError_t coa_launch_verify_lat(const LatArgs& a, hipStream_t s);
+
+// The latency kernel over device-resident inputs, enqueued on `stream`
+// (coa_runtime.cpp; the aggregation queue's small signature windows):
+// d_in [n][128 B] = msg | pk | R | s, d_res [n] words (1 << 8) | verdict.
+// Reads device `device`'s committee key cache: the caller holds that
+// device's key-cache read gate (coa_committee.h) until the kernel has run.
+// Returns COA_OK or a negative COA_E*.
+extern "C" int coa_lat_verify_device(int device, const uint8_t* d_in, size_t n, uint32_t* d_res, void* stream);
+// Calls of at most this many signatures (32-byte messages) take the latency
+// kernel (COA_LAT_MAX, default 2048).
+extern "C" size_t coa_lat_max(void);

@@ -46,8 +46,10 @@
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -128,6 +130,83 @@ double bucket_mid(int b) {
   return std::ldexp(1.0 + (m + 0.5) / 8.0, e);
 }
 
+// Callback helpers: the completion thread answers a large launch together
+// with kHelpers threads, each taking contiguous runs of requests (a launch
+// of 10^5 single signatures is 10^5 callbacks: on one thread they, not the
+// GPU, set the queue's rate).  Launches still complete in order: the next
+// one starts only when every run of this one has been answered.
+constexpr int kHelpersDefault = 3;         // COA_QUEUE_HELPERS overrides (0..15; read at queue creation)
+constexpr size_t kParallelAnswer = 8192;  // requests per launch from which the helpers join
+constexpr size_t kRun = 4096;             // requests per run
+
+struct AnswerPool {
+  std::mutex m;
+  std::condition_variable cv, done_cv;
+  std::function<void(size_t)> job;
+  size_t runs = 0, next = 0, done = 0;
+  uint64_t gen = 0;
+  bool stop = false;
+  std::vector<std::thread> th;
+
+  void start(int n) {
+    for (int i = 0; i < n; i++) th.emplace_back([this] { loop(); });
+  }
+  ~AnswerPool() {
+    {
+      std::lock_guard<std::mutex> l(m);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+  // Runs f(0..n-1) on the helpers and the calling thread; returns when all ran.
+  void run(size_t n, std::function<void(size_t)> f) {
+    {
+      std::lock_guard<std::mutex> l(m);
+      job = std::move(f);
+      runs = n;
+      next = 0;
+      done = 0;
+      gen++;
+    }
+    cv.notify_all();
+    work();
+    std::unique_lock<std::mutex> l(m);
+    done_cv.wait(l, [&] { return done == runs; });
+    job = nullptr;
+  }
+
+ private:
+  // takes runs until none is left (caller or helper)
+  void work() {
+    for (;;) {
+      size_t i;
+      std::function<void(size_t)>* f;
+      {
+        std::lock_guard<std::mutex> l(m);
+        if (next >= runs) return;
+        i = next++;
+        f = &job;
+      }
+      (*f)(i);
+      std::lock_guard<std::mutex> l(m);
+      if (++done == runs) done_cv.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(m);
+        cv.wait(l, [&] { return stop || (gen != seen && next < runs); });
+        if (stop) return;
+        seen = gen;
+      }
+      work();
+    }
+  }
+};
+
 }  // namespace
 
 struct coa_queue {
@@ -157,6 +236,9 @@ struct coa_queue {
   uint64_t m_hist[HB] = {};
 
   std::thread collector, completer;
+  AnswerPool helpers;  // started lazily by the first large launch
+  int n_helpers = kHelpersDefault;
+  bool helpers_on = false;
 
   coa_queue() {
     for (size_t i = 0; i < kShards; i++) {
@@ -289,20 +371,35 @@ struct coa_queue {
       const bool retried = recoverable(f.L.rc);
       if (retried) recover(f.L);
       const int rc = f.L.rc;
-      // callbacks; wait times from a clock read every 32 requests
-      uint64_t hist[HB] = {};
-      double wsum = 0.0, wmax = 0.0;
-      uint64_t nreq = 0;
-      int64_t tnow = now_ns();
+      // callbacks, in runs of contiguous requests (helpers join for large
+      // launches); wait times from a clock read every 32 requests
+      struct Seg {
+        const Part* p;
+        size_t lo, hi;
+      };
+      std::vector<Seg> segs;
+      size_t nreq = 0;
       for (const Part& p : f.parts) {
-        const Window& w = *p.w;
-        for (const Req& r : p.reqs) {
-          if ((nreq & 31) == 31) tnow = now_ns();
-          nreq++;
+        for (size_t lo = 0; lo < p.reqs.size(); lo += kRun) segs.push_back({&p, lo, std::min(p.reqs.size(), lo + kRun)});
+        nreq += p.reqs.size();
+      }
+      struct Tally {
+        uint64_t hist[HB] = {};
+        double wsum = 0.0, wmax = 0.0;
+      };
+      std::vector<Tally> tallies(segs.size());
+      auto answer_seg = [&](size_t si) {
+        const Seg& g = segs[si];
+        const Window& w = *g.p->w;
+        Tally& t = tallies[si];
+        int64_t tnow = now_ns();
+        for (size_t k = g.lo; k < g.hi; k++) {
+          const Req& r = g.p->reqs[k];
+          if (((k - g.lo) & 31) == 31) tnow = now_ns();
           const double us = (double)(tnow - r.t0) * 1e-3;
-          wsum += us;
-          wmax = std::max(wmax, us);
-          hist[wait_bucket(us)]++;
+          t.wsum += us;
+          t.wmax = std::max(t.wmax, us);
+          t.hist[wait_bucket(us)]++;
           switch (r.kind) {
             case K_VERIFY: r.cb(r.user, rc, w.v_out.data() + r.idx, r.n); break;
             case K_BATCH: r.cb(r.user, rc, w.g_out.data() + r.idx, 1); break;
@@ -310,6 +407,22 @@ struct coa_queue {
             case K_DIGEST: r.cb(r.user, rc, w.d_out.data() + (size_t)r.idx * 32, 32); break;
           }
         }
+      };
+      if (n_helpers > 0 && nreq >= kParallelAnswer && segs.size() > 1) {
+        if (!helpers_on) {
+          helpers.start(n_helpers);
+          helpers_on = true;
+        }
+        helpers.run(segs.size(), answer_seg);
+      } else {
+        for (size_t si = 0; si < segs.size(); si++) answer_seg(si);
+      }
+      uint64_t hist[HB] = {};
+      double wsum = 0.0, wmax = 0.0;
+      for (const Tally& t : tallies) {
+        for (int b = 0; b < HB; b++) hist[b] += t.hist[b];
+        wsum += t.wsum;
+        wmax = std::max(wmax, t.wmax);
       }
       // recycle each part's window and request vector into its shard
       for (Part& p : f.parts) {
@@ -381,6 +494,7 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
   coa_queue* q = new coa_queue();
   q->max_batch = max_batch ? max_batch : 65536;
   q->max_delay = std::chrono::microseconds(max_delay_us);
+  if (const char* e = getenv("COA_QUEUE_HELPERS")) q->n_helpers = std::max(0, std::min(15, atoi(e)));
   q->be.reset(coa_q::make_backend());
   q->start();
   return q;

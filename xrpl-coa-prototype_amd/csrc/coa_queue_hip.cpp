@@ -11,7 +11,9 @@
 // overlap the kernels of the other.
 //
 // Per kind:
-//   signatures    coa_ed25519_verify_strict_many_device (Signature::verify)
+//   signatures    coa_ed25519_verify_strict_many_device (Signature::verify);
+//                 windows of at most COA_LAT_MAX (2,048) signatures take the
+//                 latency kernel instead (one workgroup per signature)
 //   certificates  coa_certificate_verify_many_device (the fused
 //                 Certificate::verify crypto); the raw status words that need
 //                 the exact random-linear-combination check or carry a key
@@ -43,6 +45,7 @@
 #include <vector>
 
 #include "coa_committee.h"
+#include "coa_latency.h"
 #include "coa_queue.h"
 
 #define COA_QUEUE_SLOTS_DEFAULT 2
@@ -64,6 +67,7 @@ struct Slot {
   bool busy = false;
   bool launched = false;  // device work was enqueued (complete() must drain it)
   bool gate = false;      // holds the device's key-cache read gate
+  bool lat = false;       // the launch's signatures took the latency kernel (result words)
   // output offsets of the current launch
   size_t o_v = 0, o_c = 0, o_d = 0;
 };
@@ -229,20 +233,26 @@ class HipBackend : public coa_q::Backend {
   // 64-byte digests.
   int enqueue(Slot& sl, coa_q::Launch& L, bool inject) {
     if (hipSetDevice(sl.dev) != hipSuccess) return COA_EHIP;
+    // a window of few signatures takes the latency kernel (one four-wave
+    // workgroup per signature: ~0.1 ms however few, against ~0.8 ms for the
+    // one-lane throughput kernels); its inputs are interleaved 128-byte
+    // records and its results 32-bit words
+    sl.lat = L.nv > 0 && L.nv <= coa_lat_max();
     size_t o = 0;
     auto take = [&](size_t bytes) {
       const size_t at = o;
       o = al256(o + bytes);
       return at;
     };
-    const size_t i_vm = take(L.nv * 32), i_vp = take(L.nv * 32), i_vs = take(L.nv * 64);
+    const size_t i_vm = take(L.nv * (sl.lat ? 128 : 32)), i_vp = take(sl.lat ? 0 : L.nv * 32),
+                 i_vs = take(sl.lat ? 0 : L.nv * 64);
     const size_t i_ch = take(L.hbytes + 16), i_cho = take((L.nc + 1) * 8), i_cid = take(L.nc * 32),
                  i_cor = take(L.nc * 32), i_chs = take(L.nc * 64), i_crd = take(L.nc * 8),
                  i_cvp = take(L.nvotes * 32), i_cvs = take(L.nvotes * 64), i_cvo = take((L.nc + 1) * 8);
     const size_t i_dd = take(L.dbytes + 16), i_do = take((L.nd + 1) * 8);
     const size_t in_bytes = o;
     o = 0;
-    sl.o_v = take(L.nv);
+    sl.o_v = take(sl.lat ? L.nv * 4 : L.nv);
     sl.o_c = take(L.nc * 4);
     sl.o_d = take(L.nd * 64);
     const size_t out_bytes = o;
@@ -260,7 +270,15 @@ class HipBackend : public coa_q::Backend {
     uint64_t* dof = reinterpret_cast<uint64_t*>(h + i_do);
     cho[0] = cvo[0] = dof[0] = 0;
     for (const coa_q::Window* w : L.parts) {
-      if (w->nv) {
+      if (w->nv && sl.lat) {  // i_vm .. : [nv][msg | pk | R | s]
+        for (size_t i = 0; i < w->nv; i++) {
+          uint8_t* r = h + i_vm + (v + i) * 128;
+          std::memcpy(r, w->v_msgs.data() + i * 32, 32);
+          std::memcpy(r + 32, w->v_pks.data() + i * 32, 32);
+          std::memcpy(r + 64, w->v_sigs.data() + i * 64, 64);
+        }
+        v += w->nv;
+      } else if (w->nv) {
         std::memcpy(h + i_vm + v * 32, w->v_msgs.data(), w->nv * 32);
         std::memcpy(h + i_vp + v * 32, w->v_pks.data(), w->nv * 32);
         std::memcpy(h + i_vs + v * 64, w->v_sigs.data(), w->nv * 64);
@@ -299,12 +317,16 @@ class HipBackend : public coa_q::Backend {
     sl.launched = true;
     if (inject) return COA_EHIP;  // fault injection: the copy is in flight, the kernels never run
     int rc = COA_OK;
-    if (L.nv)
+    if ((sl.lat || L.nc) && !sl.gate) {  // both read the committee key cache
+      coa_keycache_read_acquire(sl.dev);
+      sl.gate = true;
+    }
+    if (L.nv && sl.lat)
+      rc = coa_lat_verify_device(sl.dev, d + i_vm, L.nv, reinterpret_cast<uint32_t*>(dout + sl.o_v), sl.s);
+    else if (L.nv)
       rc = coa_ed25519_verify_strict_many_device(sl.dev, d + i_vm, 32, d + i_vp, d + i_vs, L.nv, dout + sl.o_v, sl.ws,
                                                  sl.s);
     if (rc == COA_OK && L.nc) {
-      coa_keycache_read_acquire(sl.dev);
-      sl.gate = true;
       rc = coa_certificate_verify_many_device(
           sl.dev, d + i_ch, reinterpret_cast<const uint64_t*>(d + i_cho), d + i_cid, d + i_cor, d + i_chs,
           reinterpret_cast<const uint64_t*>(d + i_crd), d + i_cvp, d + i_cvs,
@@ -336,7 +358,12 @@ class HipBackend : public coa_q::Backend {
       const uint8_t* h = static_cast<const uint8_t*>(sl.hout);
       size_t v = 0, c = 0, dn = 0;
       for (coa_q::Window* w : L.parts) {
-        if (w->nv) std::memcpy(w->v_out.data(), h + sl.o_v + v, w->nv);
+        if (w->nv && sl.lat) {
+          const uint32_t* words = reinterpret_cast<const uint32_t*>(h + sl.o_v) + v;
+          for (size_t i = 0; i < w->nv; i++) w->v_out[i] = (uint8_t)(words[i] & 0xffu);
+        } else if (w->nv) {
+          std::memcpy(w->v_out.data(), h + sl.o_v + v, w->nv);
+        }
         for (size_t i = 0; i < w->nd; i++) std::memcpy(&w->d_out[i * 32], h + sl.o_d + (dn + i) * 64, 32);
         if (w->nc && L.rc == COA_OK)
           L.rc = resolve_certs(*w, reinterpret_cast<const uint32_t*>(h + sl.o_c) + c);

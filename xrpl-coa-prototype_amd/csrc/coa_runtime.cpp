@@ -1591,6 +1591,33 @@ void coa_keycache_read_release(int device) {
   g.cv.notify_all();
 }
 
+size_t coa_lat_max(void) { return lat_max(); }
+
+int coa_lat_verify_device(int device, const uint8_t* d_in, size_t n, uint32_t* d_res, void* stream) {
+  const int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  if (n == 0) return COA_OK;
+  if (!d_in || !d_res) return fail(COA_EINVAL, "null argument");
+  if (check_n(n) != COA_OK) return COA_EINVAL;
+  Dev* d = dev_by_id(device);
+  if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
+  HIP_TRY(hipSetDevice(device));
+  LatArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.n = (uint32_t)n;
+  a.n_inline = 0;
+  a.in = reinterpret_cast<const uint32_t*>(d_in);
+  a.res = d_res;
+  a.tag = 1;
+  a.keys = d->ckeys.as<uint32_t>();
+  a.kflags = d->kflags.as<uint32_t>();
+  a.ktabs = d->ktabs.as<uint32_t>();
+  a.nk = d->nkeys;
+  a.comb = d->comb;
+  HIP_TRY(coa_launch_verify_lat(a, stream ? (hipStream_t)stream : d->stream));
+  return COA_OK;
+}
+
 int coa_engine_recoveries(uint64_t* contexts_rebuilt, uint64_t* shards_rerun) {
   if (contexts_rebuilt) *contexts_rebuilt = g_ctx_rebuilt.load();
   if (shards_rerun) *shards_rerun = g_shards_rerun.load();
