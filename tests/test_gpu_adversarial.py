@@ -65,6 +65,8 @@ VERIFY_PATHS = {
     "split": {},                                            # default: k_pre_halve + k_verify_main
     "split/narrow": {"COA_WCOMB": "0"},                     # [e]B from the radix-256 comb
     "split/plain-main": {"COA_MAIN_IL": "0"},               # k_verify_main without interleaved products
+    "split/eb-in-main": {"COA_SPLIT_EB": "0"},              # [e]B in k_verify_main, not k_pre_halve
+    "split/eb-in-main/narrow": {"COA_SPLIT_EB": "0", "COA_WCOMB": "0"},
     "single": {"COA_VERIFY_SPLIT": "0"},                    # k_halve + k_verify_halved
     "single/narrow": {"COA_VERIFY_SPLIT": "0", "COA_WCOMB": "0"},
     "full": {"COA_VERIFY_IMPL": "full"},                    # k_hram + k_verify_strict, no halving

@@ -2,7 +2,7 @@
 # Same-box A/B of a runtime switch on the C2 bench line: ENVS="name=VAR=value ..."
 # (a name with no assignment runs the default), alternating REPS times.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && export TMPDIR=/tmp && mkdir -p gpurun_out
-ENVS=${ENVS:-"eb=COA_SPLIT_EB=1 default"}
+ENVS=${ENVS:-"ebmain=COA_SPLIT_EB=0 default"}
 for rep in $(seq ${REPS:-3}); do
   for kv in $ENVS; do
     name=${kv%%=*}; assign=${kv#*=}; [ "$assign" = "$kv" ] && assign=""

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def stats(src, defines=()):
     with tempfile.TemporaryDirectory() as d:
-        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffunction-sections", "-I" + os.path.join(ROOT, "include"),
                "-c", os.path.abspath(src), "-save-temps", "-o", os.path.join(d, "x.o")] + list(defines)
         subprocess.run(cmd, cwd=d, check=True, capture_output=True)
         base = os.path.splitext(os.path.basename(src))[0]

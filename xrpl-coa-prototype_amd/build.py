@@ -22,7 +22,7 @@ SOURCES = ["coa_kernels.hip", "coa_halved.hip", "coa_batch.hip", "coa_committee.
            "coa_runtime.cpp", "coa_queue.cpp", "coa_queue_hip.cpp", "coa_wire.cpp"]
 HEADERS = ["coa_fe.h", "coa_sc.h", "coa_ge.h", "coa_sha512.h", "coa_smul.h", "coa_kernels.h", "coa_batch.h", "coa_halved.h",
            "coa_committee.h", "coa_msm.h", "coa_fe_wave.h", "coa_ge_rows.h", "coa_halve.h", "coa_keycache.h",
-           "coa_latency.h", "coa_queue.h", "coa_rcmp.h"]
+           "coa_latency.h", "coa_queue.h", "coa_rcmp.h", "coa_lehmer.h"]
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffunction-sections", f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include")]
 
 

@@ -7,6 +7,7 @@
 // (coa_halved.hip) and the single-signature latency kernel (coa_latency.hip).
 #pragma once
 #include "coa_fe.h"
+#include "coa_lehmer.h"
 
 namespace coa_halve {
 
@@ -142,6 +143,20 @@ COA_DEV void consider(uint32_t* c_out, uint32_t* d_out, int& best, bool& best_ne
   }
 }
 
+// The three candidates of a remainder pair (a, b) with cofactors (ma, mb),
+// mb of sign tb_neg: (b, mb), (a, ma) and (a - b, ma + mb).
+COA_DEV void consider3(uint32_t* c_out, uint32_t* d_out, int& best, bool& best_neg, const uint32_t* a,
+                       const uint32_t* b, const uint32_t* ma, const uint32_t* mb, bool tb_neg) {
+  consider(c_out, d_out, best, best_neg, b, mb, tb_neg);
+  consider(c_out, d_out, best, best_neg, a, ma, !tb_neg);
+  if ((ma[0] ^ mb[0]) & 1) {
+    uint32_t cd[8], dd[8];
+    (void)sub8(cd, a, b);
+    (void)add8(dd, ma, mb);
+    consider(c_out, d_out, best, best_neg, cd, dd, !tb_neg);
+  }
+}
+
 // Half-gcd on (8l, k) by the extended Euclidean algorithm: remainders
 // r_i == t_i * k (mod 8l) with |r_{i-1} t_i| + |r_i t_{i-1}| = 8l, so once
 // r_i < 2^128, |t_i| <= 2^127.  Quotients come from an f64 estimate of a/b
@@ -150,6 +165,11 @@ COA_DEV void consider(uint32_t* c_out, uint32_t* d_out, int& best, bool& best_ne
 // step instead.  Returns the lattice vector (c, |d|, sign d) with d odd that
 // minimises max(bits(c), bits(d)) among the last remainders and their
 // neighbours; (k, 1) if none is shorter.
+// Down to 140-bit remainders the steps are taken in Lehmer blocks
+// (coa_lehmer.h: the same remainders, ~6 full-width updates instead of ~70
+// steps); the exact steps then walk the candidates' region one remainder at
+// a time.  Remainders below 124 bits cannot beat a candidate already seen
+// (their cofactors exceed 2^129), so the walk stops there.
 COA_DEV void halve(uint32_t* c_out, uint32_t* d_out, int& cost_out, bool& neg_out, const uint32_t* k) {
   uint32_t a[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0, 0, 0, 0x80000000u};  // 8l
   uint32_t b[8], ma[8], mb[8];
@@ -167,7 +187,18 @@ COA_DEV void halve(uint32_t* c_out, uint32_t* d_out, int& cost_out, bool& neg_ou
   int lb = bitlen(b, 8);
   double af = to_f64(a), bf = to_f64(b);  // f64 images, carried across steps
   for (int guard = 0; guard < 400; guard++) {
-    if (lb <= 118) break;
+    if (lb <= 124) break;
+    if (lb > 140) {  // a Lehmer block: several exact quotients at once
+      const int nst = coa_lehmer::step(a, b, ma, mb, 140);
+      if (nst) {
+        if (nst & 1) tb_neg = !tb_neg;
+        lb = bitlen(b, 8);
+        af = to_f64(a);
+        bf = to_f64(b);
+        if (lb <= 136) consider3(c_out, d_out, best, best_neg, a, b, ma, mb, tb_neg);
+        continue;
+      }
+    }
     // quotient estimate: a correctly rounded f64 division of the f64 images
     // (relative error ~2^-50), so for q < 2^31 floor() is off by at most one
     // and the fix-ups below correct it.  NOT v_rcp_f64: its approximation
@@ -226,16 +257,7 @@ COA_DEV void halve(uint32_t* c_out, uint32_t* d_out, int& cost_out, bool& neg_ou
     lb = bitlen(b, 8);
     af = bf;
     bf = to_f64(b);
-    if (lb <= 136) {
-      consider(c_out, d_out, best, best_neg, b, mb, tb_neg);
-      consider(c_out, d_out, best, best_neg, a, ma, !tb_neg);
-      if ((ma[0] ^ mb[0]) & 1) {
-        uint32_t cd[8], dd[8];
-        (void)sub8(cd, a, b);
-        (void)add8(dd, ma, mb);
-        consider(c_out, d_out, best, best_neg, cd, dd, !tb_neg);
-      }
-    }
+    if (lb <= 136) consider3(c_out, d_out, best, best_neg, a, b, ma, mb, tb_neg);
   }
   cost_out = best;
   neg_out = best_neg;

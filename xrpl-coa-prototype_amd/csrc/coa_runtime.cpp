@@ -374,7 +374,10 @@ bool split_impl() { return !env_is("COA_VERIFY_SPLIT", "0"); }
 
 // Split path in chunks of at most COA_SPLIT_CHUNK items (one slab each).
 // k from d_k, or hashed in k_pre_halve from d_msgs (msg_len bytes per item)
-// when d_k is null.
+// when d_k is null.  [e]B is summed by k_pre_halve's hash/halving role after
+// the halving (that role ends early beside the two decompression roles:
+// the 13 comb additions fill its idle tail instead of k_verify_main's lone
+// wave); COA_SPLIT_EB=0 leaves it to k_verify_main (A/B, parity tests).
 int enqueue_split(Dev& d, const uint8_t* d_msgs, size_t msg_len, const uint32_t* d_k, const uint8_t* d_pks,
                   const uint8_t* d_sigs, size_t n, uint8_t* d_verdicts, const Workspace& w, hipStream_t s) {
   for (size_t lo = 0; lo < n; lo += COA_SPLIT_CHUNK) {
@@ -382,7 +385,7 @@ int enqueue_split(Dev& d, const uint8_t* d_msgs, size_t msg_len, const uint32_t*
     HIP_TRY(coa_launch_verify_split(d_pks + lo * 32, d_sigs + lo * 64, d_k ? nullptr : d_msgs + lo * msg_len,
                                     (uint32_t)msg_len, d_k ? d_k + lo * 8 : nullptr, cnt, w.rec + lo * 32,
                                     w.flags + 2 * lo, d_verdicts + lo, w.scratch,
-                                    env_is("COA_SPLIT_EB", "1") ? w.ebp : nullptr, d.comb, wcomb_of(d), s));
+                                    env_is("COA_SPLIT_EB", "0") ? nullptr : w.ebp, d.comb, wcomb_of(d), s));
   }
   return COA_OK;
 }
