@@ -1,7 +1,8 @@
 """GPU: the single-signature latency route (coa_latency.hip k_verify_lat) --
 Signature::verify one message at a time, as Header::verify / Vote::verify call
 it (primary/src/messages.rs:64-66,139-141).  Calls of at most COA_LAT_MAX
-(default 64) triples with 32-byte messages take it; its verdicts must equal
+(default 2,048) triples with 32-byte messages take it, on one idle context
+(such calls are not sharded over GPUs); its verdicts must equal
 the oracle's (dalek verify_strict) on the golden vectors and on adversarial
 mixes, with the keys registered in the committee cache (comb path) and not
 (halved-scalar row chains)."""

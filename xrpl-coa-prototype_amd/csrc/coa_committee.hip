@@ -363,49 +363,69 @@ __global__ void __launch_bounds__(256) k_key_tables(const uint32_t* __restrict__
   store_niels(out, M);
 }
 
-// Throughput variant: a grid of two waves per SIMD; lane L takes the jobs
-// L, L + lanes, L + 2 lanes, ... (at most jpl of them).  Phase A computes
-// every job's P and parks it with the running product of the Z's in a
-// lane-major scratch slab; ONE field inversion serves all of a lane's jobs
-// (Montgomery's trick), then phase C compares each affine P with its R
-// encoding.  Per vote: ~265/jpl field operations of inversion instead of R's
-// ~277-operation decompression, and no wave-count tail.
-__global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a, uint32_t* __restrict__ pscr, uint32_t jpl) {
-  if (blockIdx.x < a.hdr_blocks) {  // header digest role, one lane per certificate
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= a.nc) return;
-    const uint64_t o0 = a.hdr_off[c], o1 = a.hdr_off[c + 1];
-    uint64_t st[8];
-    coa_sha::hash_mem(st, a.hdr_data + o0, o1 - o0);
-    uint32_t h[16], id[8];
-    coa_sha::state_to_le_words(h, st);
-    load8(id, a.ids + (uint64_t)c * 8);
-    bool same = true;
-#pragma unroll
-    for (int i = 0; i < 8; i++) same = same && h[i] == id[i];
-    if (!same) atomicOr(a.status + c, COA_CST_BAD_HEADER_ID);
-    return;
-  }
-  const uint64_t lanes = (uint64_t)(gridDim.x - a.hdr_blocks) * blockDim.x;
-  const uint64_t lane = (uint64_t)(blockIdx.x - a.hdr_blocks) * blockDim.x + threadIdx.x;
+// Throughput variant: a persistent grid of two waves per SIMD.  Each wave
+// takes chunks of 64 consecutive work items from a global counter until none
+// is left: first the header-digest chunks (64 certificates, one per lane:
+// SHA-512 of the Header::digest bytes), then the signature chunks (64 jobs,
+// one per lane).  So every SIMD stays busy to within one chunk of the end:
+// a static split leaves some SIMDs with one chunk more than others (5 vs 6
+// at C3, ~15 %) and the header waves displaced signature waves into a tail.
+// Phase A computes each job's P and parks it with the running product of the
+// Z's in a lane-major scratch slab; ONE field inversion serves all of a
+// lane's jobs (Montgomery's trick), then phase C compares each affine P with
+// its R encoding.  Per vote: ~265/jobs field operations of inversion instead
+// of R's ~277-operation decompression.  pscr[0] is the chunk counter (zeroed
+// by the launcher); the slab holds jcap jobs per lane.
+__global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a, uint32_t* __restrict__ pscr, uint32_t jcap) {
+  const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t sub = threadIdx.x & 63;
+  uint32_t* ctr = pscr;
+  uint32_t* slab = pscr + 64;
+  const uint32_t hdr_chunks = (a.nc + 63) / 64;
   const uint64_t jobs = (uint64_t)a.nc + a.nv;
-  if (lane >= jobs) return;
-  const int nj = (int)min<uint64_t>(jpl, (jobs - lane + lanes - 1) / lanes);  // this lane's jobs
-  fe zp;  // running prefix product of the Z's
+  const uint32_t chunks = hdr_chunks + (uint32_t)((jobs + 63) / 64);
+  int nj = 0;  // this wave's signature chunks (the same for all its lanes)
+  fe zp;       // running prefix product of the Z's
 #pragma unroll 1
-  for (int j = 0; j < nj; j++) {
-    const uint64_t job = lane + (uint64_t)j * lanes;
+  for (;;) {
+    if (nj >= (int)jcap) break;  // slab full: the other waves take the rest
+    uint32_t chunk = 0;
+    if (sub == 0) chunk = atomicAdd(ctr, 1u);
+    chunk = __builtin_amdgcn_readfirstlane(__shfl(chunk, 0));
+    if (chunk >= chunks) break;
+    if (chunk < hdr_chunks) {  // header digest of certificate chunk * 64 + sub
+      const uint32_t c = chunk * 64 + sub;
+      if (c < a.nc) {
+        const uint64_t o0 = a.hdr_off[c], o1 = a.hdr_off[c + 1];
+        uint64_t st[8];
+        coa_sha::hash_mem(st, a.hdr_data + o0, o1 - o0);
+        uint32_t h[16], id[8];
+        coa_sha::state_to_le_words(h, st);
+        load8(id, a.ids + (uint64_t)c * 8);
+        bool same = true;
+#pragma unroll
+        for (int i = 0; i < 8; i++) same = same && h[i] == id[i];
+        if (!same) atomicOr(a.status + c, COA_CST_BAD_HEADER_ID);
+      }
+      continue;
+    }
+    const uint64_t job = (uint64_t)(chunk - hdr_chunks) * 64 + sub;
     ge_p3 P;
     uint32_t pre = PRE_NONE, cert = 0;
-    job_comb(a, (uint32_t)job, P, pre, cert);
-    if (j == 0) zp = P.Z;
+    if (job < jobs) job_comb(a, (uint32_t)job, P, pre, cert);
+    else ge_p3_identity(P);
+    if (nj == 0) zp = P.Z;
     else fe_mul(zp, zp, P.Z);
-    pscr_put(pscr, lanes, lane, j, 0, P.X);
-    pscr_put(pscr, lanes, lane, j, 2, P.Y);
-    pscr_put(pscr, lanes, lane, j, 4, P.Z);
-    pscr_put(pscr, lanes, lane, j, 6, zp);
-    reinterpret_cast<uint4*>(pscr)[((uint64_t)j * PSCR_ROWS + 8) * lanes + lane] = make_uint4(pre, cert, 0, 0);
+    pscr_put(slab, lanes, lane, nj, 0, P.X);
+    pscr_put(slab, lanes, lane, nj, 2, P.Y);
+    pscr_put(slab, lanes, lane, nj, 4, P.Z);
+    pscr_put(slab, lanes, lane, nj, 6, zp);
+    reinterpret_cast<uint4*>(slab)[((uint64_t)nj * PSCR_ROWS + 8) * lanes + lane] =
+        make_uint4(pre, cert, (uint32_t)job, 0);
+    nj++;
   }
+  if (nj == 0) return;
   fe inv;
   fe_invert(inv, zp);
 #pragma unroll 1
@@ -413,20 +433,19 @@ __global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a, uint32_t* __
     fe zinv, x, y, X, Y;
     if (j > 0) {
       fe Z, zprev;
-      pscr_get(zprev, pscr, lanes, lane, j - 1, 6);
-      pscr_get(Z, pscr, lanes, lane, j, 4);
+      pscr_get(zprev, slab, lanes, lane, j - 1, 6);
+      pscr_get(Z, slab, lanes, lane, j, 4);
       fe_mul(zinv, inv, zprev);
       fe_mul(inv, inv, Z);
     } else {
       zinv = inv;
     }
-    pscr_get(X, pscr, lanes, lane, j, 0);
-    pscr_get(Y, pscr, lanes, lane, j, 2);
-    const uint4 m = reinterpret_cast<const uint4*>(pscr)[((uint64_t)j * PSCR_ROWS + 8) * lanes + lane];
+    pscr_get(X, slab, lanes, lane, j, 0);
+    pscr_get(Y, slab, lanes, lane, j, 2);
+    const uint4 m = reinterpret_cast<const uint4*>(slab)[((uint64_t)j * PSCR_ROWS + 8) * lanes + lane];
     fe_mul(x, X, zinv);
     fe_mul(y, Y, zinv);
-    const uint64_t job = lane + (uint64_t)j * lanes;
-    const uint32_t bits = job_verdict(a, (uint32_t)job, m.x, x, y);
+    const uint32_t bits = job_verdict(a, m.z, m.x, x, y);
     if (bits) atomicOr(a.status + m.y, bits);
   }
 }
@@ -734,10 +753,16 @@ hipError_t coa_launch_cert_verify_inl(const CertInl& ci, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Signature chunks one wave of the throughput grid may take (its slab
+// capacity): the even share plus slack for the waves that run ahead.
+static uint32_t cert_tp_jcap(uint64_t jobs, uint64_t lanes) {
+  const uint64_t waves = lanes / 64, chunks = (jobs + 63) / 64;
+  return (uint32_t)((chunks + waves - 1) / waves + 2);
+}
+
 size_t coa_cert_scratch_bytes(uint64_t jobs) {
   const uint64_t lanes = cert_tp_lanes(jobs ? jobs : 1);
-  const uint64_t jpl = (jobs + lanes - 1) / lanes;
-  return (size_t)(lanes * (jpl ? jpl : 1) * 9 * 16 + 256);
+  return (size_t)(lanes * cert_tp_jcap(jobs, lanes) * PSCR_ROWS * 16 + 256 + 256);
 }
 
 hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr, hipStream_t s) {
@@ -750,8 +775,10 @@ hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr,
     return hipGetLastError();
   }
   const uint64_t lanes = cert_tp_lanes(jobs);
-  const uint32_t jpl = (uint32_t)((jobs + lanes - 1) / lanes);
-  hipLaunchKernelGGL(k_cert_verify, dim3((uint32_t)(a.hdr_blocks + lanes / 256)), dim3(256), 0, s, a, pscr, jpl);
+  // the chunk counter (pscr[0]) starts at zero; the slab follows it
+  hipError_t e = hipMemsetAsync(pscr, 0, 4, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_cert_verify, dim3((uint32_t)(lanes / 256)), dim3(256), 0, s, a, pscr, cert_tp_jcap(jobs, lanes));
   return hipGetLastError();
 }
 

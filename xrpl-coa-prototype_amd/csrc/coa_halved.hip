@@ -436,6 +436,10 @@ __global__ void __launch_bounds__(256, WAVES) k_pre_halve(const uint8_t* __restr
   load8_u4(sw, sigs + (uint64_t)i * 64 + 32);
   halve_rec(k, sw, i, rec, e);
   if (!ebp) return;  // [e]B left to k_verify_main
+  // the 13 comb additions are issue-bound, not a latency chain: back to the
+  // default priority, so the decompression waves keep first call on issue
+  // (COA_PRE_PRIO=3 keeps the raised priority through them, A/B)
+  if ((prio & 9) == 1) __builtin_amdgcn_s_setprio(0);
   ge_p3 P;
   ge_p3_identity(P);
   if (wcomb) {
@@ -764,7 +768,11 @@ hipError_t coa_launch_verify_split(const uint8_t* pks, const uint8_t* sigs, cons
   // A library compiled with -DCOA_PRE_DIAG_BUILD also reads COA_PRE_DIAG=2 / 4:
   // skip the decompression / hash roles (role timing only, tools/pre_roles.sh;
   // verdicts are then meaningless, so release builds cannot reach it).
-  static const int prio = (getenv("COA_PRE_PRIO") && atoi(getenv("COA_PRE_PRIO")) == 0 ? 0 : 1)
+  // COA_PRE_PRIO=3: the raised priority also through the [e]B additions (bit
+  // 8; A/B).  Bits 2 and 4 are the diagnostics below.
+  static const int prio = (!getenv("COA_PRE_PRIO") ? 1
+                           : atoi(getenv("COA_PRE_PRIO")) == 0 ? 0
+                           : atoi(getenv("COA_PRE_PRIO")) == 3 ? (1 | 8) : 1)
 #ifdef COA_PRE_DIAG_BUILD
                           | (getenv("COA_PRE_DIAG") ? atoi(getenv("COA_PRE_DIAG")) & 6 : 0)
 #endif
