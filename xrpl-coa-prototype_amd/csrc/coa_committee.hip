@@ -363,13 +363,14 @@ __global__ void __launch_bounds__(256) k_key_tables(const uint32_t* __restrict__
   store_niels(out, M);
 }
 
-// Throughput variant: a persistent grid of two waves per SIMD.  Each wave
-// takes chunks of 64 consecutive work items from a global counter until none
-// is left: first the header-digest chunks (64 certificates, one per lane:
-// SHA-512 of the Header::digest bytes), then the signature chunks (64 jobs,
-// one per lane).  So every SIMD stays busy to within one chunk of the end:
-// a static split leaves some SIMDs with one chunk more than others (5 vs 6
-// at C3, ~15 %) and the header waves displaced signature waves into a tail.
+// Throughput variant.  The leading blocks hash the header digests, one lane
+// per certificate (SHA-512 of the Header::digest bytes, ~27 blocks at C3),
+// beside the signature waves.  The signature waves are a persistent grid of
+// two waves per SIMD that take chunks of 64 consecutive jobs (one per lane)
+// from a global counter until none is left, so every SIMD stays busy to
+// within one chunk of the end: a static split leaves some SIMDs with one
+// chunk more than others (5 vs 6 at C3, ~15 %), and the signature waves the
+// header waves displace start late and simply take fewer chunks.
 // Phase A computes each job's P and parks it with the running product of the
 // Z's in a lane-major scratch slab; ONE field inversion serves all of a
 // lane's jobs (Montgomery's trick), then phase C compares each affine P with
@@ -377,15 +378,29 @@ __global__ void __launch_bounds__(256) k_key_tables(const uint32_t* __restrict__
 // of R's ~277-operation decompression.  pscr[0] is the chunk counter (zeroed
 // by the launcher); the slab holds jcap jobs per lane.
 __global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a, uint32_t* __restrict__ pscr, uint32_t jcap) {
-  const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x < a.hdr_blocks) {  // header digest role, one lane per certificate
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.nc) return;
+    const uint64_t o0 = a.hdr_off[c], o1 = a.hdr_off[c + 1];
+    uint64_t st[8];
+    coa_sha::hash_mem(st, a.hdr_data + o0, o1 - o0);
+    uint32_t h[16], id[8];
+    coa_sha::state_to_le_words(h, st);
+    load8(id, a.ids + (uint64_t)c * 8);
+    bool same = true;
+#pragma unroll
+    for (int i = 0; i < 8; i++) same = same && h[i] == id[i];
+    if (!same) atomicOr(a.status + c, COA_CST_BAD_HEADER_ID);
+    return;
+  }
+  const uint64_t lanes = (uint64_t)(gridDim.x - a.hdr_blocks) * blockDim.x;
+  const uint64_t lane = (uint64_t)(blockIdx.x - a.hdr_blocks) * blockDim.x + threadIdx.x;
   const uint32_t sub = threadIdx.x & 63;
   uint32_t* ctr = pscr;
   uint32_t* slab = pscr + 64;
-  const uint32_t hdr_chunks = (a.nc + 63) / 64;
   const uint64_t jobs = (uint64_t)a.nc + a.nv;
-  const uint32_t chunks = hdr_chunks + (uint32_t)((jobs + 63) / 64);
-  int nj = 0;  // this wave's signature chunks (the same for all its lanes)
+  const uint32_t chunks = (uint32_t)((jobs + 63) / 64);
+  int nj = 0;  // this wave's chunks (the same for all its lanes)
   fe zp;       // running prefix product of the Z's
 #pragma unroll 1
   for (;;) {
@@ -394,23 +409,7 @@ __global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a, uint32_t* __
     if (sub == 0) chunk = atomicAdd(ctr, 1u);
     chunk = __builtin_amdgcn_readfirstlane(__shfl(chunk, 0));
     if (chunk >= chunks) break;
-    if (chunk < hdr_chunks) {  // header digest of certificate chunk * 64 + sub
-      const uint32_t c = chunk * 64 + sub;
-      if (c < a.nc) {
-        const uint64_t o0 = a.hdr_off[c], o1 = a.hdr_off[c + 1];
-        uint64_t st[8];
-        coa_sha::hash_mem(st, a.hdr_data + o0, o1 - o0);
-        uint32_t h[16], id[8];
-        coa_sha::state_to_le_words(h, st);
-        load8(id, a.ids + (uint64_t)c * 8);
-        bool same = true;
-#pragma unroll
-        for (int i = 0; i < 8; i++) same = same && h[i] == id[i];
-        if (!same) atomicOr(a.status + c, COA_CST_BAD_HEADER_ID);
-      }
-      continue;
-    }
-    const uint64_t job = (uint64_t)(chunk - hdr_chunks) * 64 + sub;
+    const uint64_t job = (uint64_t)chunk * 64 + sub;
     ge_p3 P;
     uint32_t pre = PRE_NONE, cert = 0;
     if (job < jobs) job_comb(a, (uint32_t)job, P, pre, cert);
@@ -778,7 +777,8 @@ hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr,
   // the chunk counter (pscr[0]) starts at zero; the slab follows it
   hipError_t e = hipMemsetAsync(pscr, 0, 4, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_cert_verify, dim3((uint32_t)(lanes / 256)), dim3(256), 0, s, a, pscr, cert_tp_jcap(jobs, lanes));
+  hipLaunchKernelGGL(k_cert_verify, dim3((uint32_t)(a.hdr_blocks + lanes / 256)), dim3(256), 0, s, a, pscr,
+                     cert_tp_jcap(jobs, lanes));
   return hipGetLastError();
 }
 
