@@ -50,6 +50,9 @@ struct CertArgs {
   const uint32_t* comb;         // B comb (coa_halved.h)
   const uint32_t* wcomb;        // wide B comb (coa_smul.h) or null
   uint32_t* status;             // [nc], zeroed by the caller
+  // throughput variant: [nc][8] Certificate::digest of each certificate,
+  // written by a prologue kernel (set by the launcher; null = per vote)
+  const uint32_t* cdig = nullptr;
   // latency variant only (optional): the last block publishes (tag << 8) |
   // status into host_res[c] (page-locked) and re-zeroes status and done_ctr
   uint32_t* host_res = nullptr;

@@ -176,7 +176,9 @@ COA_DEV void job_comb(const CertArgs& a, uint32_t job, ge_p3& P, uint32_t& pre, 
   }
   uint64_t st[8];
   uint32_t h[16];
-  if (!hdr) {  // Certificate::digest = SHA-512(id || round u64 LE || origin)[..32]
+  if (!hdr && a.cdig) {  // Certificate::digest from the prologue kernel
+    load8(msg, a.cdig + (uint64_t)c * 8);
+  } else if (!hdr) {  // Certificate::digest = SHA-512(id || round u64 LE || origin)[..32]
     uint32_t in[18];
     const uint64_t rd = a.rounds[c];
 #pragma unroll
@@ -363,6 +365,28 @@ __global__ void __launch_bounds__(256) k_key_tables(const uint32_t* __restrict__
   store_niels(out, M);
 }
 
+// Prologue of the throughput variant: Certificate::digest = SHA-512(id ||
+// round u64 LE || origin)[..32] once per certificate (primary/src/
+// messages.rs:226-234), instead of once per vote in the signature jobs (a
+// C3 certificate has 67 votes: one SHA-512 block each saved).
+__global__ void __launch_bounds__(256) k_cert_digests(CertArgs a, uint32_t* __restrict__ out) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.nc) return;
+  uint32_t in[18];
+  load8(in, a.ids + (uint64_t)c * 8);
+  const uint64_t rd = a.rounds[c];
+  in[8] = (uint32_t)rd;
+  in[9] = (uint32_t)(rd >> 32);
+  load8(in + 10, a.origins + (uint64_t)c * 8);
+  uint64_t st[8];
+  coa_sha::hash_words<18>(st, in);
+  uint32_t h[16];
+  coa_sha::state_to_le_words(h, st);
+  uint4* o = reinterpret_cast<uint4*>(out + (uint64_t)c * 8);
+  o[0] = make_uint4(h[0], h[1], h[2], h[3]);
+  o[1] = make_uint4(h[4], h[5], h[6], h[7]);
+}
+
 // Throughput variant.  The leading blocks hash the header digests, one lane
 // per certificate (SHA-512 of the Header::digest bytes, ~27 blocks at C3),
 // beside the signature waves.  The signature waves are a persistent grid of
@@ -377,7 +401,8 @@ __global__ void __launch_bounds__(256) k_key_tables(const uint32_t* __restrict__
 // its R encoding.  Per vote: ~265/jobs field operations of inversion instead
 // of R's ~277-operation decompression.  pscr[0] is the chunk counter (zeroed
 // by the launcher); the slab holds jcap jobs per lane.
-__global__ void __launch_bounds__(256, 2) k_cert_verify(CertArgs a, uint32_t* __restrict__ pscr, uint32_t jcap) {
+template <int WAVES>
+__global__ void __launch_bounds__(256, WAVES) k_cert_verify(CertArgs a, uint32_t* __restrict__ pscr, uint32_t jcap) {
   if (blockIdx.x < a.hdr_blocks) {  // header digest role, one lane per certificate
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.nc) return;
@@ -684,8 +709,14 @@ __global__ void __launch_bounds__(192) k_cert_verify_lat_inl(CertInl ci) {
 // Grid of the throughput kernel: two waves per SIMD (256 CUs x 4 SIMDs x 2
 // x 64 lanes), or one lane per job when there are fewer jobs.
 // COA_CERT_LANES_TOTAL overrides (A/B runs).
+// COA_CERT_WAVES=3: three waves per SIMD (the 168-VGPR instance, A/B).
+static int cert_tp_waves() {
+  const char* e = getenv("COA_CERT_WAVES");
+  return (e && atoi(e) == 3) ? 3 : 2;
+}
+
 uint64_t cert_tp_lanes(uint64_t jobs) {
-  uint64_t target = 256ull * 4 * 2 * 64;
+  uint64_t target = 256ull * 4 * (uint64_t)cert_tp_waves() * 64;
   if (const char* e = getenv("COA_CERT_LANES_TOTAL")) target = strtoull(e, nullptr, 10);
   if (target < 256) target = 256;
   const uint64_t lanes = jobs < target ? jobs : target;
@@ -759,9 +790,15 @@ static uint32_t cert_tp_jcap(uint64_t jobs, uint64_t lanes) {
   return (uint32_t)((chunks + waves - 1) / waves + 2);
 }
 
+// Throughput scratch: [0, 256) chunk counter | slab (lanes x jcap jobs) |
+// Certificate::digest per certificate (at most one per job).
+static size_t cert_slab_bytes(uint64_t jobs, uint64_t lanes) {
+  return (size_t)(lanes * cert_tp_jcap(jobs, lanes) * PSCR_ROWS * 16);
+}
+
 size_t coa_cert_scratch_bytes(uint64_t jobs) {
   const uint64_t lanes = cert_tp_lanes(jobs ? jobs : 1);
-  return (size_t)(lanes * cert_tp_jcap(jobs, lanes) * PSCR_ROWS * 16 + 256 + 256);
+  return 256 + cert_slab_bytes(jobs, lanes) + (size_t)(jobs ? jobs : 1) * 32 + 256;
 }
 
 hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr, hipStream_t s) {
@@ -774,11 +811,26 @@ hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr,
     return hipGetLastError();
   }
   const uint64_t lanes = cert_tp_lanes(jobs);
-  // the chunk counter (pscr[0]) starts at zero; the slab follows it
+  // the chunk counter (pscr[0]) starts at zero; the slab follows it, then the
+  // certificates' digests (prologue kernel)
   hipError_t e = hipMemsetAsync(pscr, 0, 4, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_cert_verify, dim3((uint32_t)(a.hdr_blocks + lanes / 256)), dim3(256), 0, s, a, pscr,
-                     cert_tp_jcap(jobs, lanes));
+  // the prologue pays for its launch when certificates carry many votes (C3:
+  // 67 votes, +2-5 %); with few (C1: 3 votes) the digest stays per vote.
+  // COA_CERT_DIGEST_PER_VOTE=1 forces per vote (A/B).
+  if (a.nv >= 8ull * a.nc && !getenv("COA_CERT_DIGEST_PER_VOTE")) {
+    uint32_t* cdig = pscr + 64 + cert_slab_bytes(jobs, lanes) / 4;
+    hipLaunchKernelGGL(k_cert_digests, dim3((a.nc + 255) / 256), dim3(256), 0, s, a, cdig);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    a.cdig = cdig;
+  }
+  if (cert_tp_waves() == 3)
+    hipLaunchKernelGGL(k_cert_verify<3>, dim3((uint32_t)(a.hdr_blocks + lanes / 256)), dim3(256), 0, s, a, pscr,
+                       cert_tp_jcap(jobs, lanes));
+  else
+    hipLaunchKernelGGL(k_cert_verify<2>, dim3((uint32_t)(a.hdr_blocks + lanes / 256)), dim3(256), 0, s, a, pscr,
+                       cert_tp_jcap(jobs, lanes));
   return hipGetLastError();
 }
 
