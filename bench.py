@@ -40,6 +40,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "xrpl-coa-prototype_amd")
 sys.path.insert(0, PKG)
 
+# HIP gives a process GPU_MAX_HW_QUEUES hardware queues (4 by default) and
+# maps its streams onto them: the aggregation queue's concurrent windows
+# (secondary c4_stream / queue_round_mix) run side by side only with more of
+# them.  Read once, at HIP's initialisation, so it is set before torch or the
+# engine touch the GPU (a node process does the same).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 # dalek algorithm field operations per verify_strict (fe_mul + fe_sq), measured
 # by oracle/_build/libcoa_oracle_count.so over the golden valid vectors.
 FIELD_OPS_PER_VERIFY = 2967
@@ -963,6 +970,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # COA_BENCH_ONE_DEVICE=1: every rank on device 0 (rehearses the N-rank
+    # launch, barrier and MAX-over-ranks timing on a one-GPU box; the ranks
+    # then share the GPU, so the value is not a scaling figure)
+    if os.environ.get("COA_BENCH_ONE_DEVICE") == "1":
+        local = 0
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
     torch.cuda.set_device(local)  # one process per GPU

@@ -121,7 +121,7 @@ def test_queue_certificates_and_digests_gpu(engine):
 @pytest.mark.gpu
 def test_queue_pipelined_windows_gpu(engine):
     """Many small windows in a row (max_batch 256) from four producers mixing
-    every kind: windows overlap on the two device slots (max_in_flight 2),
+    every kind: windows overlap on the device slots (max_in_flight 2..4),
     every answer equals its expectation -- valid/corrupted signatures,
     certificates including ones that need the exact host re-decision (a vote
     key outside the registered committee, a corrupted vote), digests -- and
@@ -184,5 +184,5 @@ def test_queue_pipelined_windows_gpu(engine):
                 assert got == exp, (kind, got, exp)
         m = q.metrics()
     assert m["requests"] == len(results) and m["signatures"] == n
-    assert m["windows"] > 4 and m["max_in_flight"] == 2
+    assert m["windows"] > 4 and 2 <= m["max_in_flight"] <= 4  # pipelined over the slots (4 per GPU)
     assert 0 < m["wait_us_p50"] <= m["wait_us_p99"] <= m["wait_us_max"] * 1.1
