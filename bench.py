@@ -59,7 +59,7 @@ VALU_ISSUE_CYCLES = 2  # one full-rate wave64 VALU instruction per 2 cycles per 
 PEAK_INT32_TOPS = SIMDS * 32 * CLOCK_HZ / 1e12
 C2_N = 65536
 # counter profile of the C2 verify call (tools/pmc_verify.py), tied to a build
-PMC_JSON = "r02_verify_pmc.json"
+PMC_JSON = "r03_verify_pmc.json"
 
 
 def parse():
@@ -805,8 +805,8 @@ def certificate_config(n_certs, latency_samples, cpu_threads, dev, stream, commi
 
 # Sources that make up the C2 verify kernels (k_pre_halve, k_verify_main) and
 # the build flags: a counter profile stays valid while these are unchanged.
-VERIFY_KERNEL_SOURCES = ("coa_halved.hip", "coa_halved.h", "coa_halve.h", "coa_fe.h", "coa_ge.h", "coa_sc.h",
-                         "coa_sha512.h", "coa_smul.h", "coa_kernels.h")
+VERIFY_KERNEL_SOURCES = ("coa_halved.hip", "coa_halved.h", "coa_halve.h", "coa_lehmer.h", "coa_fe.h", "coa_ge.h",
+                         "coa_sc.h", "coa_sha512.h", "coa_smul.h", "coa_kernels.h", "coa_runtime.cpp")
 
 
 def verify_kernel_src_sha256():

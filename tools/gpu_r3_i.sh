@@ -10,3 +10,10 @@ for r in 1 2 3; do for hq in 4 8; do
 done; done
 COA_BENCH_ONE_DEVICE=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 > gpurun_out/bench_2rank.json 2> gpurun_out/bench_2rank.err || { tail -20 gpurun_out/bench_2rank.err; exit 1; }
 cat gpurun_out/bench_2rank.json | cut -c1-400
+# k_pre_halve role timing on this build (diagnostic library: build/diag)
+for diag in 0 4 2; do
+  COA_VERIFY_LIB=$PWD/build/diag/libcoa_verify.so COA_PRE_DIAG=$diag timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/roles_$diag -o run --output-format csv \
+    -- python3 tools/inflight_probe.py 65536 20 > gpurun_out/roles_$diag.jsonl 2>&1 || exit 1
+  f=$(find gpurun_out/roles_$diag -name "*kernel_stats.csv" | head -1)
+  echo "diag $diag: $(grep -h 'k_pre_halve' $f | cut -d, -f1-4 | cut -c1-40,200-400)"
+done
