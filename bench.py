@@ -806,7 +806,7 @@ def certificate_config(n_certs, latency_samples, cpu_threads, dev, stream, commi
 # Sources that make up the C2 verify kernels (k_pre_halve, k_verify_main) and
 # the build flags: a counter profile stays valid while these are unchanged.
 VERIFY_KERNEL_SOURCES = ("coa_halved.hip", "coa_halved.h", "coa_halve.h", "coa_lehmer.h", "coa_fe.h", "coa_ge.h",
-                         "coa_sc.h", "coa_sha512.h", "coa_smul.h", "coa_kernels.h", "coa_runtime.cpp")
+                         "coa_sc.h", "coa_sha512.h", "coa_smul.h", "coa_kernels.h")
 
 
 def verify_kernel_src_sha256():
