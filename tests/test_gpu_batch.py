@@ -26,7 +26,15 @@ def _pack(groups):
             np.frombuffer(zs, np.uint8).reshape(n, 16).copy())
 
 
-def test_golden_batch_vectors(engine):
+@pytest.fixture(params=["prefilter", "exact"])
+def route(request, monkeypatch):
+    """Small calls through the latency prefilter (default) or straight to the
+    exact batch kernels (COA_BATCH_LAT=0)."""
+    monkeypatch.setenv("COA_BATCH_LAT", "1" if request.param == "prefilter" else "0")
+    return request.param
+
+
+def test_golden_batch_vectors(engine, route):
     gs = []
     for g in load_golden("batch_vectors.json"):
         gs.append({"msg": bytes.fromhex(g["msg"]), "pks": [bytes.fromhex(p) for p in g["pks"]],
@@ -41,11 +49,8 @@ def test_golden_batch_vectors(engine):
     assert (got2 == got).all()
 
 
-def test_torsion_batches_exact_with_given_z(engine):
-    """Mixed-order A with a torsion-matched R passes verify_strict; in a batch
-    the torsion part is multiplied by z_i h_i mod l, so the verdict depends
-    on z -- both outcomes must match the oracle for the same z."""
-    rng = random.Random(5)
+def _torsion_groups(seed=5):
+    rng = random.Random(seed)
     T8 = None
     for T in o.torsion_points():
         if not o.is_identity(o.pdbl(o.pdbl(T))):
@@ -78,10 +83,67 @@ def test_torsion_batches_exact_with_given_z(engine):
         zs = [rng.getrandbits(128) for _ in range(3)]
         exp = o.verify_batch(m, pks, sigs, zs)
         groups.append({"msg": m, "pks": pks, "sigs": sigs, "zs": zs, "expect": exp})
-    assert any(g["expect"] for g in groups)
+    assert any(g["expect"] for g in groups) and not all(g["expect"] for g in groups)
+    return groups
+
+
+def test_torsion_batches_exact_with_given_z(engine, route):
+    """Mixed-order A with a torsion-matched R passes verify_strict; in a batch
+    the torsion part is multiplied by z_i h_i mod l, so the verdict depends
+    on z -- both outcomes must match the oracle for the same z.  Through the
+    prefilter the mixed-order key fails [l]A == O, so these groups are resolved
+    by the exact kernels; a prefilter that accepted them would answer Ok for
+    the groups the oracle rejects."""
+    groups = _torsion_groups()
     msgs, pks, sigs, offs, zs = _pack(groups)
     got = engine.verify_batch_groups(msgs, pks, sigs, offs, zs=zs)
     assert [v == 0 for v in got] == [g["expect"] for g in groups]
+
+
+def test_torsion_batches_with_registered_keys(engine, monkeypatch):
+    """The same groups with every key registered: the prefilter then takes
+    [l]A == O from the key cache's flag (COA_KEY_TORSION_FREE) instead of
+    computing it, and must still send the mixed-order groups to the exact
+    kernels."""
+    monkeypatch.setenv("COA_BATCH_LAT", "1")
+    groups = _torsion_groups(seed=6)
+    msgs, pks, sigs, offs, zs = _pack(groups)
+    try:
+        engine.committee_register(pks)
+        got = engine.verify_batch_groups(msgs, pks, sigs, offs, zs=zs)
+    finally:
+        engine.committee_register(np.zeros((0, 32), np.uint8))
+    assert [v == 0 for v in got] == [g["expect"] for g in groups]
+
+
+def test_prefilter_many_groups_agree_with_exact(engine, monkeypatch):
+    """C1-like call (300 certificates x 3 votes, under the prefilter's 2,048
+    signatures) with corrupt votes, a non-canonical s, an undecodable R and
+    an empty group: the prefilter's verdicts equal the exact kernels'."""
+    from workloads import key_seeds
+
+    ng, per = 300, 3
+    seeds = key_seeds(ng * per)
+    msgs = np.frombuffer(b"".join(o.sha512(b"pf" + struct.pack("<Q", g))[:32] for g in range(ng)),
+                         np.uint8).reshape(ng, 32).copy()
+    pks, sigs = engine.sign_many(seeds, np.repeat(msgs, per, axis=0))
+    sizes = [per] * ng
+    sizes[7] = 0  # an empty group (Ok): drop its votes
+    keep = np.ones(ng * per, bool)
+    keep[7 * per:8 * per] = False
+    pks, sigs = pks[keep].copy(), sigs[keep].copy()
+    offs = np.zeros(ng + 1, np.uint64)
+    offs[1:] = np.cumsum(sizes)
+    sigs[int(offs[3]) + 1, 40] ^= 8
+    sigs[int(offs[100]), 32:] = np.frombuffer((o.L + 2).to_bytes(32, "little"), np.uint8)
+    sigs[int(offs[200]) + 2, :32] = np.frombuffer(bytes.fromhex("02" + "00" * 31), np.uint8)
+    pks[int(offs[250]) + 1, 5] ^= 1
+    got = {}
+    for r in ("1", "0"):
+        monkeypatch.setenv("COA_BATCH_LAT", r)
+        got[r] = engine.verify_batch_groups(msgs, pks, sigs, offs, rng_seed=31)
+    assert list(got["1"]) == list(got["0"])
+    assert sorted(np.nonzero(got["1"])[0].tolist()) == [3, 100, 200, 250]
 
 
 def test_committee100_certificates(engine):

@@ -5,7 +5,9 @@ multiscalar sum is exact, so the verdict must equal the oracle's (small
 groups) and the per-vote path's (coa_batch.hip, large groups) bit for bit,
 torsion components included.  COA_MSM_MIN (read per call) routes groups of
 at least that many signatures to the Pippenger kernels; COA_MSM_RUN picks the
-bucket workgroup's run length (16, 32, 64 sorted points per lane)."""
+bucket workgroup's run length (16, 32, 64 sorted points per lane).
+COA_BATCH_LAT=0 keeps small calls off the latency prefilter
+(test_gpu_batch.py covers that route)."""
 import random
 import struct
 
@@ -52,6 +54,8 @@ def _signed(engine, n, tag):
 
 
 def _verdicts(engine, monkeypatch, msm_min, msgs, pks, sigs, offs, zs=None, run=None, seed=0):
+    # the exact kernels themselves, not the latency prefilter of small calls
+    monkeypatch.setenv("COA_BATCH_LAT", "0")
     monkeypatch.setenv("COA_MSM_MIN", str(msm_min))
     if run is None:
         monkeypatch.delenv("COA_MSM_RUN", raising=False)
@@ -121,6 +125,23 @@ def test_large_group_matches_per_vote_path(engine, monkeypatch, run):
         got = _verdicts(engine, monkeypatch, 1024, msgs, p, s, offs, zs=z, run=run)
         assert got[0] == ref[0], (name, got, ref)
         assert (got[0] == 0) == (name in ("valid", "equal_weights", "zero_weights_corrupt")), name
+
+
+@pytest.mark.parametrize("n", [1, 67, 127, 128, 300, 1000, 2047])
+def test_one_chunk_groups_short_runs(engine, monkeypatch, n):
+    """Groups that fit one bucket workgroup take runs of 1..16 sorted points
+    per lane (n = 127 / 128: 255 / 257 points, either side of run 1's 256):
+    valid, a corrupted vote and equal weights agree with the per-vote path."""
+    m, pks, sigs = _signed(engine, n, b"short" + bytes([n & 255]))
+    msgs = np.frombuffer(m, np.uint8).reshape(1, 32).copy()
+    offs = np.array([0, n], np.uint64)
+    zs = np.random.default_rng(n).integers(0, 256, (n, 16), dtype=np.uint8)
+    bad = sigs.copy()
+    bad[n // 2, 50] ^= 16
+    for name, s_, z in (("valid", sigs, zs), ("corrupt", bad, zs), ("equal", sigs, np.tile(zs[:1], (n, 1)))):
+        ref = _verdicts(engine, monkeypatch, 0, msgs, pks, s_, offs, zs=z)
+        got = _verdicts(engine, monkeypatch, 1, msgs, pks, s_, offs, zs=z)
+        assert got[0] == ref[0] == (1 if name == "corrupt" else 0), (n, name, got, ref)
 
 
 def test_large_group_with_torsion_vote(engine, monkeypatch):

@@ -30,6 +30,13 @@
 // Both verdicts are dalek's bit for bit: the cached one by the same argument
 // as k_cert_verify_lat's header job, the uncached one by the halving argument
 // of coa_halved.hip (Q == [d]P exactly, d odd).
+// Batch prefilter (LatArgs::batch, Signature::verify_batch of small calls,
+// crypto/src/lib.rs:206-219): the verdict also requires [l]A == O -- the
+// registered key's flag, or for an unregistered key [l](-A) by wave 0 on
+// wave 3's table while waves 1 and 3 run their chains.  Then an accepted vote
+// satisfies R + (h mod l) A == [s]B and (z h mod l) A == z h A, so a group
+// of accepted votes passes dalek's batch equation for every z; any other
+// group is resolved by the exact batch kernels (coa_runtime.cpp).
 // kernels here exceed the +-128 KiB reach of an out-of-line fold (coa_fe.h)
 #define COA_RARE_INLINE
 #include "coa_latency.h"
@@ -226,7 +233,8 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
     if (wave == 1) {  // R's decompression on the rows, the compare, the verdict
       uint32_t pre = 0;
       const uint32_t res = rcmp::decompress_eq(cmp, rw, pre);
-      if (lane == 0) publish(a, item, pre == 0 && res == 3u);
+      const bool tf = !a.batch || (coa_sha::uni(a.kflags[slot]) & COA_KEY_TORSION_FREE) != 0u;
+      if (lane == 0) publish(a, item, pre == 0 && res == 3u && tf);
       VMARK(3)
     } else if (wave == 2) {  // [s]B on the rows, published in row-limb layout
       uint32_t dg[8];
@@ -329,7 +337,19 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
   VMARK(2)
   const int H = (int)coa_sha::uni(sh_meta[0]);
   const bool dneg = coa_sha::uni(sh_meta[1]) != 0;
-  if (wave == 1 || wave == 3) {
+  bool tfree = true;  // [l]A == O (wave 0, batch prefilter only)
+  if (wave == 0 && a.batch) {
+    // [l](-A) from wave 3's table by the same Horner chain (64 signed
+    // radix-16 digits of l; rec = l + 0x88..8), the longest chain of the
+    // kernel: ~2x the halved ones, which is the prefilter's price
+    uint32_t rec[8] = {0xe57e5c75u, 0xe09aeba2u, 0x2b80255eu, 0x9d678267u,
+                       0x88888888u, 0x88888888u, 0x88888888u, 0x98888888u};
+    ge_p3 T;
+    horner(T, sh_tab[0], rec, 64, false);
+    ge_p2 t2;
+    ge_p3_to_p2(t2, T);
+    tfree = ge_p2_is_identity(t2);
+  } else if (wave == 1 || wave == 3) {
     uint32_t rec[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) rec[i] = coa_sha::uni(sh_rec[(wave == 3 ? 0 : 8) + i]);
@@ -361,7 +381,7 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
     }
     ge_p2 q2;
     ge_p3_to_p2(q2, Q);
-    const bool ok = sh_meta[2] != 0 && sh_ok[1] != 0 && sh_ok[3] != 0 && ge_p2_is_identity(q2);
+    const bool ok = sh_meta[2] != 0 && sh_ok[1] != 0 && sh_ok[3] != 0 && ge_p2_is_identity(q2) && tfree;
     if (lane == 0) publish(a, item, ok);
     VMARK(5)
   }

@@ -589,12 +589,21 @@ MsmWs coa_msm_ws_carve(void* base, size_t n) {
 
 // Sorted entries per lane: 128 (32,768 points per workgroup) once that still
 // gives >= 512 bucket workgroups (two per CU), else fewer (down to 16) so
-// small batches fill the 256 CUs.  COA_MSM_RUN overrides (A/B runs).
+// small batches fill the 256 CUs.  A group whose points fit one workgroup at
+// run 16 takes the shortest run that still holds them (one certificate's 135
+// points: run 1, one addition per lane instead of up to 16 in a row -- the
+// lane runs are the serial part of a one-chunk window).  COA_MSM_RUN
+// overrides (A/B runs).
 uint32_t coa_msm_run(size_t n) {
   const char* e = getenv("COA_MSM_RUN");
   if (e) {
     const int r = atoi(e);
-    if (r == 16 || r == 32 || r == 64 || r == 128) return (uint32_t)r;
+    if (r >= 1 && r <= MAXRUN && (r & (r - 1)) == 0) return (uint32_t)r;
+  }
+  if (2 * n + 1 <= 256 * 16) {
+    uint32_t run = 1;
+    while (256 * run < 2 * n + 1) run <<= 1;
+    return run;
   }
   for (uint32_t run = MAXRUN; run > 16; run >>= 1) {
     const size_t chunk = 256 * (size_t)run;

@@ -496,7 +496,10 @@ int lat_res_wait(Dev& d, hipStream_t s, size_t n, uint32_t tag, uint32_t* out) {
   return COA_OK;
 }
 
-int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, size_t n, uint8_t* out) {
+// msg_of: item i's message is msgs + msg_of[i] * 32 (null: item i's own).
+// batch: the verify_batch prefilter (LatArgs::batch).
+int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, size_t n, uint8_t* out,
+               const uint32_t* msg_of = nullptr, bool batch = false) {
   uint32_t tag = 0;
   int rc = lat_res_prepare(d, n, tag);
   if (rc != COA_OK) return rc;
@@ -504,9 +507,11 @@ int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* s
   std::memset(&a, 0, sizeof(a));
   hipStream_t s = d.stream;
   a.n = (uint32_t)n;
+  a.batch = batch ? 1u : 0u;
   a.n_inline = (uint32_t)std::min<size_t>(n, COA_LAT_INLINE);
+  auto msg = [&](size_t i) { return msgs + (msg_of ? (size_t)msg_of[i] : i) * 32; };
   for (size_t i = 0; i < a.n_inline; i++) {
-    std::memcpy(&a.inl[i][0], msgs + i * 32, 32);
+    std::memcpy(&a.inl[i][0], msg(i), 32);
     std::memcpy(&a.inl[i][8], pks + i * 32, 32);
     std::memcpy(&a.inl[i][16], sigs + i * 64, 64);
   }
@@ -516,7 +521,7 @@ int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* s
     HIP_TRY(d.lat.ensure(in_bytes));
     uint8_t* h = static_cast<uint8_t*>(d.pin.p);
     for (size_t i = COA_LAT_INLINE; i < n; i++) {
-      std::memcpy(h + i * 128, msgs + i * 32, 32);
+      std::memcpy(h + i * 128, msg(i), 32);
       std::memcpy(h + i * 128 + 32, pks + i * 32, 32);
       std::memcpy(h + i * 128 + 64, sigs + i * 64, 64);
     }
@@ -706,7 +711,7 @@ int msm_group(Dev& d, const uint8_t* msg, const uint8_t* pks, const uint8_t* sig
 
 int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, const uint64_t* group_offsets,
                       size_t n_groups, const uint8_t* zs_in, uint64_t seed, uint8_t* verdicts_out,
-                      uint32_t gbase = 0);
+                      uint32_t gbase = 0, bool prefilter = true);
 
 // Large groups through the Pippenger path, dealt round-robin to the contexts
 // and run concurrently on their workers; runs of small groups through the
@@ -758,7 +763,7 @@ int batch_groups_split(const uint8_t* msgs, const uint8_t* pks, const uint8_t* s
     std::vector<uint64_t> offs(e - g + 1);
     for (size_t k = 0; k <= e - g; k++) offs[k] = group_offsets[g + k] - v0;
     rc = batch_groups_impl(msgs + g * 32, pks + v0 * 32, sigs + v0 * 64, offs.data(), e - g,
-                           zs_in ? zs_in + v0 * 16 : nullptr, seed, verdicts_out + g, gbase + (uint32_t)g);
+                           zs_in ? zs_in + v0 * 16 : nullptr, seed, verdicts_out + g, gbase + (uint32_t)g, false);
     if (rc != COA_OK) break;
   }
   std::string msg = rc != COA_OK ? g_err : std::string();
@@ -777,8 +782,40 @@ int batch_groups_split(const uint8_t* msgs, const uint8_t* pks, const uint8_t* s
   return rc;
 }
 
+// Calls of at most lat_max() signatures first go through the latency kernel
+// as a prefilter (LatArgs::batch): a group whose votes all pass it (verify_strict
+// and [l]A == O) is accepted by dalek's batch equation for every z, so its
+// verdict is Ok without the batch kernels; the other groups -- some vote
+// failing its own equation, a key with torsion, an encoding error -- are
+// resolved exactly below, each with its own global group index (the z_i
+// derivation binds it).  One launch of one workgroup per vote, the groups'
+// votes side by side: ~0.2 ms for one certificate's 67 votes against ~0.4 ms
+// through the Pippenger kernels.  COA_BATCH_LAT=0 disables it.
+int batch_prefilter(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, const uint64_t* group_offsets,
+                    size_t n_groups, uint8_t* verdicts_out, std::vector<uint8_t>& pass) {
+  const size_t total = group_offsets[n_groups];
+  std::vector<uint32_t> msg_of(total);
+  for (size_t g = 0; g < n_groups; g++)
+    for (uint64_t i = group_offsets[g]; i < group_offsets[g + 1]; i++) msg_of[i] = (uint32_t)g;
+  std::vector<uint8_t> v(total);
+  {
+    std::unique_lock<std::mutex> l;
+    Dev& d = lat_dev(l);
+    HIP_TRY(hipSetDevice(d.id));
+    const int rc = lat_verify(d, msgs, pks, sigs, total, v.data(), msg_of.data(), true);
+    if (rc != COA_OK) return rc;
+  }
+  pass.assign(n_groups, 1);
+  for (size_t g = 0; g < n_groups; g++) {
+    for (uint64_t i = group_offsets[g]; i < group_offsets[g + 1]; i++) pass[g] &= v[i] == 0 ? 1 : 0;
+    if (pass[g]) verdicts_out[g] = 0;
+  }
+  return COA_OK;
+}
+
 int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, const uint64_t* group_offsets,
-                      size_t n_groups, const uint8_t* zs_in, uint64_t seed, uint8_t* verdicts_out, uint32_t gbase) {
+                      size_t n_groups, const uint8_t* zs_in, uint64_t seed, uint8_t* verdicts_out, uint32_t gbase,
+                      bool prefilter) {
   if (n_groups == 0) return COA_OK;
   if (!msgs || !group_offsets || !verdicts_out) return fail(COA_EINVAL, "null argument");
   if (group_offsets[0] != 0) return fail(COA_EINVAL, "group_offsets[0] must be 0");
@@ -788,6 +825,28 @@ int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* si
   if (total && (!pks || !sigs)) return fail(COA_EINVAL, "null pks/sigs");
   if (check_n(total) != COA_OK) return COA_EINVAL;
   const uint64_t eff_seed = zs_in ? 0 : (seed ? seed : os_entropy_seed());
+  if (prefilter && total > 0 && total <= lat_max() && !env_is("COA_BATCH_LAT", "0")) {
+    std::vector<uint8_t> pass;
+    int rc = batch_prefilter(msgs, pks, sigs, group_offsets, n_groups, verdicts_out, pass);
+    if (rc != COA_OK) return rc;
+    // runs of groups the prefilter did not accept, through the exact path
+    for (size_t g = 0; g < n_groups;) {
+      if (pass[g]) {
+        g++;
+        continue;
+      }
+      size_t e = g;
+      while (e < n_groups && !pass[e]) e++;
+      const uint64_t v0 = group_offsets[g];
+      std::vector<uint64_t> offs(e - g + 1);
+      for (size_t k = 0; k <= e - g; k++) offs[k] = group_offsets[g + k] - v0;
+      rc = batch_groups_impl(msgs + g * 32, pks + v0 * 32, sigs + v0 * 64, offs.data(), e - g,
+                             zs_in ? zs_in + v0 * 16 : nullptr, eff_seed, verdicts_out + g, gbase + (uint32_t)g, false);
+      if (rc != COA_OK) return rc;
+      g = e;
+    }
+    return COA_OK;
+  }
   // One or two groups take the Pippenger path at any size: the per-vote path
   // waits for one lane's whole joint scalar multiplication (~1.4 ms however
   // few groups), the Pippenger kernels spread a group over the chip (~0.5 ms
