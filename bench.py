@@ -305,6 +305,63 @@ def c5_shard(local, dev, stream, n=1 << 21, steps=3):
             "verdicts_ok": ok}
 
 
+def c2_inflight(local, dev, n=65536, calls=48, depths=(1, 2, 3, 4)):
+    """C2 batches with several verify calls in flight: one stream, workspace
+    and verdict buffer per in-flight call, calls dealt round-robin -- the
+    aggregation queue's operating mode (four slots per GPU).  Each call is a
+    whole 65,536-triple C2 verify over resident inputs; depth 1 is the
+    headline's serial mode.  At one call, k_verify_main has one wave per SIMD
+    (65,536 items, one lane each); calls in flight let a second call's
+    k_pre_halve and k_verify_main waves fill the SIMD issue slots the lone
+    wave leaves.  Timed by HIP events on every stream
+    (the first waits on a start event, the last call of each stream joins)."""
+    import torch
+
+    import coa_crypto
+    import workloads
+
+    seeds = torch.from_numpy(workloads.key_seeds(n)).to(dev)
+    msgs = torch.from_numpy(workloads.messages(n)).to(dev)
+    pks = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    sigs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    coa_crypto.sign_many_device(local, seeds, msgs, pks, sigs)
+    del seeds
+    torch.cuda.synchronize()
+    out = {"workload": f"C2 batches ({n:,} triples per call) with d verify calls in flight", "depths": {}}
+    for depth in depths:
+        streams = [torch.cuda.Stream(dev) for _ in range(depth)]
+        wss = [torch.empty(coa_crypto.verify_workspace_bytes(n), dtype=torch.uint8, device=dev) for _ in range(depth)]
+        outs = [torch.ones(n, dtype=torch.uint8, device=dev) for _ in range(depth)]
+
+        def run(k):
+            for i in range(k):
+                j = i % depth
+                coa_crypto.verify_strict_many_device(local, msgs, pks, sigs, outs[j], wss[j], streams[j])
+
+        run(2 * depth)
+        torch.cuda.synchronize()
+        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        start.record(streams[0])
+        for st in streams[1:]:
+            st.wait_event(start)
+        run(calls)
+        for st in streams[1:]:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            streams[0].wait_event(ev)
+        end.record(streams[0])
+        torch.cuda.synchronize()
+        ms = start.elapsed_time(end) / calls
+        ok = all(int(o.sum().item()) == 0 for o in outs)
+        out["depths"][str(depth)] = {"ms_per_call": round(ms, 4), "verifications_per_s": round(n / (ms * 1e-3), 1),
+                                     "verdicts_ok": ok}
+        del wss, outs, streams
+        torch.cuda.empty_cache()
+    del msgs, pks, sigs
+    torch.cuda.empty_cache()
+    return out
+
+
 def batch_alg_int32_ops_survey(n):
     """SURVEY.md 8(d) W_batch(n): 2n decompressions (276 field ops each),
     Pippenger with c = 5 over 2n + 1 (+32) points (9 field ops per addition,
@@ -1087,6 +1144,8 @@ def main():
             secondary["verify_single"] = verify_single(local, cpu["single_verify_p50_ms"] if cpu else None)
         if on("c5_shard"):
             secondary["c5_shard"] = c5_shard(local, dev, stream)
+        if on("c2_inflight"):
+            secondary["c2_inflight"] = c2_inflight(local, dev)
         if on("verify_batch"):
             secondary["verify_batch"] = verify_batch_config(local, dev, stream)
         if on("c4_sha512"):

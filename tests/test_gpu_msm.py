@@ -127,11 +127,12 @@ def test_large_group_matches_per_vote_path(engine, monkeypatch, run):
         assert (got[0] == 0) == (name in ("valid", "equal_weights", "zero_weights_corrupt")), name
 
 
-@pytest.mark.parametrize("n", [1, 67, 127, 128, 300, 1000, 2047])
+@pytest.mark.parametrize("n", [1, 67, 300, 511, 512, 1000, 2047])
 def test_one_chunk_groups_short_runs(engine, monkeypatch, n):
-    """Groups that fit one bucket workgroup take runs of 1..16 sorted points
-    per lane (n = 127 / 128: 255 / 257 points, either side of run 1's 256):
-    valid, a corrupted vote and equal weights agree with the per-vote path."""
+    """Groups that fit one bucket workgroup take runs of 4..16 sorted points
+    per lane (n = 511 / 512: 1,023 / 1,025 points, either side of run 4's
+    1,024): valid, a corrupted vote and equal weights agree with the
+    per-vote path."""
     m, pks, sigs = _signed(engine, n, b"short" + bytes([n & 255]))
     msgs = np.frombuffer(m, np.uint8).reshape(1, 32).copy()
     offs = np.array([0, n], np.uint64)

@@ -590,10 +590,12 @@ MsmWs coa_msm_ws_carve(void* base, size_t n) {
 // Sorted entries per lane: 128 (32,768 points per workgroup) once that still
 // gives >= 512 bucket workgroups (two per CU), else fewer (down to 16) so
 // small batches fill the 256 CUs.  A group whose points fit one workgroup at
-// run 16 takes the shortest run that still holds them (one certificate's 135
-// points: run 1, one addition per lane instead of up to 16 in a row -- the
-// lane runs are the serial part of a one-chunk window).  COA_MSM_RUN
-// overrides (A/B runs).
+// run 16 takes the shortest run of at least 4 that still holds them: one
+// certificate's 135 points, one group through these kernels, p50 0.388 ms at
+// run 16, 0.353 at 8, 0.347 at 4, 0.374 at 2, 0.432 at 1 (tools/gpu_r3_k.sh:
+// the lane runs are the serial part of a one-chunk window, but below 4 more
+// entries become continuation segments the gather adds one by one).
+// COA_MSM_RUN overrides (A/B runs).
 uint32_t coa_msm_run(size_t n) {
   const char* e = getenv("COA_MSM_RUN");
   if (e) {
@@ -601,7 +603,7 @@ uint32_t coa_msm_run(size_t n) {
     if (r >= 1 && r <= MAXRUN && (r & (r - 1)) == 0) return (uint32_t)r;
   }
   if (2 * n + 1 <= 256 * 16) {
-    uint32_t run = 1;
+    uint32_t run = 4;
     while (256 * run < 2 * n + 1) run <<= 1;
     return run;
   }
