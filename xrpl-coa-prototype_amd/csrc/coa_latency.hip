@@ -191,6 +191,170 @@ COA_DEV void publish(const LatArgs& a, uint32_t item, bool ok) {
   __hip_atomic_store(a.res + item, (a.tag << 8) | (ok ? 0u : 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// wave 0 of the uncached path: k = SHA-512(R || A || M) mod l, the halving
+// (c, d), e = d s mod l (negated with d); the recoded c, d and e to sh_rec,
+// the chain length, d's sign and s < l to sh_meta (lane 0); e stays in `e`
+COA_DEV void halve_item(uint32_t* sh_rec, uint32_t* sh_meta, uint32_t* e_out, const uint32_t* msg,
+                        const uint32_t* pk, const uint32_t* rw, const uint32_t* sw, uint32_t lane) {
+  uint64_t st[8];
+  uint32_t h[16], w[24];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    w[i] = rw[i];
+    w[8 + i] = pk[i];
+    w[16 + i] = msg[i];
+  }
+  coa_sha::hash_words<24>(st, w);
+  coa_sha::state_to_le_words(h, st);
+  sc k;
+  sc_reduce512(k, h);
+  uint32_t c[8], d[8];
+  int cost;
+  bool neg;
+  coa_halve::halve(c, d, cost, neg, k.v);
+  sc e;
+  sc_mul(e, d, sw);  // s may be non-canonical here; the verdict rejects it
+  if (neg) {
+    sc en;
+    sc_neg(en, e.v);
+    e = en;
+  }
+  add_const_word(c, 0x88888888u);
+  add_const_word(d, 0x88888888u);
+#pragma unroll
+  for (int i = 0; i < 8; i++) e_out[i] = e.v[i];
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      sh_rec[i] = c[i];
+      sh_rec[8 + i] = d[i];
+      sh_rec[16 + i] = e.v[i];
+    }
+    sh_meta[0] = (uint32_t)((cost + 2 + 3) / 4);  // c, |d| < 2^(4H - 2)
+    sh_meta[1] = neg;
+    sh_meta[2] = sc_is_canonical(sw);
+  }
+}
+
+// waves 1 and 3: decompress the encoding on the rows and build the 8-entry
+// table j(-Q); true when it decompresses and is not of small order
+COA_DEV bool decompress_table(uint32_t* tab, const uint32_t* enc) {
+  ge_p3 Q;
+  const bool dec = ge_decompress<true>(Q, enc);
+  const bool ok = dec && !ge_is_small_order(Q);
+  build_table(tab, Q);
+  return ok;
+}
+
+// Q + P0 + P1 == O (one-lane arithmetic; the points from LDS)
+COA_DEV bool sum_is_identity(ge_p3 Q, const uint32_t* p0, const uint32_t* p1) {
+  ge_p3 T;
+  ge_cached c;
+  ge_p1p1 t;
+  const uint32_t* ps[2] = {p0, p1};
+#pragma unroll 1
+  for (int i = 0; i < 2; i++) {
+    lds_get_p3(T, ps[i]);
+    ge_p3_to_cached(c, T);
+    ge_add(t, Q, c);
+    ge_p1p1_to_p3(Q, t);
+  }
+  ge_p2 q2;
+  ge_p3_to_p2(q2, Q);
+  return ge_p2_is_identity(q2);
+}
+
+COA_DEV void flag_set(uint32_t* f) { __hip_atomic_store(f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+COA_DEV void flag_add(uint32_t* f) { __hip_atomic_fetch_add(f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+COA_DEV void flag_wait(uint32_t* f, uint32_t v) {
+#pragma unroll 1
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
+}
+
+// The verify_batch prefilter on an unregistered key (LatArgs::batch): the
+// halved-scalar verify_strict check of the barrier path, plus [l]A == O as
+// [2^252]A == [l - 2^252](-A).  [2^252]A is a pure doubling chain (the
+// kernel's longest: 252 doublings, two row products each) on wave 2 from
+// its own decompression of A, started at once; wave 0 takes over wave 2's
+// [e]B after the halving, then [l - 2^252](-A) (125 bits, 32 signed radix-16
+// digits) on wave 3's table.  LDS flags instead of barriers, so no wave waits
+// for a phase it does not need.  Same verdict as one 64-digit [l](-A) chain
+// after the barrier, in ~0.8 of its time.
+COA_DEV void uncached_batch(const LatArgs& a, uint32_t item, uint32_t wave, uint32_t lane, const uint32_t* msg,
+                            const uint32_t* pk, const uint32_t* rw, const uint32_t* sw, uint32_t* sh_rec,
+                            uint32_t* sh_ok, uint32_t (*sh_pt)[32], uint32_t (*sh_tab)[8 * 32]) {
+  __shared__ uint32_t s_meta[4];
+  __shared__ uint32_t s_flag[4];  // 0: sh_rec ready, 1: table j(-A) ready, 2: points published (count)
+  __shared__ uint32_t s_big[32];  // [2^252]A
+  if (threadIdx.x < 4) s_flag[threadIdx.x] = 0;
+  __syncthreads();
+  if (wave == 0) {
+    uint32_t e[8];
+    halve_item(sh_rec, s_meta, e, msg, pk, rw, sw, lane);
+    if (lane == 0) flag_set(&s_flag[0]);
+    ge_p3 E;
+    comb_butterfly(E, e, a.comb, lane);
+    flag_wait(&s_flag[1], 1);
+    uint32_t rec[8] = {0xe57e5c75u, 0xe09aeba2u, 0x2b80255eu, 0x9d678267u, 0, 0, 0, 0};  // (l - 2^252) + 0x88..8
+    ge_p3 D;
+    horner(D, sh_tab[0], rec, 32, false);  // D = [l - 2^252](-A)
+    flag_wait(&s_flag[2], 3);
+    bool ok = s_meta[2] != 0 && sh_ok[1] != 0 && sh_ok[3] != 0 && sum_is_identity(E, sh_pt[0], sh_pt[1]);
+    // [l]A = [2^252]A - D
+    ge_p3 big;
+    lds_get_p3(big, s_big);
+    fe_neg(D.X, D.X);
+    fe_neg(D.T, D.T);
+    ge_cached c;
+    ge_p1p1 t;
+    ge_p3_to_cached(c, D);
+    ge_add(t, big, c);
+    ge_p1p1_to_p3(big, t);
+    ge_p2 b2;
+    ge_p3_to_p2(b2, big);
+    ok = ok && ge_p2_is_identity(b2);
+    if (lane == 0) publish(a, item, ok);
+  } else if (wave == 1 || wave == 3) {
+    const bool ok = decompress_table(sh_tab[wave == 3 ? 0 : 1], wave == 3 ? pk : rw);
+    if (lane == 0) {
+      sh_ok[wave] = ok;
+      if (wave == 3) flag_set(&s_flag[1]);
+    }
+    flag_wait(&s_flag[0], 1);
+    const int H = (int)coa_sha::uni(s_meta[0]);
+    const bool dneg = coa_sha::uni(s_meta[1]) != 0;
+    uint32_t rec[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) rec[i] = coa_sha::uni(sh_rec[(wave == 3 ? 0 : 8) + i]);
+    ge_p3 T;
+    horner(T, sh_tab[wave == 3 ? 0 : 1], rec, H, wave == 1 && dneg);
+    if (lane == 0) {
+      lds_put_p3(sh_pt[wave == 3 ? 0 : 1], T);
+      flag_add(&s_flag[2]);
+    }
+  } else {  // wave 2
+    ge_p3 A;
+    (void)ge_decompress<true>(A, pk);  // a failed decompression is wave 3's verdict
+    rp::P1 acc3;
+    rp::from_p3(acc3, A);
+    rp::P2 acc2 = {acc3.X, acc3.Y, acc3.Z};
+    rp::L1 t;
+#pragma unroll 1
+    for (int k = 0; k < 251; k++) {
+      rp::dbl(t, acc2);
+      rp::to_p2(acc2, t);
+    }
+    rp::dbl(t, acc2);
+    rp::to_p3(acc3, t);
+    ge_p3 big;
+    rp::to_ge_p3(big, acc3);
+    if (lane == 0) {
+      lds_put_p3(s_big, big);
+      flag_add(&s_flag[2]);
+    }
+  }
+}
+
 }  // namespace
 
 #ifdef COA_VLAT_TRACE  // phase timestamps of item 0 per wave (tools/vlat_trace.py)
@@ -288,48 +452,15 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
   }
 
   // ------------------------------------------------------ uncached key
+  if (a.batch) {  // verify_batch prefilter: the same check plus [l]A == O
+    uncached_batch(a, item, wave, lane, msg, pk, rw, sw, sh_rec, sh_ok, sh_pt, sh_tab);
+    return;
+  }
   if (wave == 0) {
-    uint64_t st[8];
-    uint32_t h[16], w[24];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      w[i] = rw[i];
-      w[8 + i] = pk[i];
-      w[16 + i] = msg[i];
-    }
-    coa_sha::hash_words<24>(st, w);
-    coa_sha::state_to_le_words(h, st);
-    sc k;
-    sc_reduce512(k, h);
-    uint32_t c[8], d[8];
-    int cost;
-    bool neg;
-    coa_halve::halve(c, d, cost, neg, k.v);
-    sc e;
-    sc_mul(e, d, sw);  // s may be non-canonical here; the verdict rejects it
-    if (neg) {
-      sc en;
-      sc_neg(en, e.v);
-      e = en;
-    }
-    add_const_word(c, 0x88888888u);
-    add_const_word(d, 0x88888888u);
-    if (lane == 0) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        sh_rec[i] = c[i];
-        sh_rec[8 + i] = d[i];
-        sh_rec[16 + i] = e.v[i];
-      }
-      sh_meta[0] = (uint32_t)((cost + 2 + 3) / 4);  // c, |d| < 2^(4H - 2)
-      sh_meta[1] = neg;
-      sh_meta[2] = sc_is_canonical(sw);
-    }
+    uint32_t e[8];
+    halve_item(sh_rec, sh_meta, e, msg, pk, rw, sw, lane);
   } else if (wave == 1 || wave == 3) {
-    ge_p3 Q;
-    const bool dec = ge_decompress<true>(Q, wave == 3 ? pk : rw);
-    const bool ok = dec && !ge_is_small_order(Q);
-    build_table(sh_tab[wave == 3 ? 0 : 1], Q);
+    const bool ok = decompress_table(sh_tab[wave == 3 ? 0 : 1], wave == 3 ? pk : rw);
     if (lane == 0) sh_ok[wave] = ok;
   }
   VMARK(1)
@@ -337,19 +468,7 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
   VMARK(2)
   const int H = (int)coa_sha::uni(sh_meta[0]);
   const bool dneg = coa_sha::uni(sh_meta[1]) != 0;
-  bool tfree = true;  // [l]A == O (wave 0, batch prefilter only)
-  if (wave == 0 && a.batch) {
-    // [l](-A) from wave 3's table by the same Horner chain (64 signed
-    // radix-16 digits of l; rec = l + 0x88..8), the longest chain of the
-    // kernel: ~2x the halved ones, which is the prefilter's price
-    uint32_t rec[8] = {0xe57e5c75u, 0xe09aeba2u, 0x2b80255eu, 0x9d678267u,
-                       0x88888888u, 0x88888888u, 0x88888888u, 0x98888888u};
-    ge_p3 T;
-    horner(T, sh_tab[0], rec, 64, false);
-    ge_p2 t2;
-    ge_p3_to_p2(t2, T);
-    tfree = ge_p2_is_identity(t2);
-  } else if (wave == 1 || wave == 3) {
+  if (wave == 1 || wave == 3) {
     uint32_t rec[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) rec[i] = coa_sha::uni(sh_rec[(wave == 3 ? 0 : 8) + i]);
@@ -368,20 +487,9 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
   __syncthreads();
   VMARK(4)
   if (wave == 0) {
-    ge_p3 Q, T;
-    ge_cached c;
-    ge_p1p1 t;
+    ge_p3 Q;
     lds_get_p3(Q, sh_pt[2]);
-#pragma unroll 1
-    for (int i = 0; i < 2; i++) {
-      lds_get_p3(T, sh_pt[i]);
-      ge_p3_to_cached(c, T);
-      ge_add(t, Q, c);
-      ge_p1p1_to_p3(Q, t);
-    }
-    ge_p2 q2;
-    ge_p3_to_p2(q2, Q);
-    const bool ok = sh_meta[2] != 0 && sh_ok[1] != 0 && sh_ok[3] != 0 && ge_p2_is_identity(q2) && tfree;
+    const bool ok = sh_meta[2] != 0 && sh_ok[1] != 0 && sh_ok[3] != 0 && sum_is_identity(Q, sh_pt[0], sh_pt[1]);
     if (lane == 0) publish(a, item, ok);
     VMARK(5)
   }
