@@ -6,3 +6,5 @@ tail -2 gpurun_out/m_tests.log
 timeout -k 10 120 python3 tools/msm1_probe.py 67 300 || exit 1
 timeout -k 10 120 python3 tools/msm1_probe.py 3 300 || exit 1
 COA_BATCH_LAT=0 timeout -k 10 120 python3 tools/msm1_probe.py 67 300 || exit 1
+timeout -k 10 120 python3 tools/msm1_probe.py 3 200 300 || exit 1
+COA_BATCH_LAT=0 timeout -k 10 120 python3 tools/msm1_probe.py 3 200 300 || exit 1

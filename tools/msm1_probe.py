@@ -3,7 +3,8 @@ host pointers in, verdict out: Signature::verify_batch, crypto/src/lib.rs:
 206-219) -- p50 over `calls` calls; under `rocprofv3 --kernel-trace` the
 trace shows how the call's wall time splits into kernels and gaps.
 
-usage: python tools/msm1_probe.py [votes] [calls]"""
+usage: python tools/msm1_probe.py [votes] [calls] [groups]
+(groups > 1: that many certificates of `votes` votes each in one call)"""
 import json
 import os
 import sys
@@ -20,17 +21,19 @@ from workloads import key_seeds, messages  # noqa: E402
 
 nv = int(sys.argv[1]) if len(sys.argv) > 1 else 67
 calls = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+ng = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 coa_crypto.init(0)
-m = np.repeat(messages(1, 4242), nv, axis=0)
-pks, sigs = coa_crypto.sign_many(key_seeds(nv, 9000), m)
-offs = np.array([0, nv], np.uint64)
-msg = m[:1].copy()
+msg = messages(ng, 4242)
+m = np.repeat(msg, nv, axis=0)
+pks, sigs = coa_crypto.sign_many(key_seeds(nv * ng, 9000), m)
+offs = np.arange(0, nv * ng + 1, nv, dtype=np.uint64)
 lat = []
 for i in range(calls + 20):
     t0 = time.perf_counter()
     v = coa_crypto.verify_batch_groups(msg, pks, sigs, offs)
     lat.append(time.perf_counter() - t0)
-    assert int(v[0]) == 0
+    assert not v.any()
 lat = np.array(lat[20:]) * 1e3
-print(json.dumps({"votes": nv, "calls": calls, "p50_ms": round(float(np.percentile(lat, 50)), 4),
+print(json.dumps({"votes": nv, "groups": ng, "route": os.environ.get("COA_BATCH_LAT", "default"), "calls": calls,
+                  "p50_ms": round(float(np.percentile(lat, 50)), 4),
                   "p99_ms": round(float(np.percentile(lat, 99)), 4)}))
