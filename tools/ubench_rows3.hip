@@ -1,0 +1,353 @@
+// Row product A/B on a lone wave (s_memtime cycles per row squaring, 100
+// dependent squarings, unrolled by four as fw::sqn does):
+//   v2   mul_v2, the round-2 row product
+//   v3   fw::mul, round 3 (VOP2-DPP spread and wrap, masked lanes 8..15,
+//        three asm statements): the form in use
+//   v4   mul_v4, the same tail in one asm statement
+//   v5   mul_v5, one statement with the DPP operand moves interleaved with
+//        the multiply-accumulates
+// plus a correctness sweep: every row of 16 waves squares and multiplies its
+// own random value (and carry-heavy patterns) through both forms; each result
+// is compared with the one-lane fe_sq / fe_mul (canonical).
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../xrpl-coa-prototype_amd/csrc ubench_rows3.hip -o ubench_rows3
+#include <cstdio>
+#include <cstdlib>
+
+#include "coa_fe_wave.h"
+
+// the round-2 row product (coa_fe_wave.h before round 3)
+__device__ uint32_t mul_v2(uint32_t a, uint32_t b) {
+  uint32_t bk[8], ak[8];
+  bk[0] = fw::bcast<0>(b);
+  bk[1] = fw::bcast<1>(b);
+  bk[2] = fw::bcast<2>(b);
+  bk[3] = fw::bcast<3>(b);
+  bk[4] = fw::bcast<4>(b);
+  bk[5] = fw::bcast<5>(b);
+  bk[6] = fw::bcast<6>(b);
+  bk[7] = fw::bcast<7>(b);
+  ak[0] = a;
+  ak[1] = fw::shr<1>(a);
+  ak[2] = fw::shr<2>(a);
+  ak[3] = fw::shr<3>(a);
+  ak[4] = fw::shr<4>(a);
+  ak[5] = fw::shr<5>(a);
+  ak[6] = fw::shr<6>(a);
+  ak[7] = fw::shr<7>(a);
+  // the whole column in one asm statement (hipcc pads each statement with an
+  // s_nop before the next VALU that reads its outputs)
+  uint64_t acc = 0;
+  uint32_t c2 = 0;
+  asm("v_mad_u64_u32 %0, vcc, %2, %10, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %3, %11, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %4, %12, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %5, %13, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %6, %14, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %7, %15, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %8, %16, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %9, %17, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(c2)
+      : "v"(ak[0]), "v"(ak[1]), "v"(ak[2]), "v"(ak[3]), "v"(ak[4]), "v"(ak[5]), "v"(ak[6]), "v"(ak[7]), "v"(bk[0]),
+        "v"(bk[1]), "v"(bk[2]), "v"(bk[3]), "v"(bk[4]), "v"(bk[5]), "v"(bk[6]), "v"(bk[7])
+      : "vcc");
+  // column c = w0 + 2^32 w1 + 2^64 w2: spread w1 to lane c+1, w2 to c+2
+  // (n_c < 2^34), fold n_{c+8} by 38 into lane c (< 2^40), then the wrap
+  // passes of fold_carry bring every lane below 2^32
+  const uint64_t n = (uint64_t)(uint32_t)acc + fw::shr<1>((uint32_t)(acc >> 32)) + fw::shr<2>(c2);
+  const uint32_t r = fw::row_lane();
+  const uint32_t up_lo = fw::shl<8>((uint32_t)n), up_hi = fw::shl<8>((uint32_t)(n >> 32));
+  uint64_t m = (uint64_t)up_lo * 38u + (r < 8 ? n : 0);
+  m += (uint64_t)__umul24(up_hi, 38u) << 32;  // up_hi <= 3
+  return fw::normalize(m);
+}
+
+// the whole tail in one asm statement (v[2:3], v[4:5] fixed)
+__device__ uint32_t mul_v4(uint32_t a, uint32_t b) {
+  uint32_t bk[8], ak[8];
+  bk[0] = fw::bcast<0>(b);
+  bk[1] = fw::bcast<1>(b);
+  bk[2] = fw::bcast<2>(b);
+  bk[3] = fw::bcast<3>(b);
+  bk[4] = fw::bcast<4>(b);
+  bk[5] = fw::bcast<5>(b);
+  bk[6] = fw::bcast<6>(b);
+  bk[7] = fw::bcast<7>(b);
+  ak[0] = a;
+  ak[1] = fw::shr<1>(a);
+  ak[2] = fw::shr<2>(a);
+  ak[3] = fw::shr<3>(a);
+  ak[4] = fw::shr<4>(a);
+  ak[5] = fw::shr<5>(a);
+  ak[6] = fw::shr<6>(a);
+  ak[7] = fw::shr<7>(a);
+  uint32_t lo, hi, c2, nlo, nhi, ul, uh, t;
+  asm(// column c: v[2:3] + 2^64 c2 = sum_k a_{c-k} b_k
+      "v_mad_u64_u32 v[2:3], vcc, %[a0], %[b0], 0\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a1], %[b1], v[2:3]\n\t"
+      "v_addc_co_u32_e64 %[c2], vcc, 0, 0, vcc\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a2], %[b2], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a3], %[b3], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a4], %[b4], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a5], %[b5], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a6], %[b6], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a7], %[b7], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "s_nop 0\n\t"  // DPP read of v3 two instructions after its write
+      // n_c = w0_c + w1_{c-1} + c2_{c-2} (< 2^34) = nlo + 2^32 nhi
+      "v_add_co_u32_dpp %[nlo], vcc, v3, v2 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_addc_co_u32_e64 %[nhi], vcc, 0, 0, vcc\n\t"
+      "v_add_co_u32_dpp %[nlo], vcc, %[c2], %[nlo] row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_addc_co_u32_e32 %[nhi], vcc, 0, %[nhi], vcc\n\t"
+      // v[4:5] = n on lanes 0..7 (0 above); ul/uh = n_{c+8} (0 past the row)
+      "v_and_b32_e32 v4, %[nlo], %[m8]\n\t"
+      "v_and_b32_e32 v5, %[nhi], %[m8]\n\t"
+      "v_mov_b32_dpp %[ul], %[nlo] row_shl:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mov_b32_dpp %[uh], %[nhi] row_shl:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      // fold by 2^256 = 38: v[4:5] = n_c + 38 n_{c+8} < 2^40 (uh <= 3)
+      "v_mad_u64_u32 v[4:5], vcc, %[ul], 38, v[4:5]\n\t"
+      "v_mad_u32_u24 v5, %[uh], 38, v5\n\t"
+      "s_nop 1\n\t"  // DPP reads of v5 next
+      // wrap, in place on lanes 0..7 (bank_mask 0x3; lanes 8..15 hold 0):
+      // lo = m_lo + m_hi of the lane below (lane 0: + 38 m_hi of lane 7)
+      "v_mul_u32_u24_dpp %[t], v5, %[k] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_co_u32_dpp v4, vcc, v5, v4 row_shr:1 row_mask:0xf bank_mask:0x3 bound_ctrl:1\n\t"
+      "v_addc_co_u32_dpp v5, vcc, %[z], %[z], vcc quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t"
+      "v_add_co_u32_e32 v4, vcc, %[t], v4\n\t"
+      "v_addc_co_u32_e32 v5, vcc, 0, v5, vcc"
+      : [lo] "=&{v4}"(lo), [hi] "=&{v5}"(hi), [c2] "=&v"(c2), [nlo] "=&v"(nlo), [nhi] "=&v"(nhi), [ul] "=&v"(ul),
+        [uh] "=&v"(uh), [t] "=&v"(t)
+      : [a0] "v"(ak[0]), [a1] "v"(ak[1]), [a2] "v"(ak[2]), [a3] "v"(ak[3]), [a4] "v"(ak[4]), [a5] "v"(ak[5]),
+        [a6] "v"(ak[6]), [a7] "v"(ak[7]), [b0] "v"(bk[0]), [b1] "v"(bk[1]), [b2] "v"(bk[2]), [b3] "v"(bk[3]),
+        [b4] "v"(bk[4]), [b5] "v"(bk[5]), [b6] "v"(bk[6]), [b7] "v"(bk[7]), [m8] "v"(fw::lanes_lo8()),
+        [k] "v"(fw::k38_lane0()), [z] "v"(0u)
+      : "vcc", "v2", "v3");
+  if (__builtin_expect(__any(hi != 0u), 0)) {
+    const uint32_t r = fw::row_lane();
+    uint64_t v = ((uint64_t)hi << 32) | lo;
+#pragma unroll 1
+    do fw::wrap_step(v, r);
+    while (__any((uint32_t)(v >> 32) != 0u));
+    lo = (uint32_t)v;
+  }
+  return lo;
+}
+
+// one statement, the DPP operand moves interleaved with the multiply-accumulates
+__device__ uint32_t mul_v5(uint32_t a, uint32_t b) {
+  uint32_t lo, hi, c2, nlo, nhi, ul, uh, t, b0, b1, a0, a1;
+  asm("s_nop 1\n\t"  // DPP reads of a and b (written just before the statement)
+      "v_mov_b32_dpp %[b0], %[b] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %[b1], %[b] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %[a1], %[a] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a], %[b0], 0\n\t"
+      "v_mov_b32_dpp %[b0], %[b] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %[a0], %[a] row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a1], %[b1], v[2:3]\n\t"
+      "v_addc_co_u32_e64 %[c2], vcc, 0, 0, vcc\n\t"
+      "v_mov_b32_dpp %[b1], %[b] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %[a1], %[a] row_shr:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a0], %[b0], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "v_mov_b32_dpp %[b0], %[b] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %[a0], %[a] row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a1], %[b1], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "v_mov_b32_dpp %[b1], %[b] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %[a1], %[a] row_shr:5 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a0], %[b0], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "v_mov_b32_dpp %[b0], %[b] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %[a0], %[a] row_shr:6 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a1], %[b1], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "v_mov_b32_dpp %[b1], %[b] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %[a1], %[a] row_shr:7 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a0], %[b0], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[a1], %[b1], v[2:3]\n\t"
+      "v_addc_co_u32_e32 %[c2], vcc, 0, %[c2], vcc\n\t"
+      "s_nop 0\n\t"
+      "v_add_co_u32_dpp %[nlo], vcc, v3, v2 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_addc_co_u32_e64 %[nhi], vcc, 0, 0, vcc\n\t"
+      "v_add_co_u32_dpp %[nlo], vcc, %[c2], %[nlo] row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_addc_co_u32_e32 %[nhi], vcc, 0, %[nhi], vcc\n\t"
+      "v_and_b32_e32 %[lo], %[nlo], %[m8]\n\t"
+      "v_and_b32_e32 %[hi], %[nhi], %[m8]\n\t"
+      "v_mov_b32_dpp %[ul], %[nlo] row_shl:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mov_b32_dpp %[uh], %[nhi] row_shl:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mad_u64_u32 v[2:3], vcc, %[ul], 38, 0\n\t"
+      "v_mad_u32_u24 %[hi], %[uh], 38, %[hi]\n\t"
+      "v_add_co_u32_e32 %[lo], vcc, v2, %[lo]\n\t"
+      "v_addc_co_u32_e32 %[hi], vcc, v3, %[hi], vcc\n\t"
+      "s_nop 1\n\t"
+      "v_mul_u32_u24_dpp %[t], %[hi], %[k] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_co_u32_dpp %[lo], vcc, %[hi], %[lo] row_shr:1 row_mask:0xf bank_mask:0x3 bound_ctrl:1\n\t"
+      "v_addc_co_u32_dpp %[hi], vcc, %[z], %[z], vcc quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t"
+      "v_add_co_u32_e32 %[lo], vcc, %[t], %[lo]\n\t"
+      "v_addc_co_u32_e32 %[hi], vcc, 0, %[hi], vcc"
+      : [lo] "=&v"(lo), [hi] "=&v"(hi), [c2] "=&v"(c2), [nlo] "=&v"(nlo), [nhi] "=&v"(nhi), [ul] "=&v"(ul),
+        [uh] "=&v"(uh), [t] "=&v"(t), [b0] "=&v"(b0), [b1] "=&v"(b1), [a0] "=&v"(a0), [a1] "=&v"(a1)
+      : [a] "v"(a), [b] "v"(b), [m8] "v"(fw::lanes_lo8()), [k] "v"(fw::k38_lane0()), [z] "v"(0u)
+      : "vcc", "v2", "v3");
+  if (__builtin_expect(__any(hi != 0u), 0)) {
+    const uint32_t r = fw::row_lane();
+    uint64_t v = ((uint64_t)hi << 32) | lo;
+#pragma unroll 1
+    do fw::wrap_step(v, r);
+    while (__any((uint32_t)(v >> 32) != 0u));
+    lo = (uint32_t)v;
+  }
+  return lo;
+}
+
+
+template <int V>
+__device__ uint32_t sqn4(uint32_t a, int n) {
+#pragma unroll 1
+  for (int i = 0; i < n; i += 4) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) a = V == 5 ? mul_v5(a, a) : (V == 4 ? mul_v4(a, a) : (V == 3 ? fw::mul(a, a) : mul_v2(a, a)));
+  }
+  return a;
+}
+
+__global__ void k_time(const uint32_t* in, uint32_t* out, long long* cyc) {
+  fe z;
+#pragma unroll
+  for (int i = 0; i < 8; i++) z.v[i] = in[i];
+  const uint32_t x0 = fw::from_fe(z);
+  long long t0 = clock64();
+  const uint32_t a = sqn4<2>(x0, 100);
+  long long t1 = clock64();
+  const uint32_t b = sqn4<3>(x0, 100);
+  long long t2 = clock64();
+  const uint32_t c = sqn4<4>(x0, 100);
+  long long t3 = clock64();
+  const uint32_t d = sqn4<5>(x0, 100);
+  long long t4 = clock64();
+  fe y = z, ref, ya, yb, yc, yd;
+  fe_sqn(y, y, 100);
+  fe_canon(ref, y);
+  fw::to_fe(ya, a);
+  fw::to_fe(yb, b);
+  fe_canon(ya, ya);
+  fe_canon(yb, yb);
+  fw::to_fe(yc, c);
+  fe_canon(yc, yc);
+  fw::to_fe(yd, d);
+  fe_canon(yd, yd);
+  uint32_t bad = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    bad |= (ya.v[i] != ref.v[i]) | ((yb.v[i] != ref.v[i]) << 1) | ((yc.v[i] != ref.v[i]) << 2) | ((yd.v[i] != ref.v[i]) << 3);
+  if (threadIdx.x == 0) {
+    out[0] = bad;
+    cyc[0] = t1 - t0;
+    cyc[1] = t2 - t1;
+    cyc[2] = t3 - t2;
+    cyc[3] = t4 - t3;
+  }
+}
+
+// each row r of each wave: x = in[row], y = in[row + 1]; checks x^2, x*y (both
+// forms) and x^(2^9) against the one-lane arithmetic; out[row] = mismatch bits
+__global__ void k_check(const uint32_t* in, uint32_t* out, int rows) {
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int rr = row < rows ? row : rows - 1;
+  fe x, y;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    x.v[i] = in[8 * rr + i];
+    y.v[i] = in[8 * ((rr + 1) % rows) + i];
+  }
+  const uint32_t xr = fw::from_fe(x), yr = fw::from_fe(y);
+  fe s_ref, m_ref, p_ref, got;
+  fe_sq(s_ref, x);
+  fe_canon(s_ref, s_ref);
+  fe_mul(m_ref, x, y);
+  fe_canon(m_ref, m_ref);
+  p_ref = x;
+  fe_sqn(p_ref, p_ref, 9);
+  fe_canon(p_ref, p_ref);
+  uint32_t bad = 0;
+  const uint32_t res[10] = {mul_v4(xr, xr),  mul_v4(xr, yr),     mul_v2(xr, xr), mul_v2(xr, yr),
+                            fw::sqn<9>(xr),  fw::add(xr, yr),    fw::mul(xr, xr), fw::mul(xr, yr),
+                            mul_v5(xr, xr),  mul_v5(xr, yr)};
+  fe a_ref;
+  fe_add(a_ref, x, y);
+  fe_canon(a_ref, a_ref);
+  const fe* refs[10] = {&s_ref, &m_ref, &s_ref, &m_ref, &p_ref, &a_ref, &s_ref, &m_ref, &s_ref, &m_ref};
+#pragma unroll
+  for (int t = 0; t < 10; t++) {
+    fw::to_fe(got, res[t]);
+    fe_canon(got, got);
+    for (int i = 0; i < 8; i++) bad |= (got.v[i] != refs[t]->v[i]) << t;
+  }
+  if ((threadIdx.x & 15) == 0 && row < rows) out[row] = bad;
+}
+
+int main() {
+  uint32_t h[3][8] = {{0x12345678, 0x9abcdef0, 0x0fedcba9, 0x87654321, 0x11111111, 0x22222222, 0x33333333, 0x04444444},
+                      {0xffffffec, 0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff, 0x7fffffff},
+                      {0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff}};
+  uint32_t *din, *dout;
+  long long* dc;
+  const int rows = 16 * 4 * 64;  // 64 blocks of 4 waves
+  if (hipMalloc(&din, rows * 32) || hipMalloc(&dout, rows * 4) || hipMalloc(&dc, 64)) return 1;
+  int rc = 0;
+  for (int v = 0; v < 3; v++) {
+    (void)hipMemcpy(din, h[v], 32, hipMemcpyHostToDevice);
+    for (int rep = 0; rep < 3; rep++) {
+      hipLaunchKernelGGL(k_time, dim3(1), dim3(64), 0, 0, din, dout, dc);
+      long long c[4];
+      uint32_t bad = 0;
+      (void)hipMemcpy(c, dc, 32, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(&bad, dout, 4, hipMemcpyDeviceToHost);
+      printf("input %d: cycles per row squaring: v2 %.1f  v3 %.1f  v4 %.1f  v5 %.1f  mismatch mask %u\n", v,
+             c[0] / 100.0, c[1] / 100.0, c[2] / 100.0, c[3] / 100.0, bad);
+      rc |= bad != 0;
+    }
+  }
+  // correctness sweep: random limbs, all-ones / all-zero limb mixes, p-ish values
+  uint32_t* hv = (uint32_t*)malloc(rows * 32);
+  srand(12345);
+  for (int r = 0; r < rows; r++)
+    for (int i = 0; i < 8; i++) {
+      uint32_t w = ((uint32_t)rand() << 16) ^ (uint32_t)rand();
+      switch (r % 8) {
+        case 1: w = 0xffffffffu; break;
+        case 2: w = (rand() & 1) ? 0xffffffffu : 0u; break;
+        case 3: w = i == 0 ? 0xffffffedu - (uint32_t)(rand() & 3) : (i == 7 ? 0x7fffffffu : 0xffffffffu); break;
+        case 4: w = (rand() & 3) ? 0xffffffffu : w; break;
+        default: break;
+      }
+      hv[8 * r + i] = w;
+    }
+  (void)hipMemcpy(din, hv, rows * 32, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_check, dim3(rows * 16 / 256), dim3(256), 0, 0, din, dout, rows);
+  uint32_t* ho = (uint32_t*)malloc(rows * 4);
+  (void)hipMemcpy(ho, dout, rows * 4, hipMemcpyDeviceToHost);
+  int nbad = 0;
+  uint32_t orbad = 0;
+  for (int r = 0; r < rows; r++) {
+    nbad += ho[r] != 0;
+    orbad |= ho[r];
+  }
+  printf("check: %d rows, %d mismatching (bits %#x: 1 sq v4, 2 mul v4, 4 sq v2, 8 mul v2, 16 sqn9, 32 add, 64 sq v3, 128 mul v3, 256 sq v5, 512 mul v5)\n", rows,
+         nbad, orbad);
+  rc |= nbad != 0;
+  return rc;
+}

@@ -83,13 +83,60 @@ COA_DEV uint64_t four_p() {
   return r == 0 ? 0x1ffffffb4ull : (r < 8 ? 0x1fffffffeull : 0ull);
 }
 
+// Per-lane constants of the asm forms below (loop-invariant, kept in
+// registers by the compiler).
+COA_DEV uint32_t lanes_lo8() { return row_lane() < 8 ? 0xffffffffu : 0u; }
+COA_DEV uint32_t k38_lane0() { return row_lane() == 0 ? 38u : 0u; }
+
+// wrap_step as one asm statement whose adds read their shifted and broadcast
+// operands through DPP themselves (VOP2 DPP), instead of separate DPP moves,
+// lane-index compares and selects: lanes 0..7 get lo + hi_{c-1} (lane 0:
+// lo + 38 * hi_7) and the carry in hi; bank_mask 0x3 leaves lanes 8..15
+// (which must hold 0) unwritten.  The leading s_nop covers the DPP read of
+// `hi`, which the compiler's hazard check cannot see inside the statement.
+COA_DEV void wrap_dpp(uint32_t& lo, uint32_t& hi) {
+  uint32_t t;
+  asm("s_nop 1\n\t"
+      "v_mul_u32_u24_dpp %[t], %[hi], %[k] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_co_u32_dpp %[lo], vcc, %[hi], %[lo] row_shr:1 row_mask:0xf bank_mask:0x3 bound_ctrl:1\n\t"
+      "v_addc_co_u32_dpp %[hi], vcc, %[z], %[z], vcc quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t"
+      "v_add_co_u32_e32 %[lo], vcc, %[t], %[lo]\n\t"
+      "v_addc_co_u32_e32 %[hi], vcc, 0, %[hi], vcc"
+      : [lo] "+v"(lo), [hi] "+v"(hi), [t] "=&v"(t)
+      : [k] "v"(k38_lane0()), [z] "v"(0u)
+      : "vcc");
+}
+// normalize with the first pass as wrap_dpp (lanes 8..15 of m must be 0).
+COA_DEV uint32_t normalize_dpp(uint64_t m) {
+  uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+  wrap_dpp(lo, hi);
+  if (__builtin_expect(__any(hi != 0u), 0)) {
+    const uint32_t r = row_lane();
+    uint64_t v = ((uint64_t)hi << 32) | lo;
+#pragma unroll 1
+    do wrap_step(v, r);
+    while (__any((uint32_t)(v >> 32) != 0u));
+    lo = (uint32_t)v;
+  }
+  return lo;
+}
+
 // a + b and a - b mod p (not canonical).  The difference adds 4p in
 // unnormalised limbs (limb 0: 2^33 - 76, limbs 1..7: 2^33 - 2), so no lane
 // goes negative.
-COA_DEV uint32_t add(uint32_t a, uint32_t b) { return normalize((uint64_t)a + b); }
-COA_DEV uint32_t sub(uint32_t a, uint32_t b) { return normalize((uint64_t)a + four_p() - b); }
+COA_DEV uint32_t add(uint32_t a, uint32_t b) { return normalize_dpp((uint64_t)a + b); }
+COA_DEV uint32_t sub(uint32_t a, uint32_t b) { return normalize_dpp((uint64_t)a + four_p() - b); }
 
-// a * b mod p (not canonical), one product per 16-lane row.
+// a * b mod p (not canonical), one product per 16-lane row.  Round 3: the
+// round-2 steps with fewer instructions on the chain: the column sums
+// start from the first product (no zeroed accumulator, the first carry word
+// from the second product's carry), the spread of each column's upper words
+// is two VOP2 adds that read them through DPP, lanes 8..15 are cleared by a
+// mask instead of a lane compare and selects, and the wrap pass is wrap_dpp.
+// tools/ubench_rows3.hip (one wave, dependent squarings): 283-290 -> 259-265
+// cycles per squaring against the round-2 form; forms with the whole tail in
+// one statement (272) or the operand moves interleaved with the
+// multiply-accumulates (265-272) measured slower and are kept there only.
 COA_DEV uint32_t mul(uint32_t a, uint32_t b) {
   uint32_t bk[8], ak[8];
   bk[0] = bcast<0>(b);
@@ -108,14 +155,11 @@ COA_DEV uint32_t mul(uint32_t a, uint32_t b) {
   ak[5] = shr<5>(a);
   ak[6] = shr<6>(a);
   ak[7] = shr<7>(a);
-  // the whole column in one asm statement (hipcc pads each statement with an
-  // s_nop before the next VALU that reads its outputs)
-  uint64_t acc = 0;
-  uint32_t c2 = 0;
-  asm("v_mad_u64_u32 %0, vcc, %2, %10, %0\n\t"
-      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+  uint64_t acc;
+  uint32_t c2;
+  asm("v_mad_u64_u32 %0, vcc, %2, %10, 0\n\t"
       "v_mad_u64_u32 %0, vcc, %3, %11, %0\n\t"
-      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_addc_co_u32_e64 %1, vcc, 0, 0, vcc\n\t"
       "v_mad_u64_u32 %0, vcc, %4, %12, %0\n\t"
       "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
       "v_mad_u64_u32 %0, vcc, %5, %13, %0\n\t"
@@ -128,19 +172,29 @@ COA_DEV uint32_t mul(uint32_t a, uint32_t b) {
       "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
       "v_mad_u64_u32 %0, vcc, %9, %17, %0\n\t"
       "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
-      : "+v"(acc), "+v"(c2)
+      : "=&v"(acc), "=&v"(c2)
       : "v"(ak[0]), "v"(ak[1]), "v"(ak[2]), "v"(ak[3]), "v"(ak[4]), "v"(ak[5]), "v"(ak[6]), "v"(ak[7]), "v"(bk[0]),
         "v"(bk[1]), "v"(bk[2]), "v"(bk[3]), "v"(bk[4]), "v"(bk[5]), "v"(bk[6]), "v"(bk[7])
       : "vcc");
-  // column c = w0 + 2^32 w1 + 2^64 w2: spread w1 to lane c+1, w2 to c+2
-  // (n_c < 2^34), fold n_{c+8} by 38 into lane c (< 2^40), then the wrap
-  // passes of fold_carry bring every lane below 2^32
-  const uint64_t n = (uint64_t)(uint32_t)acc + shr<1>((uint32_t)(acc >> 32)) + shr<2>(c2);
-  const uint32_t r = row_lane();
-  const uint32_t up_lo = shl<8>((uint32_t)n), up_hi = shl<8>((uint32_t)(n >> 32));
-  uint64_t m = (uint64_t)up_lo * 38u + (r < 8 ? n : 0);
-  m += (uint64_t)__umul24(up_hi, 38u) << 32;  // up_hi <= 3
-  return normalize(m);
+  // n_c = w0_c + w1_{c-1} + c2_{c-2} (< 2^34) as nlo + 2^32 nhi; ml/mh = n on
+  // lanes 0..7 (0 above); ul/uh = n_{c+8} (0 past the row)
+  uint32_t nlo, nhi, ml, mh, ul, uh;
+  asm("s_nop 1\n\t"
+      "v_add_co_u32_dpp %[nlo], vcc, %[w1], %[w0] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_addc_co_u32_e64 %[nhi], vcc, 0, 0, vcc\n\t"
+      "v_add_co_u32_dpp %[nlo], vcc, %[c2], %[nlo] row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_addc_co_u32_e32 %[nhi], vcc, 0, %[nhi], vcc\n\t"
+      "v_and_b32_e32 %[ml], %[nlo], %[m8]\n\t"
+      "v_and_b32_e32 %[mh], %[nhi], %[m8]\n\t"
+      "v_mov_b32_dpp %[ul], %[nlo] row_shl:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_mov_b32_dpp %[uh], %[nhi] row_shl:8 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : [nlo] "=&v"(nlo), [nhi] "=&v"(nhi), [ml] "=&v"(ml), [mh] "=&v"(mh), [ul] "=&v"(ul), [uh] "=&v"(uh)
+      : [w0] "v"((uint32_t)acc), [w1] "v"((uint32_t)(acc >> 32)), [c2] "v"(c2), [m8] "v"(lanes_lo8())
+      : "vcc");
+  // fold n_{c+8} by 2^256 = 38 (mod p): < 2^40 on lanes 0..7, 0 above
+  uint64_t m = (uint64_t)ul * 38u + (((uint64_t)mh << 32) | ml);
+  m += (uint64_t)__umul24(uh, 38u) << 32;  // uh <= 3
+  return normalize_dpp(m);
 }
 COA_DEV uint32_t sq(uint32_t a) { return mul(a, a); }
 // a^(2^N): four squarings per loop trip (one loop branch per four: 293 ->

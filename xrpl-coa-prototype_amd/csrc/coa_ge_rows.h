@@ -43,13 +43,13 @@ COA_DEV void rows4(uint32_t q, uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_
 }
 // Sums and differences between the products stay unnormalised (64-bit lane
 // values, < 2^36): a product normalises only the two operands it picks
-// (fw::normalize), so a level costs two normalisations instead of one per
-// addition.
+// (fw::normalize_dpp), so a level costs two normalisations instead of one
+// per addition.
 COA_DEV uint64_t pick64(uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
   const uint32_t r = __lane_id() >> 4;
   return r == 0 ? a : (r == 1 ? b : (r == 2 ? c : d));
 }
-COA_DEV uint32_t nm(uint64_t v) { return fw::normalize(v); }
+COA_DEV uint32_t nm(uint64_t v) { return fw::normalize_dpp(v); }
 // 2P (p1p1, lazy) from projective P: ge_p2_dbl with its four squarings on
 // the rows
 COA_DEV void dbl(L1& r, const P2& p) {
