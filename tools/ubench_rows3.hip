@@ -6,6 +6,7 @@
 //   v4   mul_v4, the same tail in one asm statement
 //   v5   mul_v5, one statement with the DPP operand moves interleaved with
 //        the multiply-accumulates
+//   sq2  fw::sq2, the squaring's products split over a pair of rows
 // plus a correctness sweep: every row of 16 waves squares and multiplies its
 // own random value (and carry-heavy patterns) through both forms; each result
 // is compared with the one-lane fe_sq / fe_mul (canonical).
@@ -214,12 +215,107 @@ __device__ uint32_t mul_v5(uint32_t a, uint32_t b) {
 }
 
 
+// Squaring on a PAIR of rows (measured slower than fw::mul: 278 vs 259
+// cycles; the cross-row sum and its hazard pads cost what the halved
+// multiply-accumulates save).  A lone chain of squarings (the pow chains of
+// decompression and inversion) leaves three of a wave's four rows computing
+// copies; here rows 2j and 2j+1 hold the same element and split its eight
+// column products: row 2j forms k = 0..3 (a_k a_{c-k}), row 2j+1 k = 4..7
+// from two row-masked DPP copies of a (shifted up by 4 limbs for the a_{c-k}
+// side, down by 4 for the broadcasts), so each lane runs 4 multiply-
+// accumulates instead of 8.  The two rows' spread column sums (< 2^34 each)
+// are added across the pair with two v_permlane16_swap, and the fold and wrap
+// run on both rows, leaving the square on both.  The input must be the same
+// on rows 2j and 2j+1 (pair_bcast makes it so).
+__device__ uint32_t pair_bcast(uint32_t x) {  // rows (0 1 2 3) <- (r0 r0 r2 r2)
+  return __builtin_amdgcn_permlane16_swap(x, x, false, false)[0];
+}
+__device__ uint32_t sq2(uint32_t x) {
+  // odd rows: A lane c = a_{c-4} (0 below), B lane k = a_{k+4}; even rows: a
+  const uint32_t A = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x114, 0xA, 0xF, true);
+  const uint32_t B = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x104, 0xA, 0xF, true);
+  const uint32_t b0 = fw::bcast<0>(B), b1 = fw::bcast<1>(B), b2 = fw::bcast<2>(B), b3 = fw::bcast<3>(B);
+  const uint32_t a1 = fw::shr<1>(A), a2 = fw::shr<2>(A), a3 = fw::shr<3>(A);
+  uint64_t acc;
+  uint32_t c2;
+  asm("v_mad_u64_u32 %0, vcc, %2, %6, 0\n\t"
+      "v_mad_u64_u32 %0, vcc, %3, %7, %0\n\t"
+      "v_addc_co_u32_e64 %1, vcc, 0, 0, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %4, %8, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %5, %9, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "=&v"(acc), "=&v"(c2)
+      : "v"(A), "v"(a1), "v"(a2), "v"(a3), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+      : "vcc");
+  // this row's half of n_c = w0_c + w1_{c-1} + c2_{c-2} (< 2^34)
+  uint32_t nlo, nhi;
+  asm("s_nop 1\n\t"
+      "v_add_co_u32_dpp %[nlo], vcc, %[w1], %[w0] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_addc_co_u32_e64 %[nhi], vcc, 0, 0, vcc\n\t"
+      "v_add_co_u32_dpp %[nlo], vcc, %[c2], %[nlo] row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_addc_co_u32_e32 %[nhi], vcc, 0, %[nhi], vcc"
+      : [nlo] "=&v"(nlo), [nhi] "=&v"(nhi)
+      : [w0] "v"((uint32_t)acc), [w1] "v"((uint32_t)(acc >> 32)), [c2] "v"(c2)
+      : "vcc");
+  // the pair's sum (< 2^35) on both rows
+  const auto pl = __builtin_amdgcn_permlane16_swap(nlo, nlo, false, false);
+  const auto ph = __builtin_amdgcn_permlane16_swap(nhi, nhi, false, false);
+  const uint64_t n = (uint64_t)pl[0] + pl[1] + ((uint64_t)(ph[0] + ph[1]) << 32);
+  const uint32_t tl = (uint32_t)n, th = (uint32_t)(n >> 32), m8 = fw::lanes_lo8();
+  const uint32_t ul = fw::shl<8>(tl), uh = fw::shl<8>(th);
+  // fold n_{c+8} by 38: < 2^39 on lanes 0..7, 0 above
+  uint64_t m = (uint64_t)ul * 38u + (((uint64_t)(th & m8) << 32) | (tl & m8));
+  m += (uint64_t)__umul24(uh, 38u) << 32;  // uh < 8
+  return fw::normalize_dpp(m);
+}
+template <int N>
+__device__ uint32_t sqn2(uint32_t a) {
+#pragma unroll 1
+  for (int i = 0; i < N / 4; i++) {
+    a = sq2(a);
+    a = sq2(a);
+    a = sq2(a);
+    a = sq2(a);
+  }
+#pragma unroll
+  for (int i = 0; i < N % 4; i++) a = sq2(a);
+  return a;
+}
+// pow_chain with the squarings on row pairs; the result of rows 2j and 2j+1
+// is the power of row 2j's input
+__device__ uint32_t pow_chain2(uint32_t& z11, uint32_t z) {
+  z = pair_bcast(z);
+  const uint32_t z2 = sq2(z);
+  const uint32_t z9 = fw::mul(sqn2<2>(z2), z);
+  z11 = fw::mul(z9, z2);
+  const uint32_t z_5_0 = fw::mul(sq2(z11), z9);
+  const uint32_t z_10_0 = fw::mul(sqn2<5>(z_5_0), z_5_0);
+  const uint32_t z_20_0 = fw::mul(sqn2<10>(z_10_0), z_10_0);
+  const uint32_t z_40_0 = fw::mul(sqn2<20>(z_20_0), z_20_0);
+  const uint32_t z_50_0 = fw::mul(sqn2<10>(z_40_0), z_10_0);
+  const uint32_t z_100_0 = fw::mul(sqn2<50>(z_50_0), z_50_0);
+  const uint32_t z_200_0 = fw::mul(sqn2<100>(z_100_0), z_100_0);
+  return fw::mul(sqn2<50>(z_200_0), z_50_0);  // 2^250 - 1
+}
+__device__ uint32_t pow_p58_2(uint32_t z) {
+  uint32_t z11;
+  const uint32_t t = pow_chain2(z11, z);
+  return fw::mul(sqn2<2>(t), pair_bcast(z));
+}
+__device__ uint32_t invert_2(uint32_t z) {
+  uint32_t z11;
+  const uint32_t t = pow_chain2(z11, z);
+  return fw::mul(sqn2<5>(t), z11);
+}
+
+
 template <int V>
 __device__ uint32_t sqn4(uint32_t a, int n) {
 #pragma unroll 1
   for (int i = 0; i < n; i += 4) {
 #pragma unroll
-    for (int j = 0; j < 4; j++) a = V == 5 ? mul_v5(a, a) : (V == 4 ? mul_v4(a, a) : (V == 3 ? fw::mul(a, a) : mul_v2(a, a)));
+    for (int j = 0; j < 4; j++) a = V == 6 ? sq2(a) : V == 5 ? mul_v5(a, a) : (V == 4 ? mul_v4(a, a) : (V == 3 ? fw::mul(a, a) : mul_v2(a, a)));
   }
   return a;
 }
@@ -238,7 +334,9 @@ __global__ void k_time(const uint32_t* in, uint32_t* out, long long* cyc) {
   long long t3 = clock64();
   const uint32_t d = sqn4<5>(x0, 100);
   long long t4 = clock64();
-  fe y = z, ref, ya, yb, yc, yd;
+  const uint32_t e2 = sqn4<6>(x0, 100);
+  long long t5 = clock64();
+  fe y = z, ref, ya, yb, yc, yd, ye;
   fe_sqn(y, y, 100);
   fe_canon(ref, y);
   fw::to_fe(ya, a);
@@ -249,16 +347,19 @@ __global__ void k_time(const uint32_t* in, uint32_t* out, long long* cyc) {
   fe_canon(yc, yc);
   fw::to_fe(yd, d);
   fe_canon(yd, yd);
+  fw::to_fe(ye, e2);
+  fe_canon(ye, ye);
   uint32_t bad = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++)
-    bad |= (ya.v[i] != ref.v[i]) | ((yb.v[i] != ref.v[i]) << 1) | ((yc.v[i] != ref.v[i]) << 2) | ((yd.v[i] != ref.v[i]) << 3);
+    bad |= (ya.v[i] != ref.v[i]) | ((yb.v[i] != ref.v[i]) << 1) | ((yc.v[i] != ref.v[i]) << 2) | ((yd.v[i] != ref.v[i]) << 3) | ((ye.v[i] != ref.v[i]) << 4);
   if (threadIdx.x == 0) {
     out[0] = bad;
     cyc[0] = t1 - t0;
     cyc[1] = t2 - t1;
     cyc[2] = t3 - t2;
     cyc[3] = t4 - t3;
+    cyc[4] = t5 - t4;
   }
 }
 
@@ -286,6 +387,26 @@ __global__ void k_check(const uint32_t* in, uint32_t* out, int rows) {
   const uint32_t res[10] = {mul_v4(xr, xr),  mul_v4(xr, yr),     mul_v2(xr, xr), mul_v2(xr, yr),
                             fw::sqn<9>(xr),  fw::add(xr, yr),    fw::mul(xr, xr), fw::mul(xr, yr),
                             mul_v5(xr, xr),  mul_v5(xr, yr)};
+  // pair forms: rows 2j and 2j+1 compute from row 2j's value
+  const int re = rr & ~1;
+  fe xe;
+#pragma unroll
+  for (int i = 0; i < 8; i++) xe.v[i] = in[8 * re + i];
+  fe se_ref, pe_ref, ie_ref;
+  fe_sq(se_ref, xe);
+  fe_canon(se_ref, se_ref);
+  fe_pow_p58(pe_ref, xe);
+  fe_canon(pe_ref, pe_ref);
+  fe_invert(ie_ref, xe);
+  fe_canon(ie_ref, ie_ref);
+  const uint32_t pres[3] = {sq2(pair_bcast(xr)), pow_p58_2(xr), invert_2(xr)};
+  const fe* prefs[3] = {&se_ref, &pe_ref, &ie_ref};
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    fw::to_fe(got, pres[t]);
+    fe_canon(got, got);
+    for (int i = 0; i < 8; i++) bad |= (got.v[i] != prefs[t]->v[i]) << (10 + t);
+  }
   fe a_ref;
   fe_add(a_ref, x, y);
   fe_canon(a_ref, a_ref);
@@ -312,12 +433,12 @@ int main() {
     (void)hipMemcpy(din, h[v], 32, hipMemcpyHostToDevice);
     for (int rep = 0; rep < 3; rep++) {
       hipLaunchKernelGGL(k_time, dim3(1), dim3(64), 0, 0, din, dout, dc);
-      long long c[4];
+      long long c[5];
       uint32_t bad = 0;
-      (void)hipMemcpy(c, dc, 32, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(c, dc, 40, hipMemcpyDeviceToHost);
       (void)hipMemcpy(&bad, dout, 4, hipMemcpyDeviceToHost);
-      printf("input %d: cycles per row squaring: v2 %.1f  v3 %.1f  v4 %.1f  v5 %.1f  mismatch mask %u\n", v,
-             c[0] / 100.0, c[1] / 100.0, c[2] / 100.0, c[3] / 100.0, bad);
+      printf("input %d: cycles per row squaring: v2 %.1f  v3 %.1f  v4 %.1f  v5 %.1f  sq2 %.1f  mismatch mask %u\n", v,
+             c[0] / 100.0, c[1] / 100.0, c[2] / 100.0, c[3] / 100.0, c[4] / 100.0, bad);
       rc |= bad != 0;
     }
   }
@@ -346,7 +467,7 @@ int main() {
     nbad += ho[r] != 0;
     orbad |= ho[r];
   }
-  printf("check: %d rows, %d mismatching (bits %#x: 1 sq v4, 2 mul v4, 4 sq v2, 8 mul v2, 16 sqn9, 32 add, 64 sq v3, 128 mul v3, 256 sq v5, 512 mul v5)\n", rows,
+  printf("check: %d rows, %d mismatching (bits %#x: 1 sq v4, 2 mul v4, 4 sq v2, 8 mul v2, 16 sqn9, 32 add, 64 sq v3, 128 mul v3, 256 sq v5, 512 mul v5, 1024 sq2, 2048 pow_p58_2, 4096 invert_2)\n", rows,
          nbad, orbad);
   rc |= nbad != 0;
   return rc;
