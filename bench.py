@@ -1165,31 +1165,36 @@ def main():
         del ws
         torch.cuda.empty_cache()
         want = set(x for x in args.sections.split(",") if x)
-        on = lambda name: not want or name in want  # noqa: E731
         secondary = {}
-        if on("verify_single"):
-            secondary["verify_single"] = verify_single(local, cpu["single_verify_p50_ms"] if cpu else None)
-        if on("c5_shard"):
-            secondary["c5_shard"] = c5_shard(local, dev, stream)
-        if on("c2_inflight"):
-            secondary["c2_inflight"] = c2_inflight(local, dev)
-        if on("verify_batch"):
-            secondary["verify_batch"] = verify_batch_config(local, dev, stream)
-        if on("c4_sha512"):
-            secondary["c4_sha512"] = c4_sha512(local, dev, stream, [int(x) for x in args.c4_batches.split(",") if x],
-                                               2, threads)
-        if on("c3_certificate_verify"):
-            secondary["c3_certificate_verify"] = certificate_config(args.c3_certs, 1000, threads, dev, stream,
-                                                                    cpu_thread_seconds=args.cpu_thread_seconds)
-        if on("c1_certificate_verify"):
-            secondary["c1_certificate_verify"] = certificate_config(2000, 1000, threads, dev, stream,
+
+        def section(name, fn):
+            """Run one secondary measurement; a failure is recorded in the
+            line (and its traceback on stderr) instead of losing the
+            headline."""
+            if want and name not in want:
+                return
+            try:
+                secondary[name] = fn()
+            except Exception as e:  # noqa: BLE001 -- reported, not hidden
+                import traceback
+
+                traceback.print_exc(file=sys.stderr)
+                secondary[name] = {"error": f"{type(e).__name__}: {e}"}
+
+        section("verify_single", lambda: verify_single(local, cpu["single_verify_p50_ms"] if cpu else None))
+        section("c5_shard", lambda: c5_shard(local, dev, stream))
+        section("c2_inflight", lambda: c2_inflight(local, dev))
+        section("verify_batch", lambda: verify_batch_config(local, dev, stream))
+        section("c4_sha512", lambda: c4_sha512(local, dev, stream, [int(x) for x in args.c4_batches.split(",") if x],
+                                               2, threads))
+        section("c3_certificate_verify", lambda: certificate_config(args.c3_certs, 1000, threads, dev, stream,
+                                                                    cpu_thread_seconds=args.cpu_thread_seconds))
+        section("c1_certificate_verify", lambda: certificate_config(2000, 1000, threads, dev, stream,
                                                                     committee_size=4, n_payload=1,
-                                                                    cpu_thread_seconds=args.cpu_thread_seconds)
-        if on("c4_stream"):
-            c4 = secondary.get("c4_sha512", {})
-            secondary["c4_stream"] = c4_stream(c4.get("single_batch", {}).get("cpu_one_core_p50_ms"))
-        if on("queue_round_mix"):
-            secondary["queue_round_mix"] = queue_round_mix()
+                                                                    cpu_thread_seconds=args.cpu_thread_seconds))
+        section("c4_stream", lambda: c4_stream(secondary.get("c4_sha512", {}).get("single_batch", {})
+                                               .get("cpu_one_core_p50_ms")))
+        section("queue_round_mix", queue_round_mix)
 
     if rank == 0:
         line = {
