@@ -299,13 +299,15 @@ def world(engine):
     return World(engine)
 
 
-@pytest.fixture(params=["64", "64/staged", "1/T0", "1/T256", "1/T512", "1/T0/narrow"])
+@pytest.fixture(params=["64", "64/staged", "1/T0", "1/T256", "1/T512", "1/T0/narrow", "1/T0/kw16"])
 def lanes(request):
     """Latency kernel (64) and throughput kernel with one signature per lane
     (T0 = default grid) or a grid of 256 / 512 lanes, so each lane shares one
     inversion among several signatures (P compared with R's encoding).
     `narrow`: [s]B and [k](-A) from the radix-256 combs instead of the wide
-    HBM comb of B and the keys' wide combs.  `staged`: one-certificate calls
+    HBM comb of B and the keys' wide combs.  `kw16`: the keys' radix-2^16
+    wide combs (48 MiB per key) instead of the default radix-2^20 ones (654 MB
+    per key; COA_KEY_WCOMB20_MB=0 at registration).  `staged`: one-certificate calls
     through the pinned staging copy instead of the kernel arguments
     (COA_CERT_INLINE=0; certificates over 2,816 bytes take it anyway)."""
     parts = request.param.split("/")
@@ -317,12 +319,15 @@ def lanes(request):
     if "narrow" in parts:
         os.environ["COA_WCOMB"] = "0"
         os.environ["COA_KEY_WCOMB"] = "0"
+    if "kw16" in parts:
+        os.environ["COA_KEY_WCOMB20_MB"] = "0"
     yield int(parts[0])
     del os.environ["COA_CERT_LANES"]
     os.environ.pop("COA_CERT_INLINE", None)
     os.environ.pop("COA_CERT_LANES_TOTAL", None)
     os.environ.pop("COA_WCOMB", None)
     os.environ.pop("COA_KEY_WCOMB", None)
+    os.environ.pop("COA_KEY_WCOMB20_MB", None)
 
 
 def test_fused_certificates_adversarial(engine, world, lanes):

@@ -16,6 +16,15 @@
 #define COA_KWCOMB_POS 16
 #define COA_KWCOMB_ENTRIES ((uint64_t)COA_KWCOMB_POS << (COA_KWCOMB_W - 1))
 #define COA_KWCOMB_DWORDS (COA_KWCOMB_ENTRIES * 24)
+// the widest per-key comb: 13 positions x 2^19 multiples, entry (j, m-1) =
+// m * 2^(20 j) * (-A), exact integer multiples: 654 MB per key (the layout
+// of B's wide comb, coa_halved.h), 13 additions for [k](-A) instead of 16;
+// built when the committee fits the COA_KEY_WCOMB20_MB budget (shared by the
+// contexts open on a device), else the 48 MiB combs above
+#define COA_KWCOMB20_W 20
+#define COA_KWCOMB20_POS 13
+#define COA_KWCOMB20_ENTRIES ((uint64_t)COA_KWCOMB20_POS << (COA_KWCOMB20_W - 1))
+#define COA_KWCOMB20_DWORDS (COA_KWCOMB20_ENTRIES * 24)
 
 // key flag bits (k_key_flags)
 #define COA_KEY_DECOMPRESSES 1u   // CompressedEdwardsY::decompress succeeds
@@ -46,6 +55,7 @@ struct CertArgs {
   const uint32_t* kflags;       // [nk]
   const uint32_t* ktabs;        // [nk][COA_KEY_TAB_DWORDS] comb of -A per key
   const uint32_t* kwtabs;       // [nk][COA_KWCOMB_DWORDS] wide comb of -A per key, or null
+  uint32_t kw20;                // 1: kwtabs is [nk][COA_KWCOMB20_DWORDS] (radix 2^20)
   uint32_t nk;
   const uint32_t* comb;         // B comb (coa_halved.h)
   const uint32_t* wcomb;        // wide B comb (coa_smul.h) or null
@@ -88,6 +98,7 @@ hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* fla
 hipError_t coa_launch_key_tables(const uint32_t* keys, uint32_t nk, uint32_t* tabs, hipStream_t s);
 // wide combs from the radix-256 key combs (tabs already built)
 hipError_t coa_launch_key_wcombs(const uint32_t* tabs, uint32_t nk, uint32_t* wtabs, hipStream_t s);
+hipError_t coa_launch_key_wcombs20(const uint32_t* tabs, uint32_t nk, uint32_t* wtabs, hipStream_t s);
 // lanes_per_sig: 64 (latency: two waves per signature, comb terms split over
 // a wave's lanes and summed by a butterfly) or 1 (throughput: K signatures
 // per lane, K from the job count).

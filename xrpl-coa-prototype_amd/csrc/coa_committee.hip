@@ -222,8 +222,8 @@ COA_DEV void job_comb(const CertArgs& a, uint32_t job, ge_p3& P, uint32_t& pre, 
   ge_p1p1 t;
   // [s]B: 13 additions from the wide HBM comb when it is built, else the 32
   // byte terms of the radix-256 comb (an s >= l only reaches Err verdicts);
-  // [k](-A): 16 additions from the key's wide comb when the committee has
-  // them, else its 32 radix-256 terms
+  // [k](-A): 13 or 16 additions from the key's wide comb (radix 2^20 or
+  // 2^16) when the committee has them, else its 32 radix-256 terms
   if (a.wcomb) {
     wcomb_accumulate(P, sw, a.wcomb);
   } else {
@@ -235,7 +235,9 @@ COA_DEV void job_comb(const CertArgs& a, uint32_t job, ge_p3& P, uint32_t& pre, 
       ge_p1p1_to_p3(P, t);
     }
   }
-  if (a.kwtabs) {
+  if (a.kwtabs && a.kw20) {
+    wc_accumulate<COA_KWCOMB20_W, COA_KWCOMB20_POS>(P, k.v, a.kwtabs + (uint64_t)slot * COA_KWCOMB20_DWORDS);
+  } else if (a.kwtabs) {
     wc_accumulate<COA_KWCOMB_W, COA_KWCOMB_POS>(P, k.v, a.kwtabs + (uint64_t)slot * COA_KWCOMB_DWORDS);
   } else {
 #pragma unroll 1
@@ -757,6 +759,58 @@ __global__ void __launch_bounds__(256) k_key_wcomb(const uint32_t* __restrict__ 
   ge_madd(t, P, q);
   ge_p1p1_to_p3(P, t);
   store_niels(wtabs + (uint64_t)key * COA_KWCOMB_DWORDS + (uint64_t)e * 24, P);
+}
+
+// Widest comb entry (key, j, m-1) = m * 2^(20 j) * (-A): 20 j = 8 q + r, and
+// m 2^r < 2^24 is recoded into signed bytes b0, b1, b2, so the entry is the
+// sum of the exact radix-256 comb entries (q, b0), (q+1, b1), (q+2, b2) -- an
+// integer multiple, torsion kept -- made affine.  At j = 12 (q = 30) a byte
+// at position 32 would be needed only for m > 2^16, which no scalar below l
+// produces (its top digit is at most 2^13, wc_recode): those entries are
+// never read and hold the sum of the first two bytes.
+__global__ void __launch_bounds__(256) k_key_wcomb20(const uint32_t* __restrict__ tabs, uint32_t nk,
+                                                     uint32_t* __restrict__ wtabs) {
+  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t key = (uint32_t)(id / COA_KWCOMB20_ENTRIES);
+  if (key >= nk) return;
+  const uint64_t e = id % COA_KWCOMB20_ENTRIES;
+  const int j = (int)(e >> (COA_KWCOMB20_W - 1));
+  const uint32_t m = (uint32_t)(e & ((1u << (COA_KWCOMB20_W - 1)) - 1)) + 1;
+  const int bit = COA_KWCOMB20_W * j, q = bit >> 3;
+  uint32_t v = m << (bit & 7);
+  int b[3];
+  int carry = 0;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    int x = (int)(v & 255u) + carry;
+    v >>= 8;
+    carry = 0;
+    if (i < 2 && x >= 128) {
+      x -= 256;
+      carry = 1;
+    }
+    b[i] = x;
+  }
+  const uint32_t* ktab = tabs + (uint64_t)key * COA_KEY_TAB_DWORDS;
+  ge_p3 P;
+  ge_p3_identity(P);
+  ge_p1p1 t;
+  ge_niels qn;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    if (q + i > 31) break;
+    comb_select(qn, ktab, q + i, b[i]);
+    ge_madd(t, P, qn);
+    ge_p1p1_to_p3(P, t);
+  }
+  store_niels(wtabs + (uint64_t)key * COA_KWCOMB20_DWORDS + e * 24, P);
+}
+
+hipError_t coa_launch_key_wcombs20(const uint32_t* tabs, uint32_t nk, uint32_t* wtabs, hipStream_t s) {
+  if (nk == 0) return hipSuccess;
+  const uint64_t total = (uint64_t)nk * COA_KWCOMB20_ENTRIES;
+  hipLaunchKernelGGL(k_key_wcomb20, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, tabs, nk, wtabs);
+  return hipGetLastError();
 }
 
 hipError_t coa_launch_key_wcombs(const uint32_t* tabs, uint32_t nk, uint32_t* wtabs, hipStream_t s) {

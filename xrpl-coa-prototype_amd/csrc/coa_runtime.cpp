@@ -177,6 +177,7 @@ struct Dev {
   uint32_t lat_tag = 0;
   uint32_t* lat_ctr = nullptr;  // device block counter of k_cert_verify_lat (0 between calls)
   bool kwide = false;  // kwtabs holds the committee's wide combs
+  bool kw20 = false;   // ... in the radix-2^20 layout (COA_KWCOMB20_*)
   uint32_t nkeys = 0;
   PinBuf pin;
   std::mutex mu;
@@ -204,6 +205,14 @@ const uint32_t* wcomb_of(const Dev& d) { return env_is("COA_WCOMB", "0") ? nullp
 double key_wcomb_budget() {
   const char* v = getenv("COA_KEY_WCOMB_MB");
   return (v ? atof(v) : 16384.0) * 1048576.0;
+}
+// Bytes of HBM the radix-2^20 key combs (654 MB per key) may take on one
+// device, shared by the contexts open on it (COA_KEY_WCOMB20_MB, default
+// 128 GiB of the MI355X's 288 GB: committees up to ~210 keys on one context;
+// 0 disables them).
+double key_wcomb20_budget() {
+  const char* v = getenv("COA_KEY_WCOMB20_MB");
+  return (v ? atof(v) : 131072.0) * 1048576.0;
 }
 // COA_VERIFY_WAVES=3 selects the 168-VGPR instance of k_verify_halved.
 int verify_waves() {
@@ -985,6 +994,7 @@ CertArgs cert_args(Dev& d, uint8_t* base, const CertPack& p, size_t nc, size_t n
   a.comb = d.comb;
   a.wcomb = wcomb_of(d);
   a.kwtabs = (d.kwide && !env_is("COA_KEY_WCOMB", "0")) ? d.kwtabs.as<uint32_t>() : nullptr;
+  a.kw20 = d.kw20 ? 1u : 0u;
   a.status = reinterpret_cast<uint32_t*>(base + p.status);
   return a;
 }
@@ -1607,10 +1617,26 @@ int coa_committee_register(const uint8_t* pks, size_t n) {
       HIP_TRY(hipMemcpyAsync(d.ckeys.p, keys.data(), nk * 32, hipMemcpyHostToDevice, d.stream));
       HIP_TRY(coa_launch_key_flags(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.kflags.as<uint32_t>(), d.stream));
       HIP_TRY(coa_launch_key_tables(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.ktabs.as<uint32_t>(), d.stream));
-      // wide combs (48 MiB per key) when the committee fits the budget
-      // (speed only: without the memory the radix-256 key combs serve)
+      // wide combs when the committee fits the budget: radix 2^20 (654 MB
+      // per key, 13 additions per [k](-A)) within COA_KEY_WCOMB20_MB shared
+      // by the device's contexts, else radix 2^16 (48 MiB per key, 16
+      // additions) within COA_KEY_WCOMB_MB (speed only: without the memory
+      // the radix-256 key combs serve)
       d.kwide = false;
-      if ((double)nk * COA_KWCOMB_DWORDS * 4 <= key_wcomb_budget()) {
+      d.kw20 = false;
+      int ctx_on_dev = 0;
+      for (const auto& o : g_devs) ctx_on_dev += o->id == d.id ? 1 : 0;
+      if ((double)nk * COA_KWCOMB20_DWORDS * 4 <= key_wcomb20_budget() / std::max(1, ctx_on_dev)) {
+        if (d.kwtabs.ensure(nk * (size_t)COA_KWCOMB20_DWORDS * 4, true) == hipSuccess) {
+          HIP_TRY(coa_launch_key_wcombs20(d.ktabs.as<uint32_t>(), (uint32_t)nk, d.kwtabs.as<uint32_t>(), d.stream));
+          d.kwide = true;
+          d.kw20 = true;
+        } else {
+          d.kwtabs.release();
+          (void)hipGetLastError();
+        }
+      }
+      if (!d.kw20 && (double)nk * COA_KWCOMB_DWORDS * 4 <= key_wcomb_budget()) {
         if (d.kwtabs.ensure(nk * (size_t)COA_KWCOMB_DWORDS * 4, true) == hipSuccess) {
           HIP_TRY(coa_launch_key_wcombs(d.ktabs.as<uint32_t>(), (uint32_t)nk, d.kwtabs.as<uint32_t>(), d.stream));
           d.kwide = true;
@@ -1618,9 +1644,8 @@ int coa_committee_register(const uint8_t* pks, size_t n) {
           d.kwtabs.release();
           (void)hipGetLastError();
         }
-      } else {
-        d.kwtabs.release();  // a smaller committee's tables are not kept
       }
+      if (!d.kwide) d.kwtabs.release();  // a previous committee's tables are not kept
       HIP_TRY(hipStreamSynchronize(d.stream));
       d.nkeys = (uint32_t)nk;
       return COA_OK;
@@ -1759,6 +1784,7 @@ int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data,
   a.comb = d->comb;
   a.wcomb = wcomb_of(*d);
   a.kwtabs = (d->kwide && !env_is("COA_KEY_WCOMB", "0")) ? d->kwtabs.as<uint32_t>() : nullptr;
+  a.kw20 = d->kw20 ? 1u : 0u;
   a.status = d_status;
   const int lanes = cert_lanes(n + n_votes);
   HIP_TRY(hipMemsetAsync(d_status, 0, n * 4, s));
