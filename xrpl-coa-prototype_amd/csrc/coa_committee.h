@@ -17,8 +17,8 @@
 #define COA_KWCOMB_ENTRIES ((uint64_t)COA_KWCOMB_POS << (COA_KWCOMB_W - 1))
 #define COA_KWCOMB_DWORDS (COA_KWCOMB_ENTRIES * 24)
 // the widest per-key comb: 13 positions x 2^19 multiples, entry (j, m-1) =
-// m * 2^(20 j) * (-A), exact integer multiples: 654 MB per key (the layout
-// of B's wide comb, coa_halved.h), 13 additions for [k](-A) instead of 16;
+// m * 2^(20 j) * (-A), exact integer multiples: 654 MB per key (B's wide
+// comb layout at W = 20), 13 additions for [k](-A) instead of 16;
 // built when the committee fits the COA_KEY_WCOMB20_MB budget (shared by the
 // contexts open on a device), else the 48 MiB combs above
 #define COA_KWCOMB20_W 20

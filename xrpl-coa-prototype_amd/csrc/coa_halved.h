@@ -5,8 +5,8 @@
 #include <stdint.h>
 
 // wide HBM comb of B (coa_smul.h): positions x magnitudes, 24 dwords each
-#define COA_WCOMB_W 20
-#define COA_WCOMB_POS 13
+#define COA_WCOMB_W 24
+#define COA_WCOMB_POS 11
 #define COA_WCOMB_MAG (1u << (COA_WCOMB_W - 1))
 #define COA_WCOMB_ENTRIES ((uint64_t)COA_WCOMB_POS * COA_WCOMB_MAG)
 #define COA_WCOMB_DWORDS (COA_WCOMB_ENTRIES * 24)

@@ -166,7 +166,7 @@ struct Dev {
   hipStream_t stream = nullptr;
   uint32_t* btab = nullptr;  // 128 x (j+1)B, radix-256 fixed-base table (12 KiB)
   uint32_t* comb = nullptr;  // 32 x 128 x (v+1)256^j B comb for k_verify_halved (384 KiB)
-  uint32_t* wcomb = nullptr;  // wide B comb, COA_WCOMB_POS x 2^(W-1) entries (654 MB at W = 20)
+  uint32_t* wcomb = nullptr;  // wide B comb, COA_WCOMB_POS x 2^(W-1) entries (8.9 GB at W = 24)
   DevBuf msgs, pks, sigs, kbuf, rec, verdicts, scratch, aux, rbuf, seeds, offs, data, out, idx, zs, terms, flags;
   // committee key cache (f2): sorted keys, flags, one comb of -A per key
   DevBuf ckeys, kflags, ktabs, kwtabs, cert, cscr;

@@ -127,8 +127,9 @@ COA_DEV void comb_select(ge_niels& q, const uint32_t* __restrict__ comb, int j, 
 // entry (j, m-1) = m * 2^(W j) * B as canonical affine Niels (24 dwords).
 // A scalar x < 2^253 is recoded as the W-bit digits of
 // x + sum_j 2^(W j + W - 1) minus 2^(W-1), so [x]B is COA_WCOMB_POS mixed
-// additions instead of the 32 of the radix-256 comb above.  W = 20: 13
-// positions, 6.8 M entries, 654 MB of the 288 GB HBM.
+// additions instead of the 32 of the radix-256 comb above.  W = 24: 11
+// positions, 92 M entries, 8.9 GB of the 288 GB HBM (round 3; W = 20, 13
+// positions and 654 MB before: C3 +3 %, C1 +3.5 %, C2 +1 % same box).
 // ---------------------------------------------------------------------------
 
 // Generic wide comb of a point P: POS positions x 2^(W-1) magnitudes,
