@@ -698,7 +698,7 @@ def queue_round_mix(rates=(5, 10, 100, 300, 1000), seconds=0.6, committee_size=1
     items[kinds == 0] = np.arange(ns)
     res = {"workload": f"committee {committee_size}: per round {committee_size} certificates "
                        f"({committee.quorum_threshold()} votes) + {ns} header/vote signatures, evenly spread",
-           "queue": {"max_batch": 65536, "max_delay_us": 200}, "rates": {}}
+           "queue": {"max_batch": 65536, "max_delay_us": 200}}
     # CPU service times (one core, the C restatement of dalek): measured
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import random
@@ -723,6 +723,29 @@ def queue_round_mix(rates=(5, 10, 100, 300, 1000), seconds=0.6, committee_size=1
     res["cpu_service_ms"] = {"certificate": round(st_cert * 1e3, 4), "signature": round(st_single * 1e3, 4),
                              "round": round((committee_size * st_cert + ns * st_single) * 1e3, 2),
                              "max_rounds_per_s": round(1.0 / (committee_size * st_cert + ns * st_single), 2)}
+    # two window policies: the deadline (a window closes when max_delay_us
+    # has passed since its oldest request, or when full), and the same with
+    # COA_QUEUE_IDLE_LAUNCH=1 (a window also closes at once while no window
+    # is in flight: a lone request on an idle device does not wait)
+    for policy, key in (("deadline", "rates"), ("idle_launch", "rates_idle_launch")):
+        if policy == "idle_launch":
+            os.environ["COA_QUEUE_IDLE_LAUNCH"] = "1"
+        try:
+            res[key] = _round_mix_rates(rates, seconds, per_round, kinds, items, msgs, pks, sigs, ns, certs,
+                                        committee_size, st_cert, st_single, res["cpu_service_ms"]["max_rounds_per_s"])
+        finally:
+            os.environ.pop("COA_QUEUE_IDLE_LAUNCH", None)
+    coa_crypto.committee_register(np.zeros((0, 32), np.uint8))
+    return res
+
+
+def _round_mix_rates(rates, seconds, per_round, kinds, items, msgs, pks, sigs, ns, certs, committee_size, st_cert,
+                     st_single, cpu_max_rounds):
+    """queue_round_mix's paced runs, one per round rate, under the window
+    policy the environment selects."""
+    import numpy as np
+
+    out = {}
     for rate in rates:
         rounds = max(3, int(rate * seconds))
         n = rounds * per_round
@@ -749,10 +772,9 @@ def queue_round_mix(rates=(5, 10, 100, 300, 1000), seconds=0.6, committee_size=1
                          "cpu_core_run_p99_ms": round(float(np.percentile(cpu_lat[sel], 99)), 3)}
         row["queue_wait_us_p50"] = round(met["wait_us_p50"], 1)
         row["queue_wait_us_p99"] = round(met["wait_us_p99"], 1)
-        row["cpu_saturated"] = bool(rate > res["cpu_service_ms"]["max_rounds_per_s"])
-        res["rates"][str(rate)] = row
-    coa_crypto.committee_register(np.zeros((0, 32), np.uint8))
-    return res
+        row["cpu_saturated"] = bool(rate > cpu_max_rounds)
+        out[str(rate)] = row
+    return out
 
 
 def certificate_config(n_certs, latency_samples, cpu_threads, dev, stream, committee_size=100, n_payload=32,

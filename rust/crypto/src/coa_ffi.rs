@@ -170,6 +170,7 @@ extern "C" {
     pub fn coa_queue_submit_digest(q: *mut CoaQueue, data: *const u8, len: usize, cb: CoaVerdictCb,
                                    user: *mut c_void) -> c_int;
     pub fn coa_queue_flush(q: *mut CoaQueue) -> c_int;
+    pub fn coa_queue_set_idle_launch(q: *mut CoaQueue, windows_in_flight: u32) -> c_int;
     pub fn coa_queue_stats(q: *mut CoaQueue, launches: *mut u64, items: *mut u64, groups: *mut u64) -> c_int;
     pub fn coa_queue_digest_count(q: *mut CoaQueue, digests: *mut u64) -> c_int;
     pub fn coa_queue_metrics(q: *mut CoaQueue, out: *mut CoaQueueMetrics) -> c_int;

@@ -179,6 +179,9 @@ int main(int argc, char** argv) {
   CHECK(coa_queue_submit_digest(q, data, 13, cb, &seen) == COA_OK, "queue_submit_digest");
   CHECK(coa_queue_submit_verify(q, msg, pk, sig, NULL, NULL) == COA_EINVAL, "queue_submit_verify(null cb)");
   CHECK(coa_queue_flush(q) == COA_OK, "queue_flush 2");
+  CHECK(coa_queue_set_idle_launch(q, 1) == COA_OK && coa_queue_set_idle_launch(q, 0) == COA_OK &&
+            coa_queue_set_idle_launch(q, 65) == COA_EINVAL && coa_queue_set_idle_launch(NULL, 1) == COA_EINVAL,
+        "queue_set_idle_launch");
   uint64_t launches = 0, items = 0, groups = 0, digests = 0;
   CHECK(coa_queue_stats(q, &launches, &items, &groups) == COA_OK && items == 2 && groups == 2, "queue_stats");
   CHECK(coa_queue_digest_count(q, &digests) == COA_OK && digests == 1, "queue_digest_count");

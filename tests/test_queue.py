@@ -186,3 +186,28 @@ def test_queue_pipelined_windows_gpu(engine):
     assert m["requests"] == len(results) and m["signatures"] == n
     assert m["windows"] > 4 and 2 <= m["max_in_flight"] <= 4  # pipelined over the slots (4 per GPU)
     assert 0 < m["wait_us_p50"] <= m["wait_us_p99"] <= m["wait_us_max"] * 1.1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["api", "env"])
+def test_queue_idle_launch_gpu(engine, monkeypatch, mode):
+    """Idle launch (coa_queue_set_idle_launch(q, 1), or COA_QUEUE_IDLE_LAUNCH=1
+    at creation): a request arriving while no window is in flight launches at
+    once instead of waiting out max_delay_us (2 s here); one request at a
+    time, each awaited before the next, answers exactly."""
+    import time
+
+    if mode == "env":
+        monkeypatch.setenv("COA_QUEUE_IDLE_LAUNCH", "1")
+    vecs = [v for v in load_golden("verify_vectors.json") if len(v["msg"]) == 64][:24]
+    with engine.AggregationQueue(max_batch=4096, max_delay_us=2_000_000) as q:
+        if mode == "api":
+            q.set_idle_launch(1)
+        t0 = time.perf_counter()
+        for v in vecs:
+            f = q.submit_verify(bytes.fromhex(v["msg"]), bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]))
+            assert f.result(timeout=30) == v["expect"]
+        el = time.perf_counter() - t0
+        m = q.metrics()
+    assert el < 2.0, el  # the deadline policy would take 24 x 2 s
+    assert m["windows"] == len(vecs)

@@ -133,6 +133,7 @@ def lib():
         "coa_queue_submit_digest": ([vp, P8, sz, VERDICT_CB, vp], ctypes.c_int),
         "coa_queue_digest_count": ([vp, P64], ctypes.c_int),
         "coa_queue_flush": ([vp], ctypes.c_int),
+        "coa_queue_set_idle_launch": ([vp, ctypes.c_uint32], ctypes.c_int),
         "coa_queue_stats": ([vp, P64, P64, P64], ctypes.c_int),
         "coa_queue_metrics": ([vp, ctypes.POINTER(QueueMetrics)], ctypes.c_int),
         "coa_queue_destroy": ([vp], ctypes.c_int),
@@ -755,6 +756,11 @@ class AggregationQueue:
         _check(lib().coa_queue_stats(self._q, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         _check(lib().coa_queue_digest_count(self._q, ctypes.byref(d)))
         return {"launches": a.value, "signatures": b.value, "batches": c.value, "digests": d.value}
+
+    def set_idle_launch(self, windows_in_flight=1):
+        """coa_queue_set_idle_launch: also close a window at once while fewer
+        than windows_in_flight windows are in flight (0 = deadline policy)."""
+        _check(lib().coa_queue_set_idle_launch(self._q, windows_in_flight))
 
     def metrics(self):
         """coa_queue_metrics: request counts per kind, window sizes, windows in

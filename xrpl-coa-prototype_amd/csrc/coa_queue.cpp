@@ -17,7 +17,11 @@
 //               first item, then every kReport items), so producers do not
 //               share a written cache line per request
 //   collector   closes the window when `max_batch` items are pending, when
-//               the oldest request is `max_delay_us` old, or on flush, takes
+//               the oldest request is `max_delay_us` old, on flush, or --
+//               with COA_QUEUE_IDLE_LAUNCH=k -- as soon as fewer than k
+//               windows are in flight (a lone request on an idle device
+//               launches at once; under load the arrivals still coalesce
+//               behind the windows in flight), takes
 //               every non-empty shard's window (a swap per shard -- the
 //               parts are never merged on the host: the backend packs them
 //               straight into its pinned staging) and hands the parts to the
@@ -239,6 +243,9 @@ struct coa_queue {
   AnswerPool helpers;  // started lazily by the first large launch
   int n_helpers = kHelpersDefault;
   bool helpers_on = false;
+  // COA_QUEUE_IDLE_LAUNCH (read at creation; 0 = off, the default): a window
+  // closes at once while fewer than this many windows are in flight
+  size_t idle_launch = 0;
 
   coa_queue() {
     for (size_t i = 0; i < kShards; i++) {
@@ -315,8 +322,10 @@ struct coa_queue {
     for (;;) {
       cv.wait(l, [&] { return stop.load() || pend.load() > 0; });
       if (stop.load() && pend.load() <= 0) break;  // stop with nothing pending
-      // window is open: close it when full, at the deadline, on flush or stop
-      while (!stop.load() && !flush && pend.load() < (int64_t)max_batch) {
+      // window is open: close it when full, at the deadline, on flush or
+      // stop, or (idle launch) while fewer than idle_launch windows are in
+      // flight -- the completer wakes the collector when one is answered
+      while (!stop.load() && !flush && pend.load() < (int64_t)max_batch && busy >= idle_launch) {
         if (cv.wait_until(l, oldest + max_delay) == std::cv_status::timeout) break;
       }
       flush = false;
@@ -449,6 +458,7 @@ struct coa_queue {
       if (rc != COA_OK) m_failed++;
       busy--;
       if (busy == 0 && pend.load() <= 0) idle_cv.notify_all();
+      if (idle_launch && busy < idle_launch && pend.load() > 0) cv.notify_one();
     }
   }
 
@@ -495,6 +505,7 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
   q->max_batch = max_batch ? max_batch : 65536;
   q->max_delay = std::chrono::microseconds(max_delay_us);
   if (const char* e = getenv("COA_QUEUE_HELPERS")) q->n_helpers = std::max(0, std::min(15, atoi(e)));
+  if (const char* e = getenv("COA_QUEUE_IDLE_LAUNCH")) q->idle_launch = (size_t)std::max(0, std::min(64, atoi(e)));
   q->be.reset(coa_q::make_backend());
   q->start();
   return q;
@@ -589,6 +600,14 @@ int coa_queue_flush(coa_queue* q) {
     q->cv.notify_one();
   }
   q->idle_cv.wait(l, [&] { return q->pend.load() <= 0 && q->busy == 0; });
+  return COA_OK;
+}
+
+int coa_queue_set_idle_launch(coa_queue* q, uint32_t windows_in_flight) {
+  if (!q || windows_in_flight > 64) return COA_EINVAL;
+  std::lock_guard<std::mutex> l(q->mu);
+  q->idle_launch = windows_in_flight;
+  q->cv.notify_one();  // an open window may close now
   return COA_OK;
 }
 
