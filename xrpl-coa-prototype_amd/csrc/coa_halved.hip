@@ -486,9 +486,26 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
                                                         const uint32_t* __restrict__ wcomb) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = i < n;
-  const bool ok = live && reinterpret_cast<const uint16_t*>(flags)[i] == 0x0101u;
-  const uint32_t* myrec = rec + (uint64_t)(live ? i : 0) * 32;
-  const uint32_t meta = live ? myrec[24] : 0u;
+  const uint32_t ii = live ? i : 0u;  // every load below is in bounds, so none waits on a branch
+  const uint32_t* myrec = rec + (uint64_t)ii * 32;
+  // IL (a lone wave per SIMD): the flags, the record's meta and digit words
+  // and the [e]B point of phase 1 are loaded together, one memory round trip
+  // before the digit loop instead of one per dependent load (and the [e]B
+  // point's after it)
+  const uint16_t fl = reinterpret_cast<const uint16_t*>(flags)[ii];
+  const uint32_t meta0 = myrec[24];
+  uint32_t cw[8], dw[8];  // IL: the digit words in registers, not reloaded per digit
+  uint32_t ebw[32];       // IL: the [e]B cached point of phase 1
+  if constexpr (IL) {
+    load8_u4(cw, myrec);
+    load8_u4(dw, myrec + 8);
+    if (ebp) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) load8_u4(ebw + 8 * q, ebp + (uint64_t)ii * 32 + 8 * q);
+    }
+  }
+  const bool ok = live && fl == 0x0101u;
+  const uint32_t meta = live ? meta0 : 0u;
   const int H = wave_max(ok ? (int)(meta & 0xffu) : 0);
   const bool dneg = (meta >> 31) != 0;
   uint8_t verdict = 1;
@@ -497,11 +514,6 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
     ge_p2 acc2;
     ge_p1p1 t;
     ge_p3_identity(acc3);
-    uint32_t cw[8], dw[8];  // IL: the digit words in registers, not reloaded per digit
-    if constexpr (IL) {
-      load8_u4(cw, myrec);
-      load8_u4(dw, myrec + 8);
-    }
 #pragma unroll 1
     for (int pos = H - 1; pos >= 0; pos--) {
       const int sh = 4 * (pos & 7);
@@ -575,12 +587,19 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
     // + [e]B, computed by the halving role
     ge_cached eb;
     fe* f[4] = {&eb.YplusX, &eb.YminusX, &eb.Z, &eb.T2d};
+    if constexpr (IL) {
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) f[q]->v[k] = ebw[8 * q + k];
+    } else {
     const uint4* src = reinterpret_cast<const uint4*>(ebp + (uint64_t)i * 32);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const uint4 v0 = src[2 * q], v1 = src[2 * q + 1];
       f[q]->v[0] = v0.x; f[q]->v[1] = v0.y; f[q]->v[2] = v0.z; f[q]->v[3] = v0.w;
       f[q]->v[4] = v1.x; f[q]->v[5] = v1.y; f[q]->v[6] = v1.z; f[q]->v[7] = v1.w;
+    }
     }
     ge_add(t, acc3, eb);
     ge_p1p1_to_p3(acc3, t);
