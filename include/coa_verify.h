@@ -304,7 +304,7 @@ int coa_ed25519_sign_many_device(int device, const uint8_t* d_seeds, const uint8
  * callback -- the SignatureService request/oneshot idiom of
  * crypto/src/lib.rs:222-250.  Inputs are copied at submission (into one of
  * a fixed pool of intake shards, chosen by the calling thread).  A collector
- * thread launches each window on the next of two device slots per GPU
+ * thread launches each window on the next of four device slots per GPU (COA_QUEUE_SLOTS)
  * (pinned staging, own stream) without waiting for the previous window, and
  * a completion thread answers windows in order: the callback runs there with
  * status (COA_OK or a negative engine error) and the request's verdict
