@@ -476,6 +476,17 @@ __global__ void __launch_bounds__(256, WAVES) k_pre_halve(const uint8_t* __restr
 // loaded before its four doublings (launch bound of one wave per SIMD, up to
 // 512 VGPRs); larger calls keep the plain formulas (156 VGPRs, three waves
 // per SIMD).
+#ifdef COA_MAIN_TRACE  // per-wave phase stamps of k_verify_main<1, true> (tools/main_trace.py)
+__device__ unsigned long long g_main_trace[4096][4];
+#define MAIN_MARK(k)                                                                       \
+  if (IL && (threadIdx.x & 63) == 0 && (blockIdx.x * blockDim.x + threadIdx.x) / 64 < 4096) \
+    g_main_trace[(blockIdx.x * blockDim.x + threadIdx.x) / 64][k] = clock64();
+extern "C" int coa_main_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_main_trace), sizeof(g_main_trace)) == hipSuccess ? 0 : -1;
+}
+#else
+#define MAIN_MARK(k)
+#endif
 template <int WAVES, bool IL>
 __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __restrict__ rec,
                                                         const uint8_t* __restrict__ flags, uint32_t n,
@@ -484,6 +495,7 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
                                                         const uint32_t* __restrict__ ebp,
                                                         const uint32_t* __restrict__ comb,
                                                         const uint32_t* __restrict__ wcomb) {
+  MAIN_MARK(0)
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = i < n;
   const uint32_t ii = live ? i : 0u;  // every load below is in bounds, so none waits on a branch
@@ -507,6 +519,7 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
   const bool ok = live && fl == 0x0101u;
   const uint32_t meta = live ? meta0 : 0u;
   const int H = wave_max(ok ? (int)(meta & 0xffu) : 0);
+  MAIN_MARK(1)
   const bool dneg = (meta >> 31) != 0;
   uint8_t verdict = 1;
   if (ok) {
@@ -562,6 +575,7 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
         if (pos != 0) ge_p1p1_to_p2(acc2, t);
       }
     }
+    MAIN_MARK(2)
     if constexpr (IL)
       ge_p1p1_to_p3_il(acc3, t);
     else
@@ -609,6 +623,7 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
     verdict = ge_p2_is_identity(q2) ? 0 : 1;
   }
   if (live) verdicts[i] = verdict;
+  MAIN_MARK(3)
 }
 
 template <int WAVES>
