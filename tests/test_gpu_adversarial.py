@@ -64,7 +64,9 @@ def test_adversarial_device_path(engine):
 VERIFY_PATHS = {
     "split": {},                                            # default: k_pre_halve + k_verify_main
     "split/narrow": {"COA_WCOMB": "0"},                     # [e]B from the radix-256 comb
-    "split/plain-main": {"COA_MAIN_IL": "0"},               # k_verify_main without interleaved products
+    "split/plain-main": {"COA_MAIN_IL": "0", "COA_MAIN_TWO": "0"},  # k_verify_main without interleaved products
+    "split/one-wave-main": {"COA_MAIN_TWO": "0"},           # k_verify_main<1, true> (C2's kernel)
+    "split/two-wave-main": {"COA_MAIN_TWO": "1"},           # k_verify_main2 (default up to a quarter wave per SIMD)
     "split/eb-in-main": {"COA_SPLIT_EB": "0"},              # [e]B in k_verify_main, not k_pre_halve
     "split/eb-in-main/narrow": {"COA_SPLIT_EB": "0", "COA_WCOMB": "0"},
     "single": {"COA_VERIFY_SPLIT": "0"},                    # k_halve + k_verify_halved

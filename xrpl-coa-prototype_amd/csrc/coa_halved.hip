@@ -626,6 +626,97 @@ __global__ void __launch_bounds__(256, WAVES) k_verify_main(const uint32_t* __re
   MAIN_MARK(3)
 }
 
+// Split verification, phase 2 with an item's two chains in two waves: a
+// workgroup of 128 lanes takes 64 items; wave 0 runs [c](-A) over the c
+// digits, wave 1 [|d|](-sign(d) R) over the d digits, each with its own
+// doublings (twice k_verify_main's doublings per item) so that a call of one
+// wave per SIMD of items runs two waves per SIMD (or, below that size, its
+// waves on twice the SIMDs).  Wave 0 hands its point to wave 1 through LDS;
+// wave 1 adds it and the [e]B point of phase 1 and checks for the identity.
+__global__ void __launch_bounds__(128, 2) k_verify_main2(const uint32_t* __restrict__ rec,
+                                                         const uint8_t* __restrict__ flags, uint32_t n,
+                                                         uint8_t* __restrict__ verdicts,
+                                                         const uint32_t* __restrict__ scr,
+                                                         const uint32_t* __restrict__ ebp) {
+  __shared__ uint32_t qa_lds[32][64];  // wave 0's point, cached form, [dword][lane]
+  const uint32_t lane = threadIdx.x & 63u;
+  const int role = (int)(threadIdx.x >> 6);  // wave-uniform
+  const uint32_t i = blockIdx.x * 64u + lane;
+  const bool live = i < n;
+  const uint32_t ii = live ? i : 0u;
+  const uint32_t* myrec = rec + (uint64_t)ii * 32;
+  const uint16_t fl = reinterpret_cast<const uint16_t*>(flags)[ii];
+  const uint32_t meta0 = myrec[24];
+  uint32_t w[8], ebw[32];
+  load8_u4(w, myrec + 8 * role);
+  if (role == 1) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) load8_u4(ebw + 8 * q, ebp + (uint64_t)ii * 32 + 8 * q);
+  }
+  const bool ok = live && fl == 0x0101u;
+  const uint32_t meta = live ? meta0 : 0u;
+  const int H = wave_max(ok ? (int)(meta & 0xffu) : 0);
+  const bool neg = role == 1 && (meta >> 31) != 0;
+  ge_p3 acc3;
+  ge_p1p1 t;
+  ge_p3_identity(acc3);
+  if (ok) {
+    ge_p2 acc2;
+#pragma unroll 1
+    for (int pos = H - 1; pos >= 0; pos--) {
+      const int dd = (int)((w[pos >> 3] >> (4 * (pos & 7))) & 15u) - 8;
+      const int dr = neg ? -dd : dd;
+      ge_cached q;
+      tab2_load(q, scr, i, role, dr);
+      if (pos != H - 1) {
+#pragma unroll 1
+        for (int k = 0; k < 3; k++) {
+          ge_p2_dbl_il(t, acc2);
+          ge_p1p1_to_p2_il(acc2, t);
+        }
+        ge_p2_dbl_il(t, acc2);
+        ge_p1p1_to_p3_il(acc3, t);
+      }
+      tab2_fix(q, dr);
+      ge_add_il(t, acc3, q);
+      if (pos != 0) ge_p1p1_to_p2_il(acc2, t);
+    }
+    ge_p1p1_to_p3_il(acc3, t);
+    if (role == 0) {
+      ge_cached c;
+      ge_p3_to_cached(c, acc3);
+      const fe* f[4] = {&c.YplusX, &c.YminusX, &c.Z, &c.T2d};
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) qa_lds[8 * q + k][lane] = f[q]->v[k];
+    }
+  }
+  __syncthreads();
+  if (role == 0) return;
+  uint8_t verdict = 1;
+  if (ok) {
+    ge_cached qa, eb;
+    fe* fa[4] = {&qa.YplusX, &qa.YminusX, &qa.Z, &qa.T2d};
+    fe* fb[4] = {&eb.YplusX, &eb.YminusX, &eb.Z, &eb.T2d};
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        fa[q]->v[k] = qa_lds[8 * q + k][lane];
+        fb[q]->v[k] = ebw[8 * q + k];
+      }
+    ge_add_il(t, acc3, qa);
+    ge_p1p1_to_p3_il(acc3, t);
+    ge_add_il(t, acc3, eb);
+    ge_p1p1_to_p3_il(acc3, t);
+    ge_p2 q2;
+    ge_p3_to_p2(q2, acc3);
+    verdict = ge_p2_is_identity(q2) ? 0 : 1;
+  }
+  if (live) verdicts[i] = verdict;
+}
+
 template <int WAVES>
 __global__ void __launch_bounds__(256, WAVES) k_verify_halved(const uint8_t* __restrict__ pks,
                                                           const uint8_t* __restrict__ sigs,
@@ -819,7 +910,19 @@ hipError_t coa_launch_verify_split(const uint8_t* pks, const uint8_t* sigs, cons
   // C2 size): the interleaved formulas; COA_MAIN_IL=0/1 forces either (A/B)
   const char* il_env = getenv("COA_MAIN_IL");
   const bool il = il_env ? atoi(il_env) != 0 : n <= one_wave_per_simd_items();
-  if (il)
+  // an item's two chains in two waves (k_verify_main2) when the call has at
+  // most a quarter wave per SIMD of items: its waves then run on SIMDs the
+  // one-wave kernel leaves idle (4,096 / 16,384 items: 0.507 / 0.511 vs
+  // 0.594 / 0.602 ms per call).  At 32,768 some SIMDs already get two of its
+  // waves (0.82 vs 0.65 ms), and at C2's size the doubled doublings cost
+  // more than the second wave per SIMD wins back (0.90 vs 0.72 ms).
+  // COA_MAIN_TWO=0/1 forces either (A/B).
+  const char* two_s = getenv("COA_MAIN_TWO");
+  const int two_env = two_s ? atoi(two_s) : -1;
+  const bool two = ebp && (two_env >= 0 ? two_env != 0 : 4ull * n <= one_wave_per_simd_items());
+  if (two)
+    hipLaunchKernelGGL(k_verify_main2, dim3((n + 63) / 64), dim3(128), 0, s, rec, flags, n, verdicts, scratch, ebp);
+  else if (il)
     hipLaunchKernelGGL((k_verify_main<1, true>), dim3((n + main_b - 1) / main_b), dim3(main_b), 0, s, rec, flags, n,
                        verdicts, scratch, ebp, comb, wcomb);
   else
