@@ -308,6 +308,55 @@ def c5_shard(local, dev, stream, n=1 << 21, steps=3):
             "verdicts_ok": ok}
 
 
+def verify_mid(local, dev, stream, sizes=(4096, 16384), steps=20):
+    """Mid-size verify calls (an aggregation window's size, above the
+    latency kernel's 2,048): the default path (k_verify_main2, an item's two
+    chains in two waves, at <= a quarter wave per SIMD) beside the one-wave
+    k_verify_main forced by COA_MAIN_TWO=0 (read per call), same inputs."""
+    import torch
+
+    import coa_crypto
+    import workloads
+
+    out = {}
+    for n in sizes:
+        seeds = torch.from_numpy(workloads.key_seeds(n, 5)).to(dev)
+        msgs = torch.from_numpy(workloads.messages(n, 5)).to(dev)
+        pks = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        sigs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+        coa_crypto.sign_many_device(local, seeds, msgs, pks, sigs)
+        verdicts = torch.ones(n, dtype=torch.uint8, device=dev)
+        ws = torch.empty(coa_crypto.verify_workspace_bytes(n), dtype=torch.uint8, device=dev)
+        row = {}
+        for name, two in (("default", None), ("one_wave_main", "0")):
+            old = os.environ.get("COA_MAIN_TWO")
+            if two is not None:
+                os.environ["COA_MAIN_TWO"] = two
+            try:
+                verdicts.fill_(1)
+                coa_crypto.verify_strict_many_device(local, msgs, pks, sigs, verdicts, ws, stream)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(steps):
+                    coa_crypto.verify_strict_many_device(local, msgs, pks, sigs, verdicts, ws, stream)
+                e1.record(stream)
+                torch.cuda.synchronize()
+            finally:
+                if two is not None:
+                    if old is None:
+                        os.environ.pop("COA_MAIN_TWO", None)
+                    else:
+                        os.environ["COA_MAIN_TWO"] = old
+            ms = e0.elapsed_time(e1) / steps
+            row[name] = {"ms_per_call": round(ms, 4), "verifications_per_s": round(n / (ms * 1e-3), 1),
+                         "verdicts_ok": int(verdicts.sum().item()) == 0}
+        out[str(n)] = row
+        del seeds, msgs, pks, sigs, verdicts, ws
+    torch.cuda.empty_cache()
+    return out
+
+
 def c2_inflight(local, dev, n=65536, calls=48, depths=(1, 2, 3, 4)):
     """C2 batches with several verify calls in flight: one stream, workspace
     and verdict buffer per in-flight call, calls dealt round-robin -- the
@@ -1206,6 +1255,7 @@ def main():
         section("verify_single", lambda: verify_single(local, cpu["single_verify_p50_ms"] if cpu else None))
         section("c5_shard", lambda: c5_shard(local, dev, stream))
         section("c2_inflight", lambda: c2_inflight(local, dev))
+        section("verify_mid", lambda: verify_mid(local, dev, stream))
         section("verify_batch", lambda: verify_batch_config(local, dev, stream))
         section("c4_sha512", lambda: c4_sha512(local, dev, stream, [int(x) for x in args.c4_batches.split(",") if x],
                                                2, threads))
