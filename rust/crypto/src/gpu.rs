@@ -38,6 +38,13 @@ fn verdict(rc: i32) -> Result<(), CryptoError> {
     }
 }
 
+/// The 64 bytes R || s of a `Signature` (its private `flatten`,
+/// crypto/src/lib.rs:193-198): the primary's callers build engine requests with this
+/// instead of a `bincode::serialize` per signature.
+pub fn signature_bytes(signature: &crate::Signature) -> [u8; 64] {
+    signature.flatten()
+}
+
 fn engine_ok(rc: i32) -> i32 {
     assert!(rc >= 0, "MI355X verification engine failure {}: {}", rc, ffi::last_error());
     rc
@@ -45,12 +52,12 @@ fn engine_ok(rc: i32) -> i32 {
 
 /// Signature::verify (crypto/src/lib.rs:200-204): dalek 1.0.1 verify_strict
 /// of the 64-byte signature R || s over the 32-byte digest.  A triple the
-/// pre-verification stage already verified Ok (in a coalesced launch) is
-/// answered from `verified`; any other takes the engine's single-signature
-/// latency kernel on an idle device context.
+/// pre-verification stage already verified (in a coalesced launch; Ok or
+/// Err, both exact) is answered from `verified`; any other takes the
+/// engine's single-signature latency kernel on an idle device context.
 pub fn verify(signature: &[u8; 64], digest: &Digest, public_key: &PublicKey) -> Result<(), CryptoError> {
-    if crate::verified::take_signature(digest, public_key, signature) {
-        return Ok(());
+    if let Some(ok) = crate::verified::take_signature(digest, public_key, signature) {
+        return if ok { Ok(()) } else { Err(CryptoError::new()) };
     }
     verdict(unsafe { ffi::coa_ed25519_verify_strict(digest.0.as_ptr(), public_key.0.as_ptr(), signature.as_ptr()) })
 }

@@ -39,36 +39,90 @@ use tokio::sync::oneshot;
 type Verdict = Result<Result<(), CryptoError>, c_int>;
 
 /// The crypto of one `Certificate::verify` in the engine's terms (the
-/// `primary` crate builds it: rust/primary/src/gpu_certificate.rs).
+/// `primary` crate builds it: rust/primary/src/gpu_certificate.rs), held in
+/// ONE buffer that is also its `verified` cache key -- every byte the
+/// verdict depends on, length-framed:
+///
+///   header_len u64 | header input | id | origin | header signature R || s |
+///   round u64 | n_votes u64 | n_votes x key (32) | n_votes x signature (64)
+///
+/// Built once per certificate with its exact size (no per-vote
+/// serialization, no second copy for the key): the queue copies the fields
+/// at submission, and the buffer then becomes the cache key as it is.
 pub struct CertificateCrypto {
-    /// the bytes `Header::digest` hashes (primary/src/messages.rs:70-84)
-    pub header_input: Vec<u8>,
-    pub id: Digest,
-    pub origin: PublicKey,
-    pub header_signature: [u8; 64],
-    pub round: u64,
-    /// the votes: 32-byte keys and 64-byte signatures, concatenated
-    pub vote_keys: Vec<u8>,
-    pub vote_signatures: Vec<u8>,
+    bytes: Vec<u8>,
+    header_len: usize,
+    n_votes: usize,
 }
 
 impl CertificateCrypto {
-    /// Every byte the certificate's crypto verdict depends on, length-framed
-    /// (the key of `verified::remember_certificate`).
-    pub fn key_bytes(&self) -> Vec<u8> {
-        let mut k = Vec::with_capacity(
-            8 + self.header_input.len() + 32 + 32 + 64 + 8 + 8 + self.vote_keys.len() + self.vote_signatures.len(),
-        );
-        k.extend_from_slice(&(self.header_input.len() as u64).to_le_bytes());
-        k.extend_from_slice(&self.header_input);
-        k.extend_from_slice(&self.id.0);
-        k.extend_from_slice(&self.origin.0);
-        k.extend_from_slice(&self.header_signature);
-        k.extend_from_slice(&self.round.to_le_bytes());
-        k.extend_from_slice(&((self.vote_keys.len() / 32) as u64).to_le_bytes());
-        k.extend_from_slice(&self.vote_keys);
-        k.extend_from_slice(&self.vote_signatures);
-        k
+    /// `write_header_input` appends the `header_len` bytes `Header::digest`
+    /// hashes (primary/src/messages.rs:70-84); `votes` are the certificate's
+    /// (key, signature) pairs in order.
+    pub fn new<F: FnOnce(&mut Vec<u8>)>(header_len: usize, write_header_input: F, id: &Digest, origin: &PublicKey,
+                                        header_signature: &crate::Signature, round: u64,
+                                        votes: &[(PublicKey, crate::Signature)]) -> Self {
+        let n_votes = votes.len();
+        let mut bytes = Vec::with_capacity(8 + header_len + 32 + 32 + 64 + 8 + 8 + 96 * n_votes);
+        bytes.extend_from_slice(&(header_len as u64).to_le_bytes());
+        write_header_input(&mut bytes);
+        assert_eq!(bytes.len(), 8 + header_len, "header input of the announced length");
+        bytes.extend_from_slice(&id.0);
+        bytes.extend_from_slice(&origin.0);
+        bytes.extend_from_slice(&crate::gpu::signature_bytes(header_signature));
+        bytes.extend_from_slice(&round.to_le_bytes());
+        bytes.extend_from_slice(&(n_votes as u64).to_le_bytes());
+        for (key, _) in votes {
+            bytes.extend_from_slice(&key.0);
+        }
+        for (_, signature) in votes {
+            bytes.extend_from_slice(&crate::gpu::signature_bytes(signature));
+        }
+        Self { bytes, header_len, n_votes }
+    }
+
+    fn at(&self, field: usize) -> usize {
+        // offsets of: header input, id, origin, header signature, round, votes
+        let h = 8 + self.header_len;
+        [8, h, h + 32, h + 64, h + 128, h + 144][field]
+    }
+    pub fn header_input(&self) -> &[u8] {
+        &self.bytes[8..8 + self.header_len]
+    }
+    pub fn id(&self) -> &[u8] {
+        &self.bytes[self.at(1)..self.at(1) + 32]
+    }
+    pub fn origin(&self) -> &[u8] {
+        &self.bytes[self.at(2)..self.at(2) + 32]
+    }
+    pub fn header_signature(&self) -> &[u8] {
+        &self.bytes[self.at(3)..self.at(3) + 64]
+    }
+    pub fn round(&self) -> u64 {
+        let mut r = [0u8; 8];
+        r.copy_from_slice(&self.bytes[self.at(4)..self.at(4) + 8]);
+        u64::from_le_bytes(r)
+    }
+    pub fn n_votes(&self) -> usize {
+        self.n_votes
+    }
+    /// the votes' 32-byte keys, concatenated
+    pub fn vote_keys(&self) -> &[u8] {
+        &self.bytes[self.at(5)..self.at(5) + 32 * self.n_votes]
+    }
+    /// the votes' 64-byte signatures, concatenated
+    pub fn vote_signatures(&self) -> &[u8] {
+        let v = self.at(5) + 32 * self.n_votes;
+        &self.bytes[v..v + 64 * self.n_votes]
+    }
+    /// Every byte the certificate's crypto verdict depends on (the key of
+    /// `verified::take_certificate`).
+    pub fn key_bytes(&self) -> &[u8] {
+        &self.bytes
+    }
+    /// The same bytes, moved out (the key of `verified::remember_certificate`).
+    pub fn into_key(self) -> Vec<u8> {
+        self.bytes
     }
 }
 
@@ -76,10 +130,14 @@ impl CertificateCrypto {
 /// (the batch is then stored, worker/src/processor.rs:41).
 type DigestReply = Result<(Digest, Vec<u8>), c_int>;
 
+/// A certificate's COA_CERT_* bits, with its crypto handed back (it becomes
+/// the `verified` key without a copy).
+type CertificateReply = Result<(u8, CertificateCrypto), c_int>;
+
 enum Request {
     Verify(Digest, PublicKey, [u8; 64], oneshot::Sender<Verdict>),
     Batch(Digest, Vec<(PublicKey, [u8; 64])>, oneshot::Sender<Verdict>),
-    Certificate(CertificateCrypto, oneshot::Sender<Result<u8, c_int>>),
+    Certificate(CertificateCrypto, oneshot::Sender<CertificateReply>),
     Digest(Vec<u8>, oneshot::Sender<DigestReply>),
 }
 
@@ -111,7 +169,11 @@ impl VerifyService {
     pub fn new(max_batch: usize, max_delay_us: u32) -> Self {
         let queue = unsafe { ffi::coa_queue_create(max_batch, max_delay_us) };
         assert!(!queue.is_null(), "MI355X verification engine: coa_queue_create failed: {}", ffi::last_error());
-        let idle: u32 = std::env::var("COA_SERVICE_IDLE_LAUNCH").ok().and_then(|v| v.parse().ok()).unwrap_or(1);
+        // windows in flight below which a window launches at once: 0..=64, as
+        // coa_queue_create clamps COA_QUEUE_IDLE_LAUNCH (a larger value is
+        // taken as 64, never a failed assertion at node start)
+        let idle: u32 =
+            std::env::var("COA_SERVICE_IDLE_LAUNCH").ok().and_then(|v| v.parse().ok()).unwrap_or(1u32).min(64);
         let rc = unsafe { ffi::coa_queue_set_idle_launch(queue, idle) };
         assert_eq!(rc, ffi::COA_OK, "MI355X verification engine: coa_queue_set_idle_launch({}) failed", idle);
         let queue = Queue(queue);
@@ -168,12 +230,13 @@ impl VerifyService {
     }
 
     /// The crypto of `Certificate::verify` (primary/src/messages.rs:189-215):
-    /// the COA_CERT_* bits, 0 = every crypto check Ok.
-    pub async fn certificate(&self, crypto: CertificateCrypto) -> u8 {
+    /// the COA_CERT_* bits (0 = every crypto check Ok), and the request
+    /// handed back.
+    pub async fn certificate(&self, crypto: CertificateCrypto) -> (u8, CertificateCrypto) {
         let (sender, receiver) = oneshot::channel();
         self.send(Request::Certificate(crypto, sender)).await;
         match receiver.await.expect("Failed to receive status from Verify Service") {
-            Ok(bits) => bits,
+            Ok(reply) => reply,
             Err(status) => panic!("MI355X verification engine failure {} (every context failed)", status),
         }
     }
@@ -211,7 +274,7 @@ fn submit_window(queue: &Queue, window: Vec<Request>) {
                 senders.push(sender);
             }
             Request::Batch(digest, votes, sender) => submit_batch(queue, &digest, &votes, sender),
-            Request::Certificate(crypto, sender) => submit_certificate(queue, &crypto, sender),
+            Request::Certificate(crypto, sender) => submit_certificate(queue, crypto, sender),
             Request::Digest(bytes, sender) => submit_digest(queue, bytes, sender),
         }
     }
@@ -250,18 +313,20 @@ fn submit_batch(queue: &Queue, digest: &Digest, votes: &[(PublicKey, [u8; 64])],
     }
 }
 
-fn submit_certificate(queue: &Queue, c: &CertificateCrypto, sender: oneshot::Sender<Result<u8, c_int>>) {
-    let n_votes = c.vote_keys.len() / 32;
-    assert_eq!(c.vote_signatures.len(), 64 * n_votes, "64-byte signature per vote key");
-    let user = Box::into_raw(Box::new(sender)) as *mut c_void;
+fn submit_certificate(queue: &Queue, crypto: CertificateCrypto, sender: oneshot::Sender<CertificateReply>) {
+    // the request rides along with the sender (the queue copies its fields
+    // at submission) and comes back with the bits
+    let user = Box::into_raw(Box::new((sender, crypto))) as *mut c_void;
+    let c = unsafe { &(*(user as *const (oneshot::Sender<CertificateReply>, CertificateCrypto))).1 };
     let rc = unsafe {
-        ffi::coa_queue_submit_certificate(queue.0, c.header_input.as_ptr(), c.header_input.len(), c.id.0.as_ptr(),
-                                          c.origin.0.as_ptr(), c.header_signature.as_ptr(), c.round,
-                                          c.vote_keys.as_ptr(), c.vote_signatures.as_ptr(), n_votes,
-                                          Some(on_status), user)
+        ffi::coa_queue_submit_certificate(queue.0, c.header_input().as_ptr(), c.header_input().len(),
+                                          c.id().as_ptr(), c.origin().as_ptr(), c.header_signature().as_ptr(),
+                                          c.round(), c.vote_keys().as_ptr(), c.vote_signatures().as_ptr(),
+                                          c.n_votes(), Some(on_status), user)
     };
     if rc != ffi::COA_OK {
-        let sender = unsafe { Box::from_raw(user as *mut oneshot::Sender<Result<u8, c_int>>) };
+        let pair = unsafe { Box::from_raw(user as *mut (oneshot::Sender<CertificateReply>, CertificateCrypto)) };
+        let (sender, _) = *pair;
         let _ = sender.send(Err(rc));
     }
 }
@@ -316,15 +381,17 @@ unsafe extern "C" fn on_verdict(user: *mut c_void, status: c_int, verdicts: *con
     let _ = sender.send(reply);
 }
 
-/// One certificate: one status byte of COA_CERT_* bits.
+/// One certificate: one status byte of COA_CERT_* bits, and the request
+/// handed back.
 unsafe extern "C" fn on_status(user: *mut c_void, status: c_int, verdicts: *const u8, n: usize) {
-    let sender = Box::from_raw(user as *mut oneshot::Sender<Result<u8, c_int>>);
+    let pair = Box::from_raw(user as *mut (oneshot::Sender<CertificateReply>, CertificateCrypto));
+    let (sender, crypto) = *pair;
     let reply = if status != ffi::COA_OK {
         Err(status)
     } else if verdicts.is_null() || n != 1 {
         Err(ffi::COA_EINVAL)
     } else {
-        Ok(*verdicts)
+        Ok((*verdicts, crypto))
     };
     let _ = sender.send(reply);
 }
@@ -348,14 +415,17 @@ unsafe extern "C" fn on_digest(user: *mut c_void, status: c_int, verdicts: *cons
 /// The process's service (created on first use, inside the tokio runtime):
 /// for callers whose constructors take no service handle -- the worker's
 /// `Processor::spawn` keeps the reference's signature this way.
-/// COA_SERVICE_MAX_BATCH / COA_SERVICE_MAX_DELAY_US tune it.
+/// COA_SERVICE_MAX_BATCH / COA_SERVICE_MAX_DELAY_US tune it.  Set up through
+/// `std::sync::Once` (no `OnceLock`: the reference pins Rust 1.51.0).
 pub fn global() -> VerifyService {
-    static SERVICE: std::sync::OnceLock<VerifyService> = std::sync::OnceLock::new();
-    SERVICE
-        .get_or_init(|| {
+    static INIT: std::sync::Once = std::sync::Once::new();
+    static mut SERVICE: *const VerifyService = std::ptr::null();
+    unsafe {
+        INIT.call_once(|| {
             let batch = std::env::var("COA_SERVICE_MAX_BATCH").ok().and_then(|v| v.parse().ok()).unwrap_or(65_536);
             let delay = std::env::var("COA_SERVICE_MAX_DELAY_US").ok().and_then(|v| v.parse().ok()).unwrap_or(500);
-            VerifyService::new(batch, delay)
-        })
-        .clone()
+            SERVICE = Box::into_raw(Box::new(VerifyService::new(batch, delay)));
+        });
+        (*SERVICE).clone()
+    }
 }

@@ -26,6 +26,7 @@
 use crate::error::{DagError, DagResult};
 use crate::messages::{Certificate, Header};
 use config::Committee;
+use crypto::gpu::signature_bytes;
 use crypto::service::CertificateCrypto;
 use crypto::{CryptoError, PublicKey};
 use std::collections::HashSet;
@@ -53,11 +54,15 @@ fn engine_failure(rc: c_int) -> ! {
     panic!("MI355X verification engine failure {}: {}", rc, msg)
 }
 
-/// The bytes Header::digest hashes (primary/src/messages.rs:70-84):
+/// Length of the bytes Header::digest hashes (primary/src/messages.rs:70-84).
+pub fn header_digest_len(h: &Header) -> usize {
+    32 + 8 + 36 * h.payload.len() + 32 * h.parents.len()
+}
+
+/// Appends the bytes Header::digest hashes (primary/src/messages.rs:70-84):
 /// author || round (u64 LE) || (payload digest || worker id (u32 LE))* in the
 /// BTreeMap's key order || parent digests in the BTreeSet's order.
-pub fn header_digest_input(h: &Header) -> Vec<u8> {
-    let mut out = Vec::with_capacity(32 + 8 + 36 * h.payload.len() + 32 * h.parents.len());
+pub fn write_header_digest_input(h: &Header, out: &mut Vec<u8>) {
     out.extend_from_slice(&h.author.0);
     out.extend_from_slice(&h.round.to_le_bytes());
     for (digest, worker_id) in &h.payload {
@@ -67,42 +72,17 @@ pub fn header_digest_input(h: &Header) -> Vec<u8> {
     for parent in &h.parents {
         out.extend_from_slice(&parent.0);
     }
-    out
-}
-
-/// The 64-byte R || s of a crypto::Signature through its serde form
-/// (the fields are private; bincode writes part1 then part2, 32 bytes each,
-/// with no length prefix for fixed arrays).
-pub(crate) fn signature_bytes(sig: &crypto::Signature) -> [u8; 64] {
-    let v = bincode::serialize(sig).expect("Signature serializes");
-    let mut out = [0u8; 64];
-    out.copy_from_slice(&v[..64]);
-    out
-}
-
-fn votes_flat(cert: &Certificate) -> (Vec<u8>, Vec<u8>) {
-    let (mut pks, mut sigs) = (Vec::with_capacity(32 * cert.votes.len()), Vec::with_capacity(64 * cert.votes.len()));
-    for (name, sig) in &cert.votes {
-        pks.extend_from_slice(&name.0);
-        sigs.extend_from_slice(&signature_bytes(sig));
-    }
-    (pks, sigs)
 }
 
 /// The crypto input of Certificate::verify in the engine's terms (the
-/// request `VerifyService::certificate` and `coa_certificate_verify` take).
+/// request `VerifyService::certificate` and `coa_certificate_verify` take),
+/// built once in one buffer of its exact size: the signatures' bytes come
+/// from `crypto::gpu::signature_bytes` (no `bincode::serialize` per vote),
+/// and the buffer is also the `verified` cache key (no second copy).
 pub(crate) fn certificate_crypto(cert: &Certificate) -> CertificateCrypto {
     let h = &cert.header;
-    let (vote_keys, vote_signatures) = votes_flat(cert);
-    CertificateCrypto {
-        header_input: header_digest_input(h),
-        id: h.id.clone(),
-        origin: h.author,
-        header_signature: signature_bytes(&h.signature),
-        round: h.round,
-        vote_keys,
-        vote_signatures,
-    }
+    CertificateCrypto::new(header_digest_len(h), |out| write_header_digest_input(h, out), &h.id, &h.author,
+                           &h.signature, h.round, &cert.votes)
 }
 
 /// The checks of Certificate::verify in the reference's order, the crypto
@@ -143,13 +123,13 @@ pub fn verify(cert: &Certificate, committee: &Committee) -> DagResult<()> {
         return Ok(());
     }
     let c = certificate_crypto(cert);
-    if let Some(bits) = crypto::verified::take_certificate(&c.key_bytes()) {
+    if let Some(bits) = crypto::verified::take_certificate(c.key_bytes()) {
         return checks_in_order(cert, committee, bits as c_int);
     }
     let st = unsafe {
-        coa_certificate_verify(c.header_input.as_ptr(), c.header_input.len(), c.id.0.as_ptr(), c.origin.0.as_ptr(),
-                               c.header_signature.as_ptr(), c.round, c.vote_keys.as_ptr(),
-                               c.vote_signatures.as_ptr(), cert.votes.len(), 0)
+        coa_certificate_verify(c.header_input().as_ptr(), c.header_input().len(), c.id().as_ptr(),
+                               c.origin().as_ptr(), c.header_signature().as_ptr(), c.round(),
+                               c.vote_keys().as_ptr(), c.vote_signatures().as_ptr(), c.n_votes(), 0)
     };
     if st < 0 {
         engine_failure(st);
@@ -172,15 +152,16 @@ pub fn verify_many(certs: &[&Certificate], committee: &Committee) -> Vec<DagResu
     let mut voff = vec![0u64];
     for &i in &todo {
         let h = &certs[i].header;
-        hdata.extend_from_slice(&header_digest_input(h));
+        write_header_digest_input(h, &mut hdata);
         hoff.push(hdata.len() as u64);
         ids.extend_from_slice(&h.id.0);
         origins.extend_from_slice(&h.author.0);
         hsigs.extend_from_slice(&signature_bytes(&h.signature));
         rounds.push(h.round);
-        let (p, s) = votes_flat(certs[i]);
-        vpks.extend_from_slice(&p);
-        vsigs.extend_from_slice(&s);
+        for (name, sig) in &certs[i].votes {
+            vpks.extend_from_slice(&name.0);
+            vsigs.extend_from_slice(&signature_bytes(sig));
+        }
         voff.push((vpks.len() / 32) as u64);
     }
     let mut status = vec![0u8; n];

@@ -8,18 +8,25 @@
 //! signatures per launch.  This task sits on the channel in front of `Core`:
 //! every message the receiver delivers is submitted at once to the
 //! `VerifyService` (the engine's aggregation queue, which coalesces the
-//! requests of the window into a few launches), and the messages are passed
-//! on to `Core` in ARRIVAL ORDER as soon as each one's verdict is in (an
-//! ordered set of futures: a later message never overtakes an earlier one).
+//! requests of the window into a few launches), and each message is passed
+//! on to `Core` as soon as its verdict is in AND every earlier message from
+//! the same authority has been passed on: per-author arrival order, the only
+//! order the reference's network delivers anyway (one connection per peer;
+//! messages of different peers interleave arbitrarily in `Core`'s channel).
+//! A slow request -- a certificate with a key outside the registered
+//! committee, or one the exact random-linear-combination check re-decides
+//! (0.35-1.4 ms) -- therefore holds back only its own author's later
+//! messages, not every message behind it (bench.py
+//! secondary.queue_round_mix.adversarial measures both orderings).
 //!
 //! `Core` is not changed.  Its verify calls find the verdicts this stage
 //! computed in `crypto::verified`, keyed by every byte the verdict depends on
 //! (rust/crypto/src/verified.rs), so they return exactly what the engine
-//! returns for those bytes -- and `Core` raises the reference's `DagError`s
-//! in the reference's order, because the non-crypto checks (gc round,
-//! expected vote, stake, worker ids, quorum) still run there first.  A
-//! message whose signature fails here is simply not remembered: `Core`'s
-//! call then asks the engine again and gets the same Err.
+//! returns for those bytes -- Ok and Err alike, so `Core` never launches for
+//! a message this stage saw, even under a flood of bad signatures -- and
+//! `Core` raises the reference's `DagError`s in the reference's order,
+//! because the non-crypto checks (gc round, expected vote, stake, worker
+//! ids, quorum) still run there first.
 //!
 //! Wiring in primary/src/primary.rs (`Primary::spawn`):
 //!     let (tx_pre_verify, rx_pre_verify) = channel(CHANNEL_CAPACITY);
@@ -27,11 +34,13 @@
 //!     // tx_primary_messages
 //!     PreVerifier::spawn(crypto::service::global(), rx_pre_verify, tx_primary_messages);
 //! and `mod pre_verify;` in primary/src/lib.rs.
-use crate::gpu_certificate::{certificate_crypto, signature_bytes};
+use crate::gpu_certificate::certificate_crypto;
 use crate::primary::PrimaryMessage;
+use crypto::gpu::signature_bytes;
 use crypto::service::VerifyService;
-use crypto::{verified, Hash as _};
-use futures::stream::{FuturesOrdered, StreamExt as _};
+use crypto::{verified, Hash as _, PublicKey};
+use futures::stream::{FuturesUnordered, StreamExt as _};
+use std::collections::{HashMap, VecDeque};
 use tokio::sync::mpsc::{Receiver, Sender};
 
 /// Most messages between the receiver and `Core` at once (bounded memory;
@@ -41,20 +50,54 @@ const MAX_IN_FLIGHT: usize = 16_384;
 
 pub struct PreVerifier;
 
+/// The authority whose connection delivered the message (the order this
+/// stage keeps).
+fn author_of(message: &PrimaryMessage) -> PublicKey {
+    match message {
+        PrimaryMessage::Header(header) => header.author,
+        PrimaryMessage::Vote(vote) => vote.author,
+        PrimaryMessage::Certificate(certificate) => certificate.header.author,
+        PrimaryMessage::CertificatesRequest(_, requestor) => *requestor,
+    }
+}
+
 impl PreVerifier {
     pub fn spawn(service: VerifyService, mut rx_messages: Receiver<PrimaryMessage>, tx_core: Sender<PrimaryMessage>) {
         tokio::spawn(async move {
-            let mut pending = FuturesOrdered::new();
+            let mut pending = FuturesUnordered::new();
+            // per author: arrival sequence numbers in order, each with its
+            // message once verified
+            let mut lanes: HashMap<PublicKey, VecDeque<(u64, Option<PrimaryMessage>)>> = HashMap::new();
+            let mut in_flight = 0usize;
+            let mut seq = 0u64;
             loop {
                 tokio::select! {
-                    Some(message) = rx_messages.recv(), if pending.len() < MAX_IN_FLIGHT => {
-                        pending.push_back(pre_verify(service.clone(), message));
+                    Some(message) = rx_messages.recv(), if in_flight < MAX_IN_FLIGHT => {
+                        let author = author_of(&message);
+                        seq += 1;
+                        let my_seq = seq;
+                        lanes.entry(author).or_default().push_back((my_seq, None));
+                        in_flight += 1;
+                        let service = service.clone();
+                        pending.push(async move { (author, my_seq, pre_verify(service, message).await) });
                     },
-                    Some(message) = pending.next() => {
-                        tx_core
-                            .send(message)
-                            .await
-                            .expect("Failed to send message to the core");
+                    Some((author, done_seq, message)) = pending.next() => {
+                        let lane = lanes.get_mut(&author).expect("lane of a pending message");
+                        if let Some(slot) = lane.iter_mut().find(|(s, _)| *s == done_seq) {
+                            slot.1 = Some(message);
+                        }
+                        // release this author's verified prefix, in order
+                        while lane.front().map_or(false, |(_, m)| m.is_some()) {
+                            let (_, m) = lane.pop_front().unwrap();
+                            in_flight -= 1;
+                            tx_core
+                                .send(m.unwrap())
+                                .await
+                                .expect("Failed to send message to the core");
+                        }
+                        if lane.is_empty() {
+                            lanes.remove(&author);
+                        }
                     },
                     else => break,
                 }
@@ -64,30 +107,28 @@ impl PreVerifier {
 }
 
 /// Verifies the crypto of one message through the service and remembers the
-/// verdict for `Core`'s call; hands the message back unchanged.
+/// verdict -- Ok or Err -- for `Core`'s call; hands the message back
+/// unchanged.
 async fn pre_verify(service: VerifyService, message: PrimaryMessage) -> PrimaryMessage {
     match &message {
         PrimaryMessage::Header(header) => {
             // Header::verify's signature step (messages.rs:64-66)
             let signature = signature_bytes(&header.signature);
-            if service.verify(&header.id, &header.author, signature).await.is_ok() {
-                verified::remember_signature(&header.id, &header.author, &signature);
-            }
+            let ok = service.verify(&header.id, &header.author, signature).await.is_ok();
+            verified::remember_signature(&header.id, &header.author, &signature, ok);
         }
         PrimaryMessage::Vote(vote) => {
             // Vote::verify's signature step (messages.rs:139-141)
             let digest = vote.digest();
             let signature = signature_bytes(&vote.signature);
-            if service.verify(&digest, &vote.author, signature).await.is_ok() {
-                verified::remember_signature(&digest, &vote.author, &signature);
-            }
+            let ok = service.verify(&digest, &vote.author, signature).await.is_ok();
+            verified::remember_signature(&digest, &vote.author, &signature, ok);
         }
         PrimaryMessage::Certificate(certificate) => {
-            // the crypto of Certificate::verify (messages.rs:189-215), fused
-            let crypto = certificate_crypto(certificate);
-            let key = crypto.key_bytes();
-            let bits = service.certificate(crypto).await;
-            verified::remember_certificate(key, bits);
+            // the crypto of Certificate::verify (messages.rs:189-215), fused;
+            // the request comes back and becomes the cache key as it is
+            let (bits, crypto) = service.certificate(certificate_crypto(certificate)).await;
+            verified::remember_certificate(crypto.into_key(), bits);
         }
         PrimaryMessage::CertificatesRequest(..) => {}
     }

@@ -92,13 +92,15 @@ def test_no_placeholders_and_helpers_defined():
     for group in re.findall(r"\buse\s+[\w:]+::\{([^}]*)\}", text):
         defined |= {n.strip().split(" as ")[-1].strip() for n in group.split(",") if n.strip()}
     defined |= set(re.findall(r"\buse\s+[\w:]+::(\w+)\s*;", text))
+    # closure parameters of a generic `F: FnOnce(..)` type are called too
+    defined |= set(re.findall(r"\b(\w+):\s*F\b", text))
     called = set(re.findall(r"(?<![\w.:!])([a-z_][a-z0-9_]*)\s*\(", text))
     keywords = {"if", "for", "while", "match", "assert", "assert_eq", "panic", "vec", "fn", "return", "Some", "Ok",
                 "Err", "ensure", "println", "loop", "in", "as", "unsafe", "move", "Box", "format", "mod", "let",
                 "const", "mut", "pub"}
     unknown = sorted(called - defined - keywords)
     assert not unknown, unknown
-    assert "header_digest_input" in defined
+    assert "write_header_digest_input" in defined
     assert os.path.exists(os.path.join(RUST, "crypto", "build.rs"))
 
 
@@ -137,7 +139,7 @@ def test_service_callbacks_match_coa_verdict_cb():
         assert cb and cb.group(1) in names, fn_name
     # Box::into_raw / Box::from_raw balance per boxed type: each callback and
     # each submit-failure branch takes back what the submit gave away
-    given = re.findall(r"Box::into_raw\(Box::new\(", src)
+    given = re.findall(r"let user = Box::into_raw\(Box::new\(", src)
     taken = re.findall(r"Box::from_raw\(user as \*mut ", src)
     assert len(given) == 4 and len(taken) == 8, (len(given), len(taken))
     assert "panic!" not in "".join(re.findall(r'unsafe extern "C" fn.*?\n\}', src, flags=re.S))
@@ -146,13 +148,54 @@ def test_service_callbacks_match_coa_verdict_cb():
 def test_pre_verification_stage_and_processor_use_the_service():
     """The stage in front of Core and the worker's Processor go through the
     service (coalesced launches), and the synchronous drop-in calls consult
-    the verdicts the stage computed."""
+    the verdicts the stage computed -- Ok and Err alike (an Err
+    left for Core made it launch a second time per bad signature)."""
     pre = open(os.path.join(RUST, "primary", "src", "pre_verify.rs")).read()
-    assert "FuturesOrdered" in pre and "service.verify(" in pre and "service.certificate(" in pre
-    assert "remember_signature" in pre and "remember_certificate" in pre
+    assert "service.verify(" in pre and "service.certificate(" in pre
+    assert "remember_certificate" in pre
+    # both outcomes remembered: the verdict is passed, not filtered by is_ok
+    assert len(re.findall(r"remember_signature\([^;]*,\s*ok\)", pre)) == 2
+    assert "if service.verify" not in pre
+    # per-author release order (FuturesUnordered + lanes), not one global FIFO
+    assert "FuturesUnordered" in pre and "author_of" in pre
     proc_ = open(os.path.join(RUST, "worker", "src", "processor.rs")).read()
     assert "service.digest(" in proc_ and "FuturesOrdered" in proc_ and "sha512_digest" not in proc_
     gpu = open(os.path.join(RUST, "crypto", "src", "gpu.rs")).read()
-    assert "verified::take_signature" in gpu
+    assert "verified::take_signature" in gpu and "Some(ok)" in gpu
+    ver = open(os.path.join(RUST, "crypto", "src", "verified.rs")).read()
+    assert "Fifo<[u8; 128], bool>" in ver
     cert = open(os.path.join(RUST, "primary", "src", "gpu_certificate.rs")).read()
     assert "verified::take_certificate" in cert
+
+
+def test_certificate_requests_built_once_without_bincode():
+    """VERDICT r3 missing 2: the certificate request is built once, in one
+    buffer that is also the cache key (no per-vote bincode::serialize, no
+    second key copy)."""
+    srcs = {f: re.sub(r"//[^\n]*", "", open(os.path.join(RUST, "primary", "src", f)).read())
+            for f in ("pre_verify.rs", "gpu_certificate.rs")}
+    for f, src in srcs.items():
+        assert "bincode::serialize" not in src, f
+    assert "key_bytes" not in srcs["pre_verify.rs"] and "into_key()" in srcs["pre_verify.rs"]
+    assert srcs["gpu_certificate.rs"].count("key_bytes()") == 1
+    svc = open(os.path.join(RUST, "crypto", "src", "service.rs")).read()
+    assert "pub fn into_key(self) -> Vec<u8>" in svc and "pub fn key_bytes(&self) -> &[u8]" in svc
+
+
+def test_rust_sources_build_on_the_reference_toolchain():
+    """The reference's CI pins Rust 1.51.0 (.github/workflows/rust.yml:20):
+    no std API or syntax newer than that in the shim (no rustc here, so the
+    known newer ones are searched for)."""
+    newer = {
+        "OnceLock": r"\bOnceLock\b", "LazyLock": r"\bLazyLock\b", "OnceCell (std)": r"std::cell::OnceCell",
+        "is_some_and": r"\.is_some_and\(", "is_ok_and": r"\.is_ok_and\(", "then_some": r"\.then_some\(",
+        "let-else": r"\blet\s+[^;={]+=[^;{]+\belse\s*\{", "array::from_fn": r"array::from_fn",
+        "div_ceil": r"\.div_ceil\(", "abs_diff": r"\.abs_diff\(", "inline format args": r'"[^"\n]*\{[a-z_][a-z0-9_]*(:[^}]*)?\}',
+        "const Mutex::new": r"static\s+\w+\s*:\s*Mutex", "std::iter::zip": r"iter::zip\(",
+    }
+    for dirpath, _, files in os.walk(RUST):
+        for f in files:
+            if f.endswith(".rs"):
+                src = re.sub(r"//[^\n]*", "", open(os.path.join(dirpath, f)).read())
+                for what, pat in newer.items():
+                    assert not re.search(pat, src), (f, what)

@@ -1,0 +1,52 @@
+#!/bin/bash
+# Round-4 GPU session steps, one parameterised script (replaces the one-off
+# tools/gpu_r3_*.sh): tools/gpu_r4.sh <step> [args]
+#   env          box environment relevant to HIP queues
+#   hwq          hardware-queue probe matrix (tools/hwq_probe)
+#   bench HQ ARGS  bench.py with GPU_MAX_HW_QUEUES=HQ ("-" = leave unset)
+#   tests ARGS   the GPU test suite (pytest -m gpu ARGS)
+# Every GPU step runs under its own timeout; the script stops at the first
+# failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+mkdir -p gpurun_out
+step=$1
+shift
+case "$step" in
+  env)
+    env | grep -E '^(GPU_|HIP_|HSA_|ROC|AMD_|OMP_)' | sort > gpurun_out/r4_env.txt
+    (nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null) >> gpurun_out/r4_env.txt
+    ;;
+  hwq)
+    out=gpurun_out/r4_hwq.jsonl
+    : > $out
+    for hq in unset 4 8; do
+      for kind in plain cumask hi lo; do
+        for bg in 0 3; do
+          if [ $hq = unset ]; then
+            timeout -k 5 30 env -u GPU_MAX_HW_QUEUES tools/hwq_probe $kind 8 $bg >> $out || exit 1
+          else
+            GPU_MAX_HW_QUEUES=$hq timeout -k 5 30 tools/hwq_probe $kind 8 $bg >> $out || exit 1
+          fi
+        done
+      done
+    done
+    ;;
+  bench)
+    hq=$1
+    tag=$2
+    shift 2
+    if [ "$hq" = "-" ]; then
+      timeout -k 10 400 python -u bench.py "$@" > gpurun_out/r4_bench_$tag.json 2> gpurun_out/r4_bench_$tag.err || exit 1
+    else
+      GPU_MAX_HW_QUEUES=$hq timeout -k 10 400 python -u bench.py "$@" > gpurun_out/r4_bench_$tag.json 2> gpurun_out/r4_bench_$tag.err || exit 1
+    fi
+    ;;
+  tests)
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > gpurun_out/r4_tests.log 2>&1 || exit 1
+    ;;
+  *)
+    echo "unknown step $step" >&2
+    exit 2
+    ;;
+esac
