@@ -179,11 +179,24 @@ class Certificate:
         if self.is_genesis(committee):
             return
         h = self.header
-        vp = np.array([list(bytes(pk)) for pk, _ in self.votes], np.uint8).reshape(-1, 32)
-        vs = np.array([list(sg.flatten()) for _, sg in self.votes], np.uint8).reshape(-1, 64)
-        st = coa_crypto.certificate_verify(h.digest_input(), h.id, h.author, h.signature.flatten(), h.round, vp, vs,
-                                           rng_seed=rng_seed)
+        # the bits the pre-verification stage computed for exactly these bytes
+        # (coa_crypto.verified; rust/primary/src/gpu_certificate.rs), else one
+        # engine call
+        st = coa_crypto.verified.take_certificate(self.crypto_key())
+        if st is None:
+            vp = np.array([list(bytes(pk)) for pk, _ in self.votes], np.uint8).reshape(-1, 32)
+            vs = np.array([list(sg.flatten()) for _, sg in self.votes], np.uint8).reshape(-1, 64)
+            st = coa_crypto.certificate_verify(h.digest_input(), h.id, h.author, h.signature.flatten(), h.round, vp,
+                                               vs, rng_seed=rng_seed)
         _raise_in_order(self, committee, st)
+
+    def crypto_key(self):
+        """Every byte the certificate's crypto verdict depends on
+        (coa_crypto.verified.certificate_key)."""
+        h = self.header
+        return coa_crypto.verified.certificate_key(
+            h.digest_input(), h.id, h.author, h.signature.flatten(), h.round,
+            b"".join(bytes(pk) for pk, _ in self.votes), b"".join(sg.flatten() for _, sg in self.votes))
 
     def verify_stepwise(self, committee, rng_seed=0):
         """The same checks through the per-primitive entry points."""

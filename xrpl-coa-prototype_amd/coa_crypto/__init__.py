@@ -31,6 +31,8 @@ import os
 
 import numpy as np
 
+from . import verified  # noqa: E402  (the verdict cache, rust/crypto/src/verified.rs)
+
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # COA_VERIFY_LIB overrides the library (A/B runs of two builds in one session)
 LIB_PATH = os.environ.get("COA_VERIFY_LIB") or os.path.join(_PKG, "lib", "libcoa_verify.so")
@@ -258,12 +260,18 @@ class Signature:
         return self.part1 + self.part2
 
     def verify(self, digest, public_key):
-        """Ok (returns None) or raises CryptoError -- Signature::verify."""
+        """Ok (returns None) or raises CryptoError -- Signature::verify.  A
+        triple the pre-verification stage already verified (Ok or Err) is
+        answered from `verified`, as rust/crypto/src/gpu.rs does; any other
+        goes to the engine (one single-signature launch)."""
         d, pk = bytes(digest), bytes(public_key)
         if len(d) != 32 or len(pk) != 32:
             raise ValueError("digest and public key are 32 bytes")
-        rc = _check(lib().coa_ed25519_verify_strict(d, pk, self.flatten()))
-        if rc != COA_OK:
+        sig = self.flatten()
+        ok = verified.take_signature(d, pk, sig)
+        if ok is None:
+            ok = engine_verify_strict(d, pk, sig) == COA_OK
+        if not ok:
             raise CryptoError("signature verification failed")
 
     @staticmethod
@@ -283,6 +291,12 @@ class Signature:
 
 
 # ----------------------------------------------------------- engine level
+def engine_verify_strict(digest, public_key, signature):
+    """One Signature::verify through the engine (coa_ed25519_verify_strict):
+    COA_OK or COA_REJECT."""
+    return _check(lib().coa_ed25519_verify_strict(bytes(digest), bytes(public_key), bytes(signature)))
+
+
 def init(n_gpus=0):
     return _check(lib().coa_init(n_gpus))
 

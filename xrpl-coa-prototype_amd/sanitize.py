@@ -26,6 +26,7 @@ WorkerPrimaryMessage::{OurBatch, OthersBatch}(digest, worker id).
 """
 import struct
 
+import numpy as np
 
 import certificates as C
 import coa_crypto
@@ -195,6 +196,81 @@ def _certificate_from(d, j):
 
 
 # ---------------------------------------------------------------------------
+def message_author(message):
+    """The authority whose connection delivered the message: the order the
+    pre-verification stage keeps (rust/primary/src/pre_verify.rs author_of)."""
+    if isinstance(message, C.Certificate):
+        return message.origin()
+    return message.author
+
+
+class PreVerifier:
+    """Mirror of rust/primary/src/pre_verify.rs: the stage between
+    PrimaryReceiverHandler::dispatch (primary/src/primary.rs:223-244) and
+    Core (primary/src/core.rs:349-389).  A window of Header / Vote /
+    Certificate messages has its crypto verified in coalesced engine calls --
+    every header and vote signature in ONE verify_strict_many call, every
+    certificate in ONE certificate_verify_many call -- and every verdict, Ok
+    and Err alike, is remembered in coa_crypto.verified, where Core's
+    unchanged one-at-a-time calls (Header.verify, Vote.verify,
+    Certificate.verify) find it: Core then makes no engine call for any
+    message the stage saw.  `verify_many` / `certificate_many` default to the
+    engine's entry points (tests pass counting stand-ins)."""
+
+    def __init__(self, verify_many=None, certificate_many=None):
+        self.verify_many = verify_many or coa_crypto.verify_strict_many
+        self.certificate_many = certificate_many or coa_crypto.certificate_verify_many
+
+    def window(self, messages):
+        messages = list(messages)
+        trip, certs = [], []
+        for m in messages:
+            if isinstance(m, C.Header):                    # Header::verify's signature (messages.rs:64-66)
+                trip.append((bytes(m.id), bytes(m.author), m.signature.flatten()))
+            elif isinstance(m, C.Vote):                    # Vote::verify's signature (messages.rs:139-141)
+                trip.append((bytes(m.digest()), bytes(m.author), m.signature.flatten()))
+            elif isinstance(m, C.Certificate) and m.header is not None:
+                certs.append(m)
+        if trip:
+            arr = [np.frombuffer(b"".join(t[i] for t in trip), np.uint8).reshape(len(trip), -1) for i in range(3)]
+            bad = self.verify_many(*arr)
+            for (d, k, sg), b in zip(trip, bad):
+                coa_crypto.verified.remember_signature(d, k, sg, int(b) == 0)
+        if certs:
+            hdr = [c.header for c in certs]
+            offs = np.zeros(len(certs) + 1, np.uint64)
+            offs[1:] = np.cumsum([len(c.votes) for c in certs])
+            vp = np.frombuffer(b"".join(bytes(pk) for c in certs for pk, _ in c.votes), np.uint8).reshape(-1, 32)
+            vs = np.frombuffer(b"".join(sg.flatten() for c in certs for _, sg in c.votes), np.uint8).reshape(-1, 64)
+            st = self.certificate_many([h.digest_input() for h in hdr],
+                                       np.frombuffer(b"".join(bytes(h.id) for h in hdr), np.uint8).reshape(-1, 32),
+                                       np.frombuffer(b"".join(bytes(h.author) for h in hdr), np.uint8).reshape(-1, 32),
+                                       np.frombuffer(b"".join(h.signature.flatten() for h in hdr),
+                                                     np.uint8).reshape(-1, 64),
+                                       np.array([h.round for h in hdr], np.uint64), vp, vs, offs)
+            for c, b in zip(certs, st):
+                coa_crypto.verified.remember_certificate(c.crypto_key(), int(b))
+        return messages
+
+
+def release_times(arrival_s, done_s, authors, per_author=True):
+    """When the pre-verification stage hands each message to Core, given when
+    it arrived, when its verdict came back and who sent it: as soon as its
+    verdict is in and every earlier message -- of the same author
+    (rust/primary/src/pre_verify.rs, per_author=True) or of anyone (the
+    round-3 stage's one FuturesOrdered, per_author=False) -- has been handed
+    on.  Messages are in arrival order."""
+    out = [0.0] * len(done_s)
+    last = {}
+    prev = float("-inf")
+    for i, (t, a) in enumerate(zip(done_s, authors)):
+        gate = last.get(a, float("-inf")) if per_author else prev
+        out[i] = max(t, gate, arrival_s[i])
+        last[a] = out[i]
+        prev = out[i]
+    return out
+
+
 class Processor:
     """worker::Processor (worker/src/processor.rs:21-55): hash, store, emit
     the digest message.  `process` takes a window of serialized
