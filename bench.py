@@ -40,12 +40,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "xrpl-coa-prototype_amd")
 sys.path.insert(0, PKG)
 
-# HIP gives a process GPU_MAX_HW_QUEUES hardware queues (4 by default) and
-# maps its streams onto them: the aggregation queue's concurrent windows
-# (secondary c4_stream / queue_round_mix) run side by side only with more of
-# them.  Read once, at HIP's initialisation, so it is set before torch or the
-# engine touch the GPU (a node process does the same).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# HIP gives a process GPU_MAX_HW_QUEUES hardware queues per priority (4 by
+# default) and maps its streams onto them.  The bench leaves it as the box has
+# it -- a node cannot rely on exporting more before its first HIP call -- and
+# records what HIP read: the aggregation queue's slots make streams with a
+# hardware queue of their own (COA_QUEUE_STREAMS, coa_queue_hip.cpp).
+HIP_ENV_AT_START = {k: os.environ.get(k, "unset") for k in ("GPU_MAX_HW_QUEUES", "COA_QUEUE_SLOTS",
+                                                            "COA_QUEUE_DIGEST_SLOTS", "COA_QUEUE_STREAMS")}
 
 # dalek algorithm field operations per verify_strict (fe_mul + fe_sq), measured
 # by oracle/_build/libcoa_oracle_count.so over the golden valid vectors.
@@ -674,6 +675,23 @@ def paced_queue(arrive_s, kind, item, vm=None, vp=None, vs=None, vexp=None, cert
     return lat[:n] * 1e-3, el.value, met
 
 
+STREAM_KINDS = {0: "plain (shared hardware queues)", 1: "CU-masked (a hardware queue each)",
+                2: "priority pools"}
+KIND_BITS = ((1, "signatures"), (2, "batches"), (4, "certificates"), (8, "digests"))
+
+
+def queue_diag(met):
+    """Where a paced run's tail comes from (coa_queue_metrics): the slowest
+    window (launch call -> outputs in host memory) with its size and kinds,
+    the longest wait for a free slot, staging reallocations, and how the
+    slots' streams were made."""
+    return {"window_ms_max": round(met["window_us_max"] * 1e-3, 3), "window_max_items": int(met["window_max_items"]),
+            "window_max_kinds": [n for b, n in KIND_BITS if met["window_max_kinds"] & b],
+            "slot_wait_ms_max": round(met["slot_wait_us_max"] * 1e-3, 3), "staging_grows": int(met["staging_grows"]),
+            "max_in_flight": int(met["max_in_flight"]), "slots": [int(met["slots_verify"]), int(met["slots_digest"])],
+            "streams": STREAM_KINDS.get(int(met["stream_kind"]), str(met["stream_kind"]))}
+
+
 def c4_stream(cpu_p50_batch_ms, rates=(1000, 4000), seconds=1.5):
     """C4 as the worker streams it (rust/worker/src/processor.rs): 508 KB
     batches arriving at a fixed rate (1,000/s = BASELINE C4's 1M tx/s of
@@ -702,11 +720,13 @@ def c4_stream(cpu_p50_batch_ms, rates=(1000, 4000), seconds=1.5):
         n = int(rate * seconds)
         arrive = np.arange(n) / rate
         lat, el, met = paced_queue(arrive, np.full(n, 2), np.arange(n) % nb, ddata=data, doff=offs, dexp=dexp)
+        if os.environ.get("COA_BENCH_DUMP"):  # per-request latencies for offline analysis
+            np.save(os.path.join(os.environ["COA_BENCH_DUMP"], f"c4_stream_{rate}.npy"), np.stack([arrive, lat]))
         out[f"rate_{rate}"] = {"batches": n, "achieved_batches_per_s": round(n / el, 1),
                                "p50_ms": round(float(np.percentile(lat, 50)), 3),
                                "p99_ms": round(float(np.percentile(lat, 99)), 3),
                                "windows": met["windows"], "mean_batches_per_window": round(n / max(1, met["windows"]), 1),
-                               "retried_windows": met["retried_windows"]}
+                               "retried_windows": met["retried_windows"], "diag": queue_diag(met)}
     if cpu_p50_batch_ms:
         out["cpu_one_core"] = {"p50_ms_per_batch": cpu_p50_batch_ms,
                                "max_batches_per_s": round(1e3 / cpu_p50_batch_ms, 1),
@@ -821,6 +841,7 @@ def _round_mix_rates(rates, seconds, per_round, kinds, items, msgs, pks, sigs, n
                          "cpu_core_run_p99_ms": round(float(np.percentile(cpu_lat[sel], 99)), 3)}
         row["queue_wait_us_p50"] = round(met["wait_us_p50"], 1)
         row["queue_wait_us_p99"] = round(met["wait_us_p99"], 1)
+        row["diag"] = queue_diag(met)
         row["cpu_saturated"] = bool(rate > cpu_max_rounds)
         out[str(rate)] = row
     return out
@@ -990,16 +1011,21 @@ def load_pmc(n):
     return pj, None
 
 
-def timed_steps(step, steps, warmup, world, dist, sync):
+def timed_steps(step, steps, warmup, world, dist, sync, before_timed=None):
     """The contract's timed region: `warmup` untimed steps, then exactly
     `steps` steps bracketed by a barrier + device sync on both sides; returns
     the MAX over ranks of the elapsed seconds (gloo all-reduce, control only:
-    no data-path collective)."""
+    no data-path collective).  before_timed() runs after the warmup, outside
+    the clock (the bench resets the verdicts there, so the check after the
+    timed steps sees only what they wrote)."""
     import sharding
 
     for _ in range(warmup):
         step(None)
     sync()
+    if before_timed:
+        before_timed()
+        sync()
     if world > 1:
         dist.barrier()
     sync()
@@ -1174,7 +1200,6 @@ def main():
     torch.cuda.synchronize()
     if int(verdicts.sum().item()) != 0:
         raise SystemExit("engine rejected valid benchmark signatures")
-    verdicts.fill_(1)
     # clock settle: right after setup the GPU has been mostly idle (host-side
     # signing and copies), and the first ~0.1 s of back-to-back calls run a
     # few percent slower than the same calls later in the process; the timed
@@ -1184,7 +1209,10 @@ def main():
         for _ in range(8):
             step(None)
         torch.cuda.synchronize()
-    elapsed = timed_steps(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize)
+    # every verdict set to Err right before the timed steps: verdicts_ok then
+    # reports what the timed calls themselves wrote
+    elapsed = timed_steps(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize,
+                          before_timed=lambda: verdicts.fill_(1))
     if args.per_call_events:
         verify_ms = sum(a.elapsed_time(b) for a, b in per_call) / args.steps
     else:
@@ -1287,6 +1315,7 @@ def main():
                        "triples_per_gpu": n, "parallelism": f"index-range shards x{world}"},
             "kernel_ms": {"verify_call": round(verify_ms, 4)},
             "verdicts_ok": ok,
+            "env": HIP_ENV_AT_START,
             "roofline": roof,
             "cpu_baseline": cpu,
             "secondary": secondary,

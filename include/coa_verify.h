@@ -296,21 +296,25 @@ int coa_ed25519_sign_many_device(int device, const uint8_t* d_seeds, const uint8
 
 /* ------------------------------------------------ aggregation queue (f1)
  * Pre-verification stage for Core::run (primary/src/core.rs:349-389), which
- * verifies one message at a time: producers submit header/vote signatures
- * and certificate vote batches; the queue's worker thread coalesces them into
- * coa_ed25519_verify_strict_many / coa_ed25519_verify_batch_groups launches
- * (when max_batch signatures are pending, when the oldest request is
- * max_delay_us old, or on flush) and replies per request through the
- * callback -- the SignatureService request/oneshot idiom of
+ * verifies one message at a time: producers submit header/vote signatures,
+ * vote batches, certificates and worker batch digests; the queue coalesces
+ * them into launches (when max_batch items are pending, when the oldest
+ * request is max_delay_us old, or on flush) and replies per request through
+ * the callback -- the SignatureService request/oneshot idiom of
  * crypto/src/lib.rs:222-250.  Inputs are copied at submission (into one of
- * a fixed pool of intake shards, chosen by the calling thread).  A collector
- * thread launches each window on the next of four device slots per GPU (COA_QUEUE_SLOTS)
- * (pinned staging, own stream) without waiting for the previous window, and
- * a completion thread answers windows in order: the callback runs there with
- * status (COA_OK or a negative engine error) and the request's verdict
- * byte(s).  coa_committee_register waits for in-flight windows that read the
- * committee key cache (certificate windows) and holds new ones back until it
- * has finished, so registration stays verdict-neutral under load. */
+ * a fixed pool of intake shards, chosen by the calling thread).  Two lanes,
+ * each with its own collector, device slots and completion thread: one for
+ * signatures, vote batches and certificates, one for digests (a digest
+ * window is a 14 ms serial chain; it never delays a verdict).  A lane's
+ * collector launches each window on a free slot (four per GPU per lane,
+ * COA_QUEUE_SLOTS / COA_QUEUE_DIGEST_SLOTS; pinned staging, its own stream
+ * on its own hardware queue, COA_QUEUE_STREAMS) without waiting for the
+ * previous window, and its completion thread answers windows in order: the
+ * callback runs there with status (COA_OK or a negative engine error) and
+ * the request's verdict byte(s).  Windows that read the committee key cache
+ * pin the generation they launched with; coa_committee_register builds the
+ * next generation beside it, so registration neither waits for nor holds
+ * back a window and stays verdict-neutral under load. */
 typedef struct coa_queue coa_queue;
 typedef void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n);
 coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us);
@@ -369,7 +373,30 @@ typedef struct {
   uint64_t retried_windows;   /* windows whose launch failed and were re-run */
   uint64_t recovered_windows; /* ... of which a re-run succeeded */
   uint64_t failed_windows;    /* windows answered with an engine error */
+  /* where a tail comes from: the slowest window from its launch call (the
+   * collector hands it to a slot) to its outputs in host memory, with its
+   * size and kinds; the longest a launch waited for a free slot; staging
+   * reallocations (page-locked or device allocations on the launch path) */
+  double window_us_max;
+  uint64_t window_max_items;
+  uint32_t window_max_kinds;  /* COA_QUEUE_KIND_* bits */
+  int32_t stream_kind;        /* COA_QUEUE_STREAM_*: how the slots' streams were made */
+  double slot_wait_us_max;
+  uint64_t staging_grows;
+  uint32_t slots_verify, slots_digest; /* device slots of each lane, over all devices */
 } coa_queue_metrics_t;
+#define COA_QUEUE_KIND_SIGNATURES 1u
+#define COA_QUEUE_KIND_BATCHES 2u
+#define COA_QUEUE_KIND_CERTIFICATES 4u
+#define COA_QUEUE_KIND_DIGESTS 8u
+/* COA_QUEUE_STREAMS=plain|cumask|priority (read at the first launch): plain
+ * streams share the process's GPU_MAX_HW_QUEUES hardware queues (HIP's
+ * default 4) with every other stream of the process; CU-masked streams (all
+ * CUs enabled) get a hardware queue each, whatever GPU_MAX_HW_QUEUES says;
+ * priority streams come from the high-priority pool (verify lane) */
+#define COA_QUEUE_STREAM_PLAIN 0
+#define COA_QUEUE_STREAM_CUMASK 1
+#define COA_QUEUE_STREAM_PRIORITY 2
 int coa_queue_metrics(coa_queue* q, coa_queue_metrics_t* out);
 int coa_queue_destroy(coa_queue* q);
 

@@ -55,6 +55,14 @@ pub struct CoaQueueMetrics {
     pub retried_windows: u64,
     pub recovered_windows: u64,
     pub failed_windows: u64,
+    pub window_us_max: f64,
+    pub window_max_items: u64,
+    pub window_max_kinds: u32,
+    pub stream_kind: i32,
+    pub slot_wait_us_max: f64,
+    pub staging_grows: u64,
+    pub slots_verify: u32,
+    pub slots_digest: u32,
 }
 
 /// void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n)

@@ -102,7 +102,7 @@ class StubBackend : public coa_q::Backend {
 };
 }  // namespace
 
-coa_q::Backend* coa_q::make_backend() { return new StubBackend(); }
+coa_q::Backend* coa_q::make_backend(int) { return new StubBackend(); }
 
 // -------------------------------------------------------------- producers
 struct Req {

@@ -57,7 +57,11 @@ class QueueMetrics(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("requests", "windows", "signatures", "batches", "certificates",
                                                "digests", "max_window", "max_in_flight", "max_pending")] + \
                [(n, ctypes.c_double) for n in ("wait_us_mean", "wait_us_p50", "wait_us_p99", "wait_us_max")] + \
-               [(n, ctypes.c_uint64) for n in ("retried_windows", "recovered_windows", "failed_windows")]
+               [(n, ctypes.c_uint64) for n in ("retried_windows", "recovered_windows", "failed_windows")] + \
+               [("window_us_max", ctypes.c_double), ("window_max_items", ctypes.c_uint64),
+                ("window_max_kinds", ctypes.c_uint32), ("stream_kind", ctypes.c_int32),
+                ("slot_wait_us_max", ctypes.c_double), ("staging_grows", ctypes.c_uint64),
+                ("slots_verify", ctypes.c_uint32), ("slots_digest", ctypes.c_uint32)]
 
 
 # void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n)

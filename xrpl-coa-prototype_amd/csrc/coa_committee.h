@@ -85,14 +85,17 @@ struct CertInl {
 };
 hipError_t coa_launch_cert_verify_inl(const CertInl& ci, hipStream_t s);
 
-// Key-cache read gate of HIP device `device` (coa_runtime.cpp).  The
-// aggregation queue holds it from a certificate window's launch to that
-// window's completion (the kernels read the key tables asynchronously);
-// coa_committee_register waits until no window holds it and keeps new
-// windows out until the tables are rebuilt.  Release may come from another
-// thread than the acquire.
-extern "C" void coa_keycache_read_acquire(int device);
-extern "C" void coa_keycache_read_release(int device);
+// Committee key-cache generations of HIP device `device` (coa_runtime.cpp).
+// coa_committee_register builds a new generation of the key tables while
+// every call and queue window keeps reading the one it started with, swaps
+// it in, and frees the old one once nothing holds it -- so registration
+// never waits for a window and never holds one back.  The aggregation queue
+// pins the current generation from a window's launch to its completion (the
+// kernels read the tables asynchronously) and has its launches read that
+// pinned generation (coa_keycache_use on the launching thread).
+extern "C" void* coa_keycache_pin(int device);  // opaque handle (null: device not open)
+extern "C" void coa_keycache_unpin(void* pin);  // any thread; null is a no-op
+extern "C" void coa_keycache_use(void* pin);    // this thread's launches read `pin` (null: the current one)
 
 hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s);
 hipError_t coa_launch_key_tables(const uint32_t* keys, uint32_t nk, uint32_t* tabs, hipStream_t s);

@@ -37,13 +37,20 @@
 //               never fails for a reason other than the signature, and
 //               Core::run logs every error and continues
 //               (primary/src/core.rs:390-398).
+// Lanes: all of the above exists twice -- one lane for signatures, vote
+// batches and certificates, one for worker-batch digests -- each with its own
+// shards, collector, backend slots and completer.  A digest window is a 14 ms
+// serial SHA-512 chain per batch; in a shared window, slot or completion
+// order it would hold every verdict behind it for that long.
 // The backend (coa_queue.h) is the HIP one (coa_queue_hip.cpp) or, in the
 // sanitizer and CPU tests, a stub.
 //
 // Metrics (coa_queue_metrics): per-kind request counts, window sizes,
-// windows in flight, pending depth, retried / recovered / failed windows and
-// the submit -> callback wait time of every request (mean, max, p50/p99 from
-// a log-spaced histogram) -- the numbers needed to tune max_batch /
+// windows in flight, pending depth, retried / recovered / failed windows, the
+// submit -> callback wait time of every request (mean, max, p50/p99 from a
+// log-spaced histogram), and where a tail comes from: the slowest window's
+// launch -> completion time with its size and kinds, the longest wait for a
+// free slot, staging reallocations -- the numbers needed to tune max_batch /
 // max_delay_us against the serial Core::run.
 #include <algorithm>
 #include <atomic>
@@ -107,6 +114,7 @@ struct Part {
 struct Flight {
   std::vector<Part> parts;
   Launch L;
+  int64_t t_launch = 0;  // ns, when the collector handed the window to the backend
 };
 
 std::atomic<uint64_t> g_queue_ids{1};
@@ -211,13 +219,11 @@ struct AnswerPool {
   }
 };
 
-}  // namespace
-
-struct coa_queue {
+// One lane of a queue: intake shards, collector, backend slots, completer.
+struct Lane {
   size_t max_batch = 65536;
   std::chrono::microseconds max_delay{500};
   std::unique_ptr<coa_q::Backend> be;
-  const uint64_t id = g_queue_ids.fetch_add(1);
   std::unique_ptr<Shard[]> shards{new Shard[kShards]};
 
   std::mutex mu;
@@ -238,6 +244,11 @@ struct coa_queue {
   std::atomic<int64_t> m_max_pending{0};
   double m_wait_sum = 0.0, m_wait_max = 0.0;
   uint64_t m_hist[HB] = {};
+  // the slowest window (launch call -> outputs in host memory) and the
+  // longest wait for a free slot
+  double m_window_us_max = 0.0, m_slot_wait_us_max = 0.0;
+  uint64_t m_window_max_items = 0;
+  uint32_t m_window_max_kinds = 0;
 
   std::thread collector, completer;
   AnswerPool helpers;  // started lazily by the first large launch
@@ -247,7 +258,7 @@ struct coa_queue {
   // closes at once while fewer than this many windows are in flight
   size_t idle_launch = 0;
 
-  coa_queue() {
+  Lane() {
     for (size_t i = 0; i < kShards; i++) {
       shards[i].w.reset(new Window());
       shards[i].w->reset();
@@ -343,6 +354,7 @@ struct coa_queue {
       l.unlock();
       f.L.reset_outputs();
       f.L.attempts = 1;
+      f.t_launch = now_ns();
       be->launch(f.L);  // stages and enqueues; blocks only while every slot is busy
       l.lock();
       m_windows++;
@@ -377,6 +389,7 @@ struct coa_queue {
       flight.pop_front();
       l.unlock();
       be->complete(f.L);
+      const double window_us = (double)(now_ns() - f.t_launch) * 1e-3;
       const bool retried = recoverable(f.L.rc);
       if (retried) recover(f.L);
       const int rc = f.L.rc;
@@ -455,6 +468,12 @@ struct coa_queue {
         m_retried++;
         if (rc == COA_OK) m_recovered++;
       }
+      if (window_us > m_window_us_max) {
+        m_window_us_max = window_us;
+        m_window_max_items = f.L.items();
+        m_window_max_kinds = f.L.kinds();
+      }
+      m_slot_wait_us_max = std::max(m_slot_wait_us_max, (double)f.L.slot_wait_ns * 1e-3);
       if (rc != COA_OK) m_failed++;
       busy--;
       if (busy == 0 && pend.load() <= 0) idle_cv.notify_all();
@@ -462,22 +481,51 @@ struct coa_queue {
     }
   }
 
-  double percentile(double q) const {  // under mu
-    uint64_t total = 0;
-    for (uint64_t c : m_hist) total += c;
-    if (total == 0) return 0.0;
-    const double want = q * (double)total;
-    uint64_t run = 0;
-    for (int b = 0; b < HB; b++) {
-      run += m_hist[b];
-      if ((double)run >= want) return bucket_mid(b);
+  void shutdown() {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      stop = true;
+      cv.notify_one();
     }
-    return bucket_mid(HB - 1);
+    collector.join();
+    completer.join();
+  }
+
+  int flush_all() {
+    std::unique_lock<std::mutex> l(mu);
+    if (pend.load() <= 0 && busy == 0) return COA_OK;
+    if (pend.load() > 0) {
+      flush = true;
+      cv.notify_one();
+    }
+    idle_cv.wait(l, [&] { return pend.load() <= 0 && busy == 0; });
+    return COA_OK;
   }
 };
 
+double hist_percentile(const uint64_t* hist, double q) {
+  uint64_t total = 0;
+  for (int b = 0; b < HB; b++) total += hist[b];
+  if (total == 0) return 0.0;
+  const double want = q * (double)total;
+  uint64_t run = 0;
+  for (int b = 0; b < HB; b++) {
+    run += hist[b];
+    if ((double)run >= want) return bucket_mid(b);
+  }
+  return bucket_mid(HB - 1);
+}
+
+}  // namespace
+
+struct coa_queue {
+  const uint64_t id = g_queue_ids.fetch_add(1);
+  Lane lanes[coa_q::LANES];
+  Lane& lane_of(Kind k) { return lanes[k == K_DIGEST ? coa_q::LANE_DIGEST : coa_q::LANE_VERIFY]; }
+};
+
 namespace {
-void submitted(coa_queue* q, Shard& sh, std::unique_lock<std::mutex>& sl, Kind kind, uint32_t idx, uint32_t n,
+void submitted(Lane* q, Shard& sh, std::unique_lock<std::mutex>& sl, Kind kind, uint32_t idx, uint32_t n,
                coa_verdict_cb cb, void* user, size_t items) {
   sh.reqs.push_back(Req{cb, user, now_ns(), idx, n, kind});
   sh.items += items;
@@ -502,60 +550,65 @@ extern "C" {
 
 coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
   coa_queue* q = new coa_queue();
-  q->max_batch = max_batch ? max_batch : 65536;
-  q->max_delay = std::chrono::microseconds(max_delay_us);
-  if (const char* e = getenv("COA_QUEUE_HELPERS")) q->n_helpers = std::max(0, std::min(15, atoi(e)));
-  if (const char* e = getenv("COA_QUEUE_IDLE_LAUNCH")) q->idle_launch = (size_t)std::max(0, std::min(64, atoi(e)));
-  q->be.reset(coa_q::make_backend());
-  q->start();
+  for (int k = 0; k < coa_q::LANES; k++) {
+    Lane& L = q->lanes[k];
+    L.max_batch = max_batch ? max_batch : 65536;
+    L.max_delay = std::chrono::microseconds(max_delay_us);
+    if (const char* e = getenv("COA_QUEUE_HELPERS")) L.n_helpers = std::max(0, std::min(15, atoi(e)));
+    if (const char* e = getenv("COA_QUEUE_IDLE_LAUNCH")) L.idle_launch = (size_t)std::max(0, std::min(64, atoi(e)));
+    L.be.reset(coa_q::make_backend(k));
+    L.be->prepare();
+    L.start();
+  }
   return q;
 }
 
-// The submissions: the request goes into the calling thread's shard under
-// that shard's lock; then the queue's pending count (and, on an edge, the
-// collector) learns of it.
-#define COA_Q_INTAKE(q)                        \
-  Shard& sh = (q)->my_shard();                 \
+// The submissions: the request goes into the calling thread's shard of the
+// kind's lane under that shard's lock; then the lane's pending count (and, on
+// an edge, its collector) learns of it.
+#define COA_Q_INTAKE(q, kind)                  \
+  Lane* ln = &(q)->lane_of(kind);              \
+  Shard& sh = ln->my_shard();                  \
   std::unique_lock<std::mutex> sl(sh.mu);      \
-  if ((q)->stop.load()) return COA_EINVAL;     \
+  if (ln->stop.load()) return COA_EINVAL;      \
   Window& w = *sh.w;
 
 
 int coa_queue_submit_verify(coa_queue* q, const uint8_t msg[32], const uint8_t pk[32], const uint8_t sig[64],
                             coa_verdict_cb cb, void* user) {
   if (!q || !msg || !pk || !sig || !cb) return COA_EINVAL;
-  COA_Q_INTAKE(q)
+  COA_Q_INTAKE(q, K_VERIFY)
   put<32>(w.v_msgs, msg);
   put<32>(w.v_pks, pk);
   put<64>(w.v_sigs, sig);
-  submitted(q, sh, sl, K_VERIFY, (uint32_t)w.nv++, 1, cb, user, 1);
+  submitted(ln, sh, sl, K_VERIFY, (uint32_t)w.nv++, 1, cb, user, 1);
   return COA_OK;
 }
 
 int coa_queue_submit_verify_many(coa_queue* q, const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, size_t n,
                                  coa_verdict_cb cb, void* user) {
   if (!q || !cb || n == 0 || n > UINT32_MAX || !msgs || !pks || !sigs) return COA_EINVAL;
-  COA_Q_INTAKE(q)
+  COA_Q_INTAKE(q, K_VERIFY)
   w.v_msgs.insert(w.v_msgs.end(), msgs, msgs + n * 32);
   w.v_pks.insert(w.v_pks.end(), pks, pks + n * 32);
   w.v_sigs.insert(w.v_sigs.end(), sigs, sigs + n * 64);
   const uint32_t idx = (uint32_t)w.nv;
   w.nv += n;
-  submitted(q, sh, sl, K_VERIFY, idx, (uint32_t)n, cb, user, n);
+  submitted(ln, sh, sl, K_VERIFY, idx, (uint32_t)n, cb, user, n);
   return COA_OK;
 }
 
 int coa_queue_submit_batch(coa_queue* q, const uint8_t msg[32], const uint8_t* pks, const uint8_t* sigs, size_t n,
                            coa_verdict_cb cb, void* user) {
   if (!q || !msg || (n && (!pks || !sigs)) || !cb) return COA_EINVAL;
-  COA_Q_INTAKE(q)
+  COA_Q_INTAKE(q, K_BATCH)
   put<32>(w.g_msgs, msg);
   if (n) {
     w.g_pks.insert(w.g_pks.end(), pks, pks + n * 32);
     w.g_sigs.insert(w.g_sigs.end(), sigs, sigs + n * 64);
   }
   w.g_offs.push_back(w.g_offs.back() + n);
-  submitted(q, sh, sl, K_BATCH, (uint32_t)w.ng++, 1, cb, user, n ? n : 1);
+  submitted(ln, sh, sl, K_BATCH, (uint32_t)w.ng++, 1, cb, user, n ? n : 1);
   return COA_OK;
 }
 
@@ -566,7 +619,7 @@ int coa_queue_submit_certificate(coa_queue* q, const uint8_t* header_data, size_
   if (!q || (header_len && !header_data) || !id || !origin || !header_sig || (n_votes && (!vote_pks || !vote_sigs)) ||
       !cb)
     return COA_EINVAL;
-  COA_Q_INTAKE(q)
+  COA_Q_INTAKE(q, K_CERT)
   if (header_len) w.c_hdata.insert(w.c_hdata.end(), header_data, header_data + header_len);
   w.c_hoff.push_back(w.c_hdata.size());
   put<32>(w.c_ids, id);
@@ -578,87 +631,101 @@ int coa_queue_submit_certificate(coa_queue* q, const uint8_t* header_data, size_
     w.c_sigs.insert(w.c_sigs.end(), vote_sigs, vote_sigs + n_votes * 64);
   }
   w.c_voff.push_back(w.c_voff.back() + n_votes);
-  submitted(q, sh, sl, K_CERT, (uint32_t)w.nc++, 1, cb, user, 1 + n_votes);
+  submitted(ln, sh, sl, K_CERT, (uint32_t)w.nc++, 1, cb, user, 1 + n_votes);
   return COA_OK;
 }
 
 int coa_queue_submit_digest(coa_queue* q, const uint8_t* data, size_t len, coa_verdict_cb cb, void* user) {
   if (!q || (len && !data) || !cb) return COA_EINVAL;
-  COA_Q_INTAKE(q)
+  COA_Q_INTAKE(q, K_DIGEST)
   if (len) w.d_data.insert(w.d_data.end(), data, data + len);
   w.d_offs.push_back(w.d_data.size());
-  submitted(q, sh, sl, K_DIGEST, (uint32_t)w.nd++, 1, cb, user, 1);
+  submitted(ln, sh, sl, K_DIGEST, (uint32_t)w.nd++, 1, cb, user, 1);
   return COA_OK;
 }
 
 int coa_queue_flush(coa_queue* q) {
   if (!q) return COA_EINVAL;
-  std::unique_lock<std::mutex> l(q->mu);
-  if (q->pend.load() <= 0 && q->busy == 0) return COA_OK;
-  if (q->pend.load() > 0) {
-    q->flush = true;
-    q->cv.notify_one();
-  }
-  q->idle_cv.wait(l, [&] { return q->pend.load() <= 0 && q->busy == 0; });
+  for (Lane& L : q->lanes) L.flush_all();
   return COA_OK;
 }
 
 int coa_queue_set_idle_launch(coa_queue* q, uint32_t windows_in_flight) {
   if (!q || windows_in_flight > 64) return COA_EINVAL;
-  std::lock_guard<std::mutex> l(q->mu);
-  q->idle_launch = windows_in_flight;
-  q->cv.notify_one();  // an open window may close now
+  for (Lane& L : q->lanes) {
+    std::lock_guard<std::mutex> l(L.mu);
+    L.idle_launch = windows_in_flight;
+    L.cv.notify_one();  // an open window may close now
+  }
   return COA_OK;
 }
 
 int coa_queue_stats(coa_queue* q, uint64_t* launches, uint64_t* items, uint64_t* groups) {
   if (!q) return COA_EINVAL;
-  std::lock_guard<std::mutex> l(q->mu);
-  if (launches) *launches = q->m_windows;
-  if (items) *items = q->m_sig;
-  if (groups) *groups = q->m_batch + q->m_cert;
+  uint64_t w = 0, it = 0, g = 0;
+  for (Lane& L : q->lanes) {
+    std::lock_guard<std::mutex> l(L.mu);
+    w += L.m_windows;
+    it += L.m_sig;
+    g += L.m_batch + L.m_cert;
+  }
+  if (launches) *launches = w;
+  if (items) *items = it;
+  if (groups) *groups = g;
   return COA_OK;
 }
 
 int coa_queue_digest_count(coa_queue* q, uint64_t* digests) {
   if (!q || !digests) return COA_EINVAL;
-  std::lock_guard<std::mutex> l(q->mu);
-  *digests = q->m_dig;
+  Lane& L = q->lanes[coa_q::LANE_DIGEST];
+  std::lock_guard<std::mutex> l(L.mu);
+  *digests = L.m_dig;
   return COA_OK;
 }
 
 int coa_queue_metrics(coa_queue* q, coa_queue_metrics_t* out) {
   if (!q || !out) return COA_EINVAL;
-  std::lock_guard<std::mutex> l(q->mu);
-  out->requests = q->m_requests;
-  out->windows = q->m_windows;
-  out->signatures = q->m_sig;
-  out->batches = q->m_batch;
-  out->certificates = q->m_cert;
-  out->digests = q->m_dig;
-  out->max_window = q->m_max_window;
-  out->max_in_flight = q->m_max_in_flight;
-  out->max_pending = (uint64_t)std::max<int64_t>(0, q->m_max_pending.load());
-  out->wait_us_mean = q->m_requests ? q->m_wait_sum / (double)q->m_requests : 0.0;
-  out->wait_us_p50 = q->percentile(0.50);
-  out->wait_us_p99 = q->percentile(0.99);
-  out->wait_us_max = q->m_wait_max;
-  out->retried_windows = q->m_retried;
-  out->recovered_windows = q->m_recovered;
-  out->failed_windows = q->m_failed;
+  std::memset(out, 0, sizeof(*out));
+  uint64_t hist[HB] = {};
+  double wsum = 0.0;
+  for (int k = 0; k < coa_q::LANES; k++) {
+    Lane& L = q->lanes[k];
+    std::lock_guard<std::mutex> l(L.mu);
+    out->requests += L.m_requests;
+    out->windows += L.m_windows;
+    out->signatures += L.m_sig;
+    out->batches += L.m_batch;
+    out->certificates += L.m_cert;
+    out->digests += L.m_dig;
+    out->max_window = std::max<uint64_t>(out->max_window, L.m_max_window);
+    out->max_in_flight = std::max<uint64_t>(out->max_in_flight, L.m_max_in_flight);
+    out->max_pending = std::max<uint64_t>(out->max_pending, (uint64_t)std::max<int64_t>(0, L.m_max_pending.load()));
+    for (int b = 0; b < HB; b++) hist[b] += L.m_hist[b];
+    wsum += L.m_wait_sum;
+    out->wait_us_max = std::max(out->wait_us_max, L.m_wait_max);
+    out->retried_windows += L.m_retried;
+    out->recovered_windows += L.m_recovered;
+    out->failed_windows += L.m_failed;
+    if (L.m_window_us_max > out->window_us_max) {
+      out->window_us_max = L.m_window_us_max;
+      out->window_max_items = L.m_window_max_items;
+      out->window_max_kinds = L.m_window_max_kinds;
+    }
+    out->slot_wait_us_max = std::max(out->slot_wait_us_max, L.m_slot_wait_us_max);
+    out->staging_grows += L.be->grows();
+    out->stream_kind = std::max(out->stream_kind, (int32_t)L.be->stream_kind());
+    (k == coa_q::LANE_DIGEST ? out->slots_digest : out->slots_verify) = (uint32_t)L.be->slots();
+  }
+  out->wait_us_mean = out->requests ? wsum / (double)out->requests : 0.0;
+  out->wait_us_p50 = hist_percentile(hist, 0.50);
+  out->wait_us_p99 = hist_percentile(hist, 0.99);
   return COA_OK;
 }
 
 int coa_queue_destroy(coa_queue* q) {
   if (!q) return COA_EINVAL;
   coa_queue_flush(q);
-  {
-    std::lock_guard<std::mutex> l(q->mu);
-    q->stop = true;
-    q->cv.notify_one();
-  }
-  q->collector.join();
-  q->completer.join();
+  for (Lane& L : q->lanes) L.shutdown();
   delete q;
   return COA_OK;
 }

@@ -75,6 +75,12 @@ struct Launch {
   int rc = COA_OK;     // engine status (negative = failure), set by the backend
   int slot = -1;       // backend slot the launch ran on
   int attempts = 0;    // launches of this window (1 + retries)
+  int64_t slot_wait_ns = 0;  // how long launch() waited for a free slot (set by the backend)
+  // COA_QUEUE_KIND_* bits of the kinds the launch holds
+  uint32_t kinds() const {
+    return (nv ? COA_QUEUE_KIND_SIGNATURES : 0u) | (ng ? COA_QUEUE_KIND_BATCHES : 0u) |
+           (nc ? COA_QUEUE_KIND_CERTIFICATES : 0u) | (nd ? COA_QUEUE_KIND_DIGESTS : 0u);
+  }
   void tally() {
     nv = ng = nc = nd = nvotes = hbytes = dbytes = gvotes = 0;
     for (const Window* w : parts) {
@@ -117,9 +123,22 @@ class Backend {
   virtual int slots() const = 0;
   // Number of device contexts retries can go to (at least 1).
   virtual int devices() const = 0;
+  // Sets the slots up (streams, staging) before the first window: called once
+  // at queue creation, so no request pays for it.
+  virtual void prepare() {}
+  // Staging reallocations so far (each a page-locked or device allocation).
+  virtual uint64_t grows() const { return 0; }
+  // How the slots' streams were made (COA_QUEUE_STREAM_*).
+  virtual int stream_kind() const { return 0; }
 };
 
-// The HIP backend (coa_queue_hip.cpp), or a test stub.
-Backend* make_backend();
+// The queue's lanes: signature, vote-batch and certificate windows
+// (latency-bound, ~0.1-1 ms on the device) and worker-batch digest windows
+// (a 14 ms serial SHA-512 chain per batch) never share a window, a slot, a
+// stream or a completion order.
+enum LaneId { LANE_VERIFY = 0, LANE_DIGEST = 1, LANES = 2 };
+
+// The HIP backend (coa_queue_hip.cpp), or a test stub, for one lane.
+Backend* make_backend(int lane);
 
 }  // namespace coa_q

@@ -1,9 +1,22 @@
-// HIP launch backend of the aggregation queue (coa_queue.h): device slots
-// (four per opened GPU context by default: a committee-100 round mix at
-// 1,000 rounds/s has p99 1.9 ms with four, 7.6 ms with two; streamed worker
-// batches need them with GPU_MAX_HW_QUEUES >= 8, bench.py
-// secondary.c4_stream), each with its own non-blocking
-// stream, event, page-locked staging and device buffers.  launch() packs the
+// HIP launch backend of the aggregation queue (coa_queue.h), one per lane:
+// device slots (four per opened GPU context and lane by default:
+// COA_QUEUE_SLOTS for the verify lane, COA_QUEUE_DIGEST_SLOTS for the digest
+// lane), each with its own stream, event, page-locked staging and device
+// buffers.
+//
+// Hardware queues.  HIP gives a process GPU_MAX_HW_QUEUES hardware queues
+// per priority (4 by default, and a node cannot rely on exporting more
+// before its first HIP call) and maps every stream onto them; streams that
+// share a hardware queue run one after another.  With the engine's context
+// streams, a host's own streams and eight slots on four queues, a 14 ms
+// digest window would sit in front of a certificate window (round 3:
+// queue_round_mix p99 7.2-7.7 ms and c4_stream 4,000/s p50 94 ms on a box
+// with the default 4).  So a slot's stream is made to get a hardware queue
+// of its own (COA_QUEUE_STREAMS, tools/hwq_probe.hip measures which kind
+// does): "cumask" (the default) -- hipExtStreamCreateWithCUMask with every
+// CU enabled: HIP never shares a CU-masked stream's queue, whatever
+// GPU_MAX_HW_QUEUES says; "priority" -- the high-priority pool (its own 4
+// queues) for the verify lane; "plain" -- shared queues (the round-3 form).  launch() packs the
 // launch's parts (one per intake shard) straight into one pinned block --
 // the parts are never merged first -- issues ONE host-to-device copy, the
 // engine's device-resident entry points (asynchronous with an explicit
@@ -40,6 +53,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -57,8 +72,15 @@ namespace {
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+struct Grave {  // an outgrown staging buffer (see grow_pinned)
+  void* p;
+  bool pinned;
+};
+
 struct Slot {
   int dev = -1;
+  int kind = COA_QUEUE_STREAM_PLAIN;  // how its stream is made
+  int lane = 0;
   hipStream_t s = nullptr;
   hipEvent_t ev = nullptr;
   void* hin = nullptr;   // pinned input block
@@ -67,33 +89,48 @@ struct Slot {
   void* dout = nullptr;  // device output block
   void* ws = nullptr;    // device workspace (verify + certificates)
   size_t cap_hin = 0, cap_hout = 0, cap_din = 0, cap_dout = 0, cap_ws = 0;
+  std::vector<Grave> grave;  // outgrown staging, freed with the slot
   bool busy = false;
   bool launched = false;  // device work was enqueued (complete() must drain it)
-  bool gate = false;      // holds the device's key-cache read gate
+  void* keys = nullptr;   // the key-cache generation the launch pinned (coa_keycache_pin)
   bool lat = false;       // the launch's signatures took the latency kernel (result words)
   // output offsets of the current launch
   size_t o_v = 0, o_c = 0, o_d = 0;
 };
 
-hipError_t grow_pinned(void*& p, size_t& cap, size_t want) {
+std::atomic<uint64_t> g_grows{0};  // staging reallocations (all backends)
+
+// A slot's staging grows geometrically (twice what a window needs) and an
+// outgrown buffer is not freed on the launch path: hipFree / hipHostFree wait
+// for the whole device, i.e. for every other slot's window in flight (round
+// 4: a 3-batch digest window took 136 ms behind its lane's regrowths at
+// 4,000 batches/s).  Outgrown buffers go to the slot's graveyard, freed with
+// the slot; the geometric growth bounds them to the final size.
+hipError_t grow_pinned(void*& p, size_t& cap, size_t want, std::vector<Grave>& grave) {
   if (want <= cap) return hipSuccess;
-  if (p) (void)hipHostFree(p);
+  g_grows++;
+  if (p) grave.push_back({p, true});
   p = nullptr;
   cap = 0;
-  want = want + want / 4 + 4096;
+  want = 2 * want + 4096;
   hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
   if (e == hipSuccess) cap = want;
   return e;
 }
-hipError_t grow_dev(void*& p, size_t& cap, size_t want) {
+hipError_t grow_dev(void*& p, size_t& cap, size_t want, std::vector<Grave>& grave) {
   if (want <= cap) return hipSuccess;
-  if (p) (void)hipFree(p);
+  g_grows++;
+  if (p) grave.push_back({p, false});
   p = nullptr;
   cap = 0;
-  want = want + want / 4 + 4096;
+  want = 2 * want + 4096;
   hipError_t e = hipMalloc(&p, want);
   if (e == hipSuccess) cap = want;
   return e;
+}
+void bury(std::vector<Grave>& grave) {
+  for (const Grave& g : grave) (void)(g.pinned ? hipHostFree(g.p) : hipFree(g.p));
+  grave.clear();
 }
 
 // New stream and event for a slot; its device buffers are freed (regrown by
@@ -115,11 +152,34 @@ int make_stream(Slot& sl) {
       *p = nullptr;
     }
   sl.cap_din = sl.cap_dout = sl.cap_ws = 0;
+  bury(sl.grave);
   (void)hipGetLastError();  // a failed launch's error is not sticky for the new stream
-  if (hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess)
-    return COA_EHIP;
+  hipError_t e;
+  if (sl.kind == COA_QUEUE_STREAM_CUMASK) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, sl.dev) != hipSuccess || cus <= 0)
+      return COA_EHIP;
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+    for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
+    e = hipExtStreamCreateWithCUMask(&sl.s, (uint32_t)mask.size(), mask.data());
+  } else if (sl.kind == COA_QUEUE_STREAM_PRIORITY) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return COA_EHIP;
+    e = hipStreamCreateWithPriority(&sl.s, hipStreamNonBlocking, sl.lane == coa_q::LANE_VERIFY ? greatest : least);
+  } else {
+    e = hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking);
+  }
+  if (e != hipSuccess || hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) return COA_EHIP;
   return COA_OK;
+}
+
+int stream_kind_env() {
+  const char* e = getenv("COA_QUEUE_STREAMS");
+  if (!e) return COA_QUEUE_STREAM_CUMASK;
+  const std::string v(e);
+  if (v == "plain") return COA_QUEUE_STREAM_PLAIN;
+  if (v == "priority") return COA_QUEUE_STREAM_PRIORITY;
+  return COA_QUEUE_STREAM_CUMASK;
 }
 
 void free_slot(Slot& sl) {
@@ -133,10 +193,12 @@ void free_slot(Slot& sl) {
   if (sl.ws) (void)hipFree(sl.ws);
   if (sl.ev) (void)hipEventDestroy(sl.ev);
   if (sl.s) (void)hipStreamDestroy(sl.s);
+  bury(sl.grave);
 }
 
 class HipBackend : public coa_q::Backend {
  public:
+  explicit HipBackend(int lane) : lane_(lane) {}
   ~HipBackend() override {
     for (Slot& sl : slots_) free_slot(sl);
     for (Slot& sl : rescue_) free_slot(sl);
@@ -144,6 +206,27 @@ class HipBackend : public coa_q::Backend {
 
   int slots() const override { return (int)slots_.size(); }
   int devices() const override { return std::max<int>(1, (int)devs_.size()); }
+  uint64_t grows() const override { return g_grows.load(); }
+
+  // Everything a first window would otherwise pay for, done at queue
+  // creation: the slots' streams, their page-locked and device staging, and
+  // one small copy through each stream, which makes HIP create the stream's
+  // hardware queue (a CU-masked stream's first dispatch took ~25-75 ms:
+  // round-4 paced runs, one queue per rate, p99 20-75 ms from that alone).
+  void prepare() override {
+    if (!ready()) return;
+    for (Slot& sl : slots_) {
+      const size_t pre_din = lane_ == coa_q::LANE_DIGEST ? (32u << 20) : (4u << 20);
+      if (hipSetDevice(sl.dev) != hipSuccess || grow_dev(sl.din, sl.cap_din, pre_din, sl.grave) != hipSuccess ||
+          grow_dev(sl.dout, sl.cap_dout, 256u << 10, sl.grave) != hipSuccess)
+        continue;  // the first launch regrows and reports any failure
+      (void)hipMemcpyAsync(sl.din, sl.hin, 4096, hipMemcpyHostToDevice, sl.s);
+      (void)hipMemsetAsync(sl.dout, 0, 4096, sl.s);
+      (void)hipStreamSynchronize(sl.s);
+    }
+    (void)hipGetLastError();
+  }
+  int stream_kind() const override { return kind_; }
 
   void launch(coa_q::Launch& L) override {
     if (!ready()) {
@@ -153,9 +236,23 @@ class HipBackend : public coa_q::Backend {
     Slot* sl;
     bool inject = false;
     {
+      // the next free slot in turn (a busy slot is passed over, not waited for)
       std::unique_lock<std::mutex> l(m_);
-      const size_t k = next_++ % slots_.size();
-      cv_.wait(l, [&] { return !slots_[k].busy; });
+      auto free_slot = [&]() -> long {
+        for (size_t k = 0; k < slots_.size(); k++) {
+          const size_t i = (next_ + k) % slots_.size();
+          if (!slots_[i].busy) return (long)i;
+        }
+        return -1;
+      };
+      long k = free_slot();
+      if (k < 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        cv_.wait(l, [&] { return (k = free_slot()) >= 0; });
+        L.slot_wait_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+                             .count();
+      }
+      next_ = (size_t)k + 1;
       slots_[k].busy = true;
       L.slot = (int)k;
       sl = &slots_[k];
@@ -207,18 +304,27 @@ class HipBackend : public coa_q::Backend {
       return false;
     }
     const int nctx = std::min(n, 64);
-    // device slots per context: windows in flight at once (COA_QUEUE_SLOTS,
-    // 1..8; tools/queue_probe.c measures the choice)
+    // device slots per context: windows in flight at once (1..8;
+    // COA_QUEUE_SLOTS for the verify lane, COA_QUEUE_DIGEST_SLOTS for the
+    // digest lane; tools/queue_probe.c measures the choice)
     size_t per = COA_QUEUE_SLOTS_DEFAULT;
-    if (const char* e = getenv("COA_QUEUE_SLOTS")) {
+    if (const char* e = getenv(lane_ == coa_q::LANE_DIGEST ? "COA_QUEUE_DIGEST_SLOTS" : "COA_QUEUE_SLOTS")) {
       const int v = atoi(e);
       if (v >= 1 && v <= 8) per = (size_t)v;
     }
     if (const char* e = getenv("COA_QUEUE_FAULT")) fault_every_ = strtoull(e, nullptr, 10);
+    kind_ = stream_kind_env();
     slots_.resize(per * (size_t)nctx);
+    // page-locked staging sized up front for the usual windows (a reallocation
+    // on the launch path is a hipHostFree/hipHostMalloc pair: milliseconds)
+    const size_t pre_in = lane_ == coa_q::LANE_DIGEST ? (32u << 20) : (4u << 20);  // doubled by grow_pinned
     for (size_t k = 0; k < slots_.size(); k++) {
-      slots_[k].dev = ids[k % (size_t)nctx];
-      if (make_stream(slots_[k]) != COA_OK) {
+      Slot& sl = slots_[k];
+      sl.dev = ids[k % (size_t)nctx];
+      sl.kind = kind_;
+      sl.lane = lane_;
+      if (make_stream(sl) != COA_OK || grow_pinned(sl.hin, sl.cap_hin, pre_in, sl.grave) != hipSuccess ||
+          grow_pinned(sl.hout, sl.cap_hout, 256u << 10, sl.grave) != hipSuccess) {
         init_rc_ = COA_EHIP;
         return false;
       }
@@ -226,7 +332,11 @@ class HipBackend : public coa_q::Backend {
     for (int i = 0; i < nctx; i++)
       if (std::find(devs_.begin(), devs_.end(), ids[i]) == devs_.end()) devs_.push_back(ids[i]);
     rescue_.resize(devs_.size());
-    for (size_t i = 0; i < devs_.size(); i++) rescue_[i].dev = devs_[i];
+    for (size_t i = 0; i < devs_.size(); i++) {
+      rescue_[i].dev = devs_[i];
+      rescue_[i].kind = kind_;
+      rescue_[i].lane = lane_;
+    }
     return true;
   }
 
@@ -261,10 +371,11 @@ class HipBackend : public coa_q::Backend {
     const size_t out_bytes = o;
     const size_t ws_v = L.nv ? coa_verify_workspace_bytes(L.nv) : 0;
     const size_t ws_c = L.nc ? coa_certificate_workspace_bytes(L.nc, L.nvotes) : 0;
-    if (grow_pinned(sl.hin, sl.cap_hin, in_bytes) != hipSuccess ||
-        grow_pinned(sl.hout, sl.cap_hout, out_bytes) != hipSuccess ||
-        grow_dev(sl.din, sl.cap_din, in_bytes) != hipSuccess || grow_dev(sl.dout, sl.cap_dout, out_bytes) != hipSuccess ||
-        grow_dev(sl.ws, sl.cap_ws, std::max(ws_v, ws_c) + 256) != hipSuccess)
+    if (grow_pinned(sl.hin, sl.cap_hin, in_bytes, sl.grave) != hipSuccess ||
+        grow_pinned(sl.hout, sl.cap_hout, out_bytes, sl.grave) != hipSuccess ||
+        grow_dev(sl.din, sl.cap_din, in_bytes, sl.grave) != hipSuccess ||
+        grow_dev(sl.dout, sl.cap_dout, out_bytes, sl.grave) != hipSuccess ||
+        grow_dev(sl.ws, sl.cap_ws, std::max(ws_v, ws_c) + 256, sl.grave) != hipSuccess)
       return COA_ENOMEM;
     uint8_t* h = static_cast<uint8_t*>(sl.hin);
     size_t v = 0, c = 0, cv = 0, hb = 0, dn = 0, db = 0;
@@ -320,10 +431,11 @@ class HipBackend : public coa_q::Backend {
     sl.launched = true;
     if (inject) return COA_EHIP;  // fault injection: the copy is in flight, the kernels never run
     int rc = COA_OK;
-    if ((sl.lat || L.nc) && !sl.gate) {  // both read the committee key cache
-      coa_keycache_read_acquire(sl.dev);
-      sl.gate = true;
-    }
+    // both read the committee key cache: the launch pins the current
+    // generation until complete() (a registration meanwhile builds the next
+    // one beside it) and its launches read that one
+    if ((sl.lat || L.nc) && !sl.keys) sl.keys = coa_keycache_pin(sl.dev);
+    coa_keycache_use(sl.keys);
     if (L.nv && sl.lat)
       rc = coa_lat_verify_device(sl.dev, d + i_vm, L.nv, reinterpret_cast<uint32_t*>(dout + sl.o_v), sl.s);
     else if (L.nv)
@@ -339,6 +451,7 @@ class HipBackend : public coa_q::Backend {
     if (rc == COA_OK && L.nd)
       rc = coa_sha512_many_device(sl.dev, d + i_dd, reinterpret_cast<const uint64_t*>(d + i_do), L.nd, dout + sl.o_d,
                                   sl.s);
+    coa_keycache_use(nullptr);
     if (rc != COA_OK) return rc;
     if (hipMemcpyAsync(sl.hout, dout, out_bytes, hipMemcpyDeviceToHost, sl.s) != hipSuccess) return COA_EHIP;
     if (hipEventRecord(sl.ev, sl.s) != hipSuccess) return COA_EHIP;
@@ -378,9 +491,9 @@ class HipBackend : public coa_q::Backend {
         dn += w->nd;
       }
     }
-    if (sl.gate) {
-      coa_keycache_read_release(sl.dev);
-      sl.gate = false;
+    if (sl.keys) {
+      coa_keycache_unpin(sl.keys);
+      sl.keys = nullptr;
     }
   }
 
@@ -418,6 +531,8 @@ class HipBackend : public coa_q::Backend {
   std::vector<Slot> slots_;
   std::vector<Slot> rescue_;  // one recovery context per device, used only by retry()
   std::vector<int> devs_;     // distinct device ids
+  const int lane_;
+  int kind_ = COA_QUEUE_STREAM_PLAIN;
   size_t next_ = 0;
   std::mutex m_;
   std::condition_variable cv_;
@@ -428,4 +543,4 @@ class HipBackend : public coa_q::Backend {
 
 }  // namespace
 
-coa_q::Backend* coa_q::make_backend() { return new HipBackend(); }
+coa_q::Backend* coa_q::make_backend(int lane) { return new HipBackend(lane); }

@@ -160,30 +160,60 @@ class Worker {
   std::thread th_;  // last: starts after the members above exist
 };
 
+// One committee's key tables on one device (f2): sorted keys, flags, a
+// radix-256 comb of -A per key and (within the HBM budget) the wide combs.
+// Immutable once built and shared by every context open on the device; a
+// registration builds the next generation beside it (DevShared).
+struct KeySet {
+  int dev = -1;
+  DevBuf ckeys, kflags, ktabs, kwtabs;
+  uint32_t nkeys = 0;
+  bool kwide = false;  // kwtabs holds the committee's wide combs
+  bool kw20 = false;   // ... in the radix-2^20 layout (COA_KWCOMB20_*)
+  KeySet() = default;
+  KeySet(const KeySet&) = delete;
+  KeySet& operator=(const KeySet&) = delete;
+  ~KeySet() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+    for (DevBuf* b : {&ckeys, &kflags, &ktabs, &kwtabs}) b->release();
+  }
+};
+using KeySetP = std::shared_ptr<const KeySet>;
+
+// What the contexts open on one HIP device share: B's wide comb (8.9 GB,
+// built once per device, not once per context) and the current key-cache
+// generation.  coa_committee_register builds a new generation on `build`
+// (no context's lock, stream or buffers), swaps it in under `mu`, and frees
+// the old one once no call or queue window holds it.
+struct DevShared {
+  int id = -1;
+  uint32_t* wcomb = nullptr;  // wide B comb, COA_WCOMB_POS x 2^(W-1) entries (8.9 GB at W = 24)
+  hipStream_t build = nullptr;
+  std::mutex mu;  // guards `keys`
+  KeySetP keys;   // never null while the device is open
+  std::mutex reg_mu;  // one registration at a time per device
+};
+
 struct Dev {
   int id = 0;
+  DevShared* sh = nullptr;
   std::unique_ptr<Worker> worker;
   hipStream_t stream = nullptr;
   uint32_t* btab = nullptr;  // 128 x (j+1)B, radix-256 fixed-base table (12 KiB)
   uint32_t* comb = nullptr;  // 32 x 128 x (v+1)256^j B comb for k_verify_halved (384 KiB)
-  uint32_t* wcomb = nullptr;  // wide B comb, COA_WCOMB_POS x 2^(W-1) entries (8.9 GB at W = 24)
   DevBuf msgs, pks, sigs, kbuf, rec, verdicts, scratch, aux, rbuf, seeds, offs, data, out, idx, zs, terms, flags;
-  // committee key cache (f2): sorted keys, flags, one comb of -A per key
-  DevBuf ckeys, kflags, ktabs, kwtabs, cert, cscr;
+  DevBuf cert, cscr;
   DevBuf msm;  // Pippenger workspace (one large verify_batch group)
   DevBuf lat;  // single-signature latency path: inputs beyond the inline ones
   uint32_t* lat_res = nullptr;  // page-locked result words the latency kernels write
   size_t lat_res_cap = 0;
   uint32_t lat_tag = 0;
   uint32_t* lat_ctr = nullptr;  // device block counter of k_cert_verify_lat (0 between calls)
-  bool kwide = false;  // kwtabs holds the committee's wide combs
-  bool kw20 = false;   // ... in the radix-2^20 layout (COA_KWCOMB20_*)
-  uint32_t nkeys = 0;
   PinBuf pin;
   std::mutex mu;
   std::vector<DevBuf*> all() {
-    return {&msgs,  &pks,  &sigs, &kbuf, &rec, &verdicts, &scratch, &aux,  &rbuf,   &seeds, &offs,
-            &data,  &out,  &idx,  &zs,   &terms, &flags,  &ckeys,   &kflags, &ktabs, &kwtabs, &cert, &cscr, &msm, &lat};
+    return {&msgs, &pks, &sigs, &kbuf, &rec, &verdicts, &scratch, &aux, &rbuf, &seeds, &offs, &data,
+            &out,  &idx, &zs,   &terms, &flags, &cert, &cscr, &msm, &lat};
   }
 };
 
@@ -199,17 +229,19 @@ bool env_is(const char* name, const char* value) {
 }
 // The wide comb is built at device open unless COA_WCOMB=0 then; COA_WCOMB=0
 // at call time selects the radix-256 comb (A/B runs; read per call).
-const uint32_t* wcomb_of(const Dev& d) { return env_is("COA_WCOMB", "0") ? nullptr : d.wcomb; }
+const uint32_t* wcomb_of(const Dev& d) { return env_is("COA_WCOMB", "0") ? nullptr : d.sh->wcomb; }
 // Bytes of HBM the committee's wide key combs may take (COA_KEY_WCOMB_MB,
 // default 16 GiB: committees up to 341 keys; 0 disables them).
 double key_wcomb_budget() {
   const char* v = getenv("COA_KEY_WCOMB_MB");
   return (v ? atof(v) : 16384.0) * 1048576.0;
 }
-// Bytes of HBM the radix-2^20 key combs (654 MB per key) may take on one
-// device, shared by the contexts open on it (COA_KEY_WCOMB20_MB, default
-// 128 GiB of the MI355X's 288 GB: committees up to ~210 keys on one context;
-// 0 disables them).
+// Bytes of HBM the radix-2^20 key combs (654 MB per key) of one key-cache
+// generation may take on one device (COA_KEY_WCOMB20_MB, default 128 GiB of
+// the MI355X's 288 GB: committees up to ~210 keys; 0 disables them).  The
+// generation is shared by the device's contexts; while a registration
+// builds the next one both are resident for a moment (the new one falls
+// back to the radix-2^16 combs, or to none, when that does not fit).
 double key_wcomb20_budget() {
   const char* v = getenv("COA_KEY_WCOMB20_MB");
   return (v ? atof(v) : 131072.0) * 1048576.0;
@@ -227,31 +259,22 @@ bool g_inited = false;
 // Engine-failure recovery counters (coa_engine_recoveries).
 std::atomic<uint64_t> g_ctx_rebuilt{0}, g_shards_rerun{0};
 
-// Key-cache gate per HIP device id (coa_committee.h): readers are the
-// aggregation queue's in-flight certificate windows, the writer is
-// coa_committee_register.  A waiting writer holds new readers back.
-struct KeyGate {
-  std::mutex mu;
-  std::condition_variable cv;
-  int readers = 0;
-  bool writer = false;
-};
-constexpr int kMaxDevIds = 64;
-KeyGate g_kgate[kMaxDevIds];
-KeyGate& kgate(int device) { return g_kgate[(unsigned)device % kMaxDevIds]; }
+std::vector<std::unique_ptr<DevShared>> g_shared;  // one per opened HIP device id
 
-void kgate_write_lock(int device) {
-  KeyGate& g = kgate(device);
-  std::unique_lock<std::mutex> l(g.mu);
-  g.cv.wait(l, [&] { return !g.writer; });
-  g.writer = true;
-  g.cv.wait(l, [&] { return g.readers == 0; });
+DevShared* shared_of(int id) {
+  for (auto& p : g_shared)
+    if (p->id == id) return p.get();
+  return nullptr;
 }
-void kgate_write_unlock(int device) {
-  KeyGate& g = kgate(device);
-  std::lock_guard<std::mutex> l(g.mu);
-  g.writer = false;
-  g.cv.notify_all();
+
+// The key-cache generation a call or launch on context d reads: the one this
+// thread pinned (coa_keycache_use, the aggregation queue's windows) or the
+// device's current one.  Holding the returned pointer keeps it alive.
+thread_local const KeySetP* t_keys_pinned = nullptr;
+KeySetP keys_now(const Dev& d) {
+  if (t_keys_pinned && *t_keys_pinned && (*t_keys_pinned)->dev == d.id) return *t_keys_pinned;
+  std::lock_guard<std::mutex> l(d.sh->mu);
+  return d.sh->keys;
 }
 
 int open_device(int d) {
@@ -263,16 +286,26 @@ int open_device(int d) {
   HIP_TRY(coa_launch_build_btable(dev->btab, dev->stream));
   HIP_TRY(hipMalloc(&dev->comb, COA_COMB_DWORDS * sizeof(uint32_t)));
   HIP_TRY(coa_launch_build_comb(dev->comb, dev->btab, dev->stream));
-  // the wide comb only speeds things up: without the memory for it the
-  // radix-256 comb serves every call
-  if (!env_is("COA_WCOMB", "0")) {
-    if (hipMalloc(&dev->wcomb, COA_WCOMB_DWORDS * sizeof(uint32_t)) == hipSuccess) {
-      HIP_TRY(coa_launch_build_wcomb(dev->wcomb, dev->comb, dev->stream));
-    } else {
-      dev->wcomb = nullptr;
-      (void)hipGetLastError();
+  DevShared* sh = shared_of(d);
+  if (!sh) {  // first context on this device: its shared tables
+    g_shared.push_back(std::make_unique<DevShared>());
+    sh = g_shared.back().get();
+    sh->id = d;
+    auto empty = std::make_shared<KeySet>();
+    empty->dev = d;
+    sh->keys = std::move(empty);
+    // the wide comb only speeds things up: without the memory for it the
+    // radix-256 comb serves every call
+    if (!env_is("COA_WCOMB", "0")) {
+      if (hipMalloc(&sh->wcomb, COA_WCOMB_DWORDS * sizeof(uint32_t)) == hipSuccess) {
+        HIP_TRY(coa_launch_build_wcomb(sh->wcomb, dev->comb, dev->stream));
+      } else {
+        sh->wcomb = nullptr;
+        (void)hipGetLastError();
+      }
     }
   }
+  dev->sh = sh;
   HIP_TRY(hipStreamSynchronize(dev->stream));
   dev->worker = std::make_unique<Worker>();
   g_devs.push_back(std::move(dev));
@@ -540,10 +573,11 @@ int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* s
   }
   a.tag = tag;
   a.res = d.lat_res;
-  a.keys = d.ckeys.as<uint32_t>();
-  a.kflags = d.kflags.as<uint32_t>();
-  a.ktabs = d.ktabs.as<uint32_t>();
-  a.nk = d.nkeys;
+  const KeySetP ks = keys_now(d);  // held until the verdicts are in
+  a.keys = ks->ckeys.as<uint32_t>();
+  a.kflags = ks->kflags.as<uint32_t>();
+  a.ktabs = ks->ktabs.as<uint32_t>();
+  a.nk = ks->nkeys;
   a.comb = d.comb;
   HIP_TRY(coa_launch_verify_lat(a, s));
   std::vector<uint32_t> words(n);
@@ -973,7 +1007,7 @@ CertPack cert_layout(size_t nc, size_t nv, size_t hbytes) {
   return p;
 }
 
-CertArgs cert_args(Dev& d, uint8_t* base, const CertPack& p, size_t nc, size_t nv) {
+CertArgs cert_args(Dev& d, const KeySet& ks, uint8_t* base, const CertPack& p, size_t nc, size_t nv) {
   CertArgs a;
   a.hdr_data = base + p.hdata;
   a.hdr_off = reinterpret_cast<const uint64_t*>(base + p.hoff);
@@ -987,14 +1021,14 @@ CertArgs cert_args(Dev& d, uint8_t* base, const CertPack& p, size_t nc, size_t n
   a.nc = (uint32_t)nc;
   a.nv = (uint32_t)nv;
   a.hdr_blocks = 0;
-  a.keys = d.ckeys.as<uint32_t>();
-  a.kflags = d.kflags.as<uint32_t>();
-  a.ktabs = d.ktabs.as<uint32_t>();
-  a.nk = d.nkeys;
+  a.keys = ks.ckeys.as<uint32_t>();
+  a.kflags = ks.kflags.as<uint32_t>();
+  a.ktabs = ks.ktabs.as<uint32_t>();
+  a.nk = ks.nkeys;
   a.comb = d.comb;
   a.wcomb = wcomb_of(d);
-  a.kwtabs = (d.kwide && !env_is("COA_KEY_WCOMB", "0")) ? d.kwtabs.as<uint32_t>() : nullptr;
-  a.kw20 = d.kw20 ? 1u : 0u;
+  a.kwtabs = (ks.kwide && !env_is("COA_KEY_WCOMB", "0")) ? ks.kwtabs.as<uint32_t>() : nullptr;
+  a.kw20 = ks.kw20 ? 1u : 0u;
   a.status = reinterpret_cast<uint32_t*>(base + p.status);
   return a;
 }
@@ -1052,7 +1086,8 @@ int cert_inline(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status
   int rc = lat_res_prepare(d, nc, tag);
   if (rc != COA_OK) return rc;
   CertArgs& a = ci.a;
-  a = cert_args(d, nullptr, CertPack{}, nc, nv);
+  const KeySetP ks = keys_now(d);  // held until the status words are in
+  a = cert_args(d, *ks, nullptr, CertPack{}, nc, nv);
   a.status = d.lat_ctr + 1;
   a.host_res = d.lat_res;
   a.done_ctr = d.lat_ctr;
@@ -1091,7 +1126,8 @@ int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_
   if (hb) std::memcpy(h + p.hdata, in.hdr_data + h0, hb);
   hipStream_t s = d.stream;
   HIP_TRY(hipMemcpyAsync(d.cert.p, h, p.total, hipMemcpyHostToDevice, s));
-  CertArgs a = cert_args(d, d.cert.as<uint8_t>(), p, nc, nv);
+  const KeySetP ks = keys_now(d);  // held until the status words are in
+  CertArgs a = cert_args(d, *ks, d.cert.as<uint8_t>(), p, nc, nv);
   const int lanes = cert_lanes(nc + nv);
   if (lanes == 64 && publish) {  // the last block writes the status words to host memory
     if (!d.lat_ctr) {
@@ -1221,6 +1257,68 @@ int sign_enqueue(Dev& d, const uint8_t* d_seeds, const uint8_t* d_msgs, size_t m
   return COA_OK;
 }
 
+// Builds the next key-cache generation of device sh on its build stream
+// while every call and queue window keeps the current one, swaps it in, then
+// frees the old generation once nothing holds it: no call or window waits
+// for a registration, and none is held back (the round-3 write gate stalled
+// the queue's certificate windows for the whole 0.6-2.7 s build).
+int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys) {
+  std::lock_guard<std::mutex> r(sh.reg_mu);
+  HIP_TRY(hipSetDevice(sh.id));
+  if (!sh.build) HIP_TRY(hipStreamCreateWithFlags(&sh.build, hipStreamNonBlocking));
+  const size_t nk = keys.size();
+  auto ks = std::make_shared<KeySet>();
+  ks->dev = sh.id;
+  hipStream_t s = sh.build;
+  if (nk) {
+    HIP_TRY(ks->ckeys.ensure(nk * 32));
+    HIP_TRY(ks->kflags.ensure(nk * 4));
+    HIP_TRY(ks->ktabs.ensure(nk * (size_t)COA_KEY_TAB_DWORDS * 4));
+    HIP_TRY(hipMemcpyAsync(ks->ckeys.p, keys.data(), nk * 32, hipMemcpyHostToDevice, s));
+    HIP_TRY(coa_launch_key_flags(ks->ckeys.as<uint32_t>(), (uint32_t)nk, ks->kflags.as<uint32_t>(), s));
+    HIP_TRY(coa_launch_key_tables(ks->ckeys.as<uint32_t>(), (uint32_t)nk, ks->ktabs.as<uint32_t>(), s));
+    // wide combs when the committee fits the budget: radix 2^20 (654 MB per
+    // key, 13 additions per [k](-A)) within COA_KEY_WCOMB20_MB, else radix
+    // 2^16 (48 MiB per key, 16 additions) within COA_KEY_WCOMB_MB (speed
+    // only: without the memory the radix-256 key combs serve)
+    KeySet& k = *ks;
+    if ((double)nk * COA_KWCOMB20_DWORDS * 4 <= key_wcomb20_budget()) {
+      if (k.kwtabs.ensure(nk * (size_t)COA_KWCOMB20_DWORDS * 4, true) == hipSuccess) {
+        HIP_TRY(coa_launch_key_wcombs20(k.ktabs.as<uint32_t>(), (uint32_t)nk, k.kwtabs.as<uint32_t>(), s));
+        k.kwide = k.kw20 = true;
+      } else {
+        k.kwtabs.release();
+        (void)hipGetLastError();
+      }
+    }
+    if (!k.kw20 && (double)nk * COA_KWCOMB_DWORDS * 4 <= key_wcomb_budget()) {
+      if (k.kwtabs.ensure(nk * (size_t)COA_KWCOMB_DWORDS * 4, true) == hipSuccess) {
+        HIP_TRY(coa_launch_key_wcombs(k.ktabs.as<uint32_t>(), (uint32_t)nk, k.kwtabs.as<uint32_t>(), s));
+        k.kwide = true;
+      } else {
+        k.kwtabs.release();
+        (void)hipGetLastError();
+      }
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    k.nkeys = (uint32_t)nk;
+  }
+  KeySetP old;
+  {
+    std::lock_guard<std::mutex> l(sh.mu);
+    old = std::move(sh.keys);
+    sh.keys = std::move(ks);
+  }
+  // the old generation: calls and windows that took it still hold it (their
+  // kernels read it until they complete); a device-pointer call on a caller's
+  // stream holds it only while it enqueues, so its kernels are waited for
+  // below.  Only this thread waits.
+  while (old.use_count() > 1) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  HIP_TRY(hipDeviceSynchronize());
+  old.reset();
+  return COA_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1252,13 +1350,19 @@ int coa_shutdown(void) {
     d->lat_res_cap = 0;
     if (d->lat_ctr) (void)hipFree(d->lat_ctr);
     d->lat_ctr = nullptr;
-    d->nkeys = 0;
     if (d->btab) (void)hipFree(d->btab);
     if (d->comb) (void)hipFree(d->comb);
-    if (d->wcomb) (void)hipFree(d->wcomb);
     (void)hipStreamDestroy(d->stream);
   }
   g_devs.clear();
+  for (auto& sh : g_shared) {
+    (void)hipSetDevice(sh->id);
+    if (sh->wcomb) (void)hipFree(sh->wcomb);
+    if (sh->build) (void)hipStreamDestroy(sh->build);
+    std::lock_guard<std::mutex> l(sh->mu);
+    sh->keys.reset();
+  }
+  g_shared.clear();
   g_inited = false;
   return COA_OK;
 }
@@ -1285,13 +1389,13 @@ int coa_self_test(int device, uint64_t* bad_entries) {
   Dev* d = dev_by_id(device);
   if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
   std::lock_guard<std::mutex> l(d->mu);
-  if (!d->wcomb) return COA_OK;
+  if (!d->sh->wcomb) return COA_OK;
   HIP_TRY(hipSetDevice(d->id));
   uint32_t* dbad = nullptr;
   HIP_TRY(hipMalloc(&dbad, sizeof(uint32_t)));
   uint32_t hbad = 0;
   hipError_t e = hipMemsetAsync(dbad, 0, sizeof(uint32_t), d->stream);
-  if (e == hipSuccess) e = coa_launch_check_wcomb(d->wcomb, dbad, d->stream);
+  if (e == hipSuccess) e = coa_launch_check_wcomb(d->sh->wcomb, dbad, d->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(&hbad, dbad, sizeof(uint32_t), hipMemcpyDeviceToHost, d->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
   (void)hipFree(dbad);
@@ -1600,83 +1704,32 @@ int coa_committee_register(const uint8_t* pks, size_t n) {
   for (size_t i = 0; i < n; i++) std::memcpy(keys[i].data(), pks + i * 32, 32);
   std::sort(keys.begin(), keys.end());
   keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
-  const size_t nk = keys.size();
-  // every context builds its own copy, concurrently on the context workers
+  // one generation per device (shared by its contexts), the devices built
+  // concurrently on the worker of each device's first context
   std::vector<std::pair<Dev*, std::function<int()>>> tasks;
-  for (auto& dp : g_devs) {
-    Dev* dv = dp.get();
-    tasks.emplace_back(dv, [dv, nk, &keys]() -> int {
-      Dev& d = *dv;
-      std::lock_guard<std::mutex> l(d.mu);
-      HIP_TRY(hipSetDevice(d.id));
-      d.nkeys = 0;
-      if (nk == 0) return COA_OK;
-      HIP_TRY(d.ckeys.ensure(nk * 32));
-      HIP_TRY(d.kflags.ensure(nk * 4));
-      HIP_TRY(d.ktabs.ensure(nk * (size_t)COA_KEY_TAB_DWORDS * 4));
-      HIP_TRY(hipMemcpyAsync(d.ckeys.p, keys.data(), nk * 32, hipMemcpyHostToDevice, d.stream));
-      HIP_TRY(coa_launch_key_flags(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.kflags.as<uint32_t>(), d.stream));
-      HIP_TRY(coa_launch_key_tables(d.ckeys.as<uint32_t>(), (uint32_t)nk, d.ktabs.as<uint32_t>(), d.stream));
-      // wide combs when the committee fits the budget: radix 2^20 (654 MB
-      // per key, 13 additions per [k](-A)) within COA_KEY_WCOMB20_MB shared
-      // by the device's contexts, else radix 2^16 (48 MiB per key, 16
-      // additions) within COA_KEY_WCOMB_MB (speed only: without the memory
-      // the radix-256 key combs serve)
-      d.kwide = false;
-      d.kw20 = false;
-      int ctx_on_dev = 0;
-      for (const auto& o : g_devs) ctx_on_dev += o->id == d.id ? 1 : 0;
-      if ((double)nk * COA_KWCOMB20_DWORDS * 4 <= key_wcomb20_budget() / std::max(1, ctx_on_dev)) {
-        if (d.kwtabs.ensure(nk * (size_t)COA_KWCOMB20_DWORDS * 4, true) == hipSuccess) {
-          HIP_TRY(coa_launch_key_wcombs20(d.ktabs.as<uint32_t>(), (uint32_t)nk, d.kwtabs.as<uint32_t>(), d.stream));
-          d.kwide = true;
-          d.kw20 = true;
-        } else {
-          d.kwtabs.release();
-          (void)hipGetLastError();
-        }
-      }
-      if (!d.kw20 && (double)nk * COA_KWCOMB_DWORDS * 4 <= key_wcomb_budget()) {
-        if (d.kwtabs.ensure(nk * (size_t)COA_KWCOMB_DWORDS * 4, true) == hipSuccess) {
-          HIP_TRY(coa_launch_key_wcombs(d.ktabs.as<uint32_t>(), (uint32_t)nk, d.kwtabs.as<uint32_t>(), d.stream));
-          d.kwide = true;
-        } else {
-          d.kwtabs.release();
-          (void)hipGetLastError();
-        }
-      }
-      if (!d.kwide) d.kwtabs.release();  // a previous committee's tables are not kept
-      HIP_TRY(hipStreamSynchronize(d.stream));
-      d.nkeys = (uint32_t)nk;
-      return COA_OK;
-    });
+  for (auto& shp : g_shared) {
+    DevShared* sh = shp.get();
+    Dev* first = nullptr;
+    for (auto& dp : g_devs)
+      if (dp->id == sh->id && !first) first = dp.get();
+    if (!first) continue;
+    tasks.emplace_back(first, [sh, &keys]() -> int { return build_keyset(*sh, keys); });
   }
-  // the aggregation queue's in-flight certificate windows read these tables
-  // asynchronously: wait for them and hold new ones back (coa_committee.h)
-  std::vector<int> ids;
-  for (auto& dp : g_devs)
-    if (std::find(ids.begin(), ids.end(), dp->id) == ids.end()) ids.push_back(dp->id);
-  std::sort(ids.begin(), ids.end());
-  for (int id : ids) kgate_write_lock(id);
   rc = run_tasks(tasks);
-  for (int id : ids) kgate_write_unlock(id);
   if (rc != COA_OK) return rc;
-  return (int)nk;
+  return (int)keys.size();
 }
 
-void coa_keycache_read_acquire(int device) {
-  KeyGate& g = kgate(device);
-  std::unique_lock<std::mutex> l(g.mu);
-  g.cv.wait(l, [&] { return !g.writer; });
-  g.readers++;
+void* coa_keycache_pin(int device) {
+  DevShared* sh = shared_of(device);
+  if (!sh) return nullptr;
+  std::lock_guard<std::mutex> l(sh->mu);
+  return new KeySetP(sh->keys);
 }
 
-void coa_keycache_read_release(int device) {
-  KeyGate& g = kgate(device);
-  std::lock_guard<std::mutex> l(g.mu);
-  g.readers--;
-  g.cv.notify_all();
-}
+void coa_keycache_unpin(void* pin) { delete static_cast<KeySetP*>(pin); }
+
+void coa_keycache_use(void* pin) { t_keys_pinned = static_cast<const KeySetP*>(pin); }
 
 size_t coa_lat_max(void) { return lat_max(); }
 
@@ -1696,10 +1749,13 @@ int coa_lat_verify_device(int device, const uint8_t* d_in, size_t n, uint32_t* d
   a.in = reinterpret_cast<const uint32_t*>(d_in);
   a.res = d_res;
   a.tag = 1;
-  a.keys = d->ckeys.as<uint32_t>();
-  a.kflags = d->kflags.as<uint32_t>();
-  a.ktabs = d->ktabs.as<uint32_t>();
-  a.nk = d->nkeys;
+  // the pinned generation (the queue) or the current one: a registration
+  // frees a replaced generation only after the device has drained
+  const KeySetP ks = keys_now(*d);
+  a.keys = ks->ckeys.as<uint32_t>();
+  a.kflags = ks->kflags.as<uint32_t>();
+  a.ktabs = ks->ktabs.as<uint32_t>();
+  a.nk = ks->nkeys;
   a.comb = d->comb;
   HIP_TRY(coa_launch_verify_lat(a, stream ? (hipStream_t)stream : d->stream));
   return COA_OK;
@@ -1716,13 +1772,14 @@ int coa_committee_key_flags(uint32_t* flags_out, size_t cap) {
   if (rc != COA_OK) return rc;
   Dev& d = *g_devs[0];
   std::lock_guard<std::mutex> l(d.mu);
-  const size_t nk = std::min<size_t>(d.nkeys, cap);
-  if (nk == 0) return (int)d.nkeys;
+  const KeySetP ks = keys_now(d);
+  const size_t nk = std::min<size_t>(ks->nkeys, cap);
+  if (nk == 0) return (int)ks->nkeys;
   if (!flags_out) return fail(COA_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(d.id));
-  HIP_TRY(hipMemcpyAsync(flags_out, d.kflags.p, nk * 4, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(hipMemcpyAsync(flags_out, ks->kflags.p, nk * 4, hipMemcpyDeviceToHost, d.stream));
   HIP_TRY(hipStreamSynchronize(d.stream));
-  return (int)d.nkeys;
+  return (int)ks->nkeys;
 }
 
 int coa_certificate_verify_many(const uint8_t* header_data, const uint64_t* header_offsets, const uint8_t* ids,
@@ -1777,14 +1834,15 @@ int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data,
   a.nc = (uint32_t)n;
   a.nv = (uint32_t)n_votes;
   a.hdr_blocks = 0;
-  a.keys = d->ckeys.as<uint32_t>();
-  a.kflags = d->kflags.as<uint32_t>();
-  a.ktabs = d->ktabs.as<uint32_t>();
-  a.nk = d->nkeys;
+  const KeySetP ks = keys_now(*d);  // pinned (the queue) or current; see coa_lat_verify_device
+  a.keys = ks->ckeys.as<uint32_t>();
+  a.kflags = ks->kflags.as<uint32_t>();
+  a.ktabs = ks->ktabs.as<uint32_t>();
+  a.nk = ks->nkeys;
   a.comb = d->comb;
   a.wcomb = wcomb_of(*d);
-  a.kwtabs = (d->kwide && !env_is("COA_KEY_WCOMB", "0")) ? d->kwtabs.as<uint32_t>() : nullptr;
-  a.kw20 = d->kw20 ? 1u : 0u;
+  a.kwtabs = (ks->kwide && !env_is("COA_KEY_WCOMB", "0")) ? ks->kwtabs.as<uint32_t>() : nullptr;
+  a.kw20 = ks->kw20 ? 1u : 0u;
   a.status = d_status;
   const int lanes = cert_lanes(n + n_votes);
   HIP_TRY(hipMemsetAsync(d_status, 0, n * 4, s));
