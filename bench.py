@@ -808,6 +808,170 @@ def queue_round_mix(rates=(5, 10, 100, 300, 1000), seconds=0.6, committee_size=1
     return res
 
 
+def _concat_batches(a, b_sel):
+    """Certificates of batch a followed by b_sel = (batch b, indices)."""
+    import numpy as np
+
+    import certificates as C
+
+    b, idx = b_sel
+    assert a.round == b.round
+    votes_b = [np.arange(int(b.offsets[i]), int(b.offsets[i + 1])) for i in idx]
+    vb = np.concatenate(votes_b) if votes_b else np.zeros(0, np.int64)
+    offs = np.concatenate([a.offsets, a.offsets[-1] + np.cumsum([len(v) for v in votes_b]).astype(np.uint64)])
+    cat = lambda x, y: np.concatenate([x, y[idx]])  # noqa: E731
+    return C.CertificateBatch(a.header_inputs + [b.header_inputs[i] for i in idx], cat(a.ids, b.ids),
+                              cat(a.authors, b.authors), cat(a.header_sigs, b.header_sigs),
+                              cat(a.cert_digests, b.cert_digests), np.concatenate([a.vote_pks, b.vote_pks[vb]]),
+                              np.concatenate([a.vote_sigs, b.vote_sigs[vb]]), offs.astype(np.uint64), None, None,
+                              a.round)
+
+
+def queue_round_mix_adversarial(rates=(100, 1000), seconds=0.6, committee_size=100, bad_sig=0.10, n_core_rounds=3):
+    """The committee-100 round mix with an adversarial share (VERDICT r3
+    next 2): 10 % of the header/vote signatures invalid and 1 % of the
+    certificates carrying keys outside the registered committee (their crypto
+    valid, decided on the uncached path, 0.35-1.4 ms).  Reported beside the
+    submit -> callback latencies:
+      head_of_line   when the pre-verification stage hands each message to
+                     Core: with one global FuturesOrdered (round 3) a slow
+                     certificate holds every later message; with per-author
+                     order (rust/primary/src/pre_verify.rs) only its own
+                     author's (sanitize.release_times over the measured
+                     callback times)
+      core_engine_calls_per_round  Core's own engine calls after the stage,
+                     replayed through the Python mirror (Header/Vote
+                     Signature.verify, Certificate.verify consult
+                     coa_crypto.verified) over the first rounds: the
+                     round-3 stage remembered Ok only (every invalid
+                     signature launched again on Core's task), this one
+                     remembers both."""
+    import numpy as np
+
+    import certificates as C
+    import coa_crypto
+    import sanitize
+    import workloads
+
+    committee, certs_a = C.synth_certificates(committee_size, committee_size=committee_size, n_payload=32, seed=11)
+    _, certs_b = C.synth_certificates(2 * committee_size, committee_size=2 * committee_size,
+                                      n_votes=committee.quorum_threshold(), n_payload=32, seed=12)
+    n_unreg = max(1, committee_size // 100)
+    certs = _concat_batches(certs_a, (certs_b, np.arange(committee_size, committee_size + n_unreg)))
+    committee.register()
+    seeds = workloads.key_seeds(committee_size)
+    ns = 2 * committee_size
+    idx = np.arange(ns) % committee_size
+    msgs = workloads.messages(ns, start=70_000)
+    pks, sigs = coa_crypto.sign_many(seeds[idx], msgs)
+    rng = np.random.default_rng(21)
+    bad = rng.random(ns) < bad_sig
+    sigs = sigs.copy()
+    sigs[bad, 5] ^= 0x40
+    vexp = bad.astype(np.uint8)
+    per_round = committee_size + ns
+    # certificates 0..99 of the registered committee, the unregistered one(s)
+    # in place of the first n_unreg of them in every round
+    kinds = np.array([1 if j % 3 == 0 else 0 for j in range(per_round)], np.int32)
+    items = np.zeros(per_round, np.uint32)
+    citems = np.arange(committee_size)
+    citems[:n_unreg] = committee_size + np.arange(n_unreg)
+    items[kinds == 1] = citems
+    items[kinds == 0] = np.arange(ns)
+    # who sent each message (its author's key): the order the stage keeps
+    authors = np.empty(per_round, object)
+    authors[kinds == 0] = [bytes(pks[k]) for k in range(ns)]
+    authors[kinds == 1] = [bytes(certs.authors[c]) for c in citems]
+    res = {"workload": f"committee {committee_size} round mix, {int(bad.sum())} of {ns} header/vote signatures "
+                       f"invalid, {n_unreg} of {committee_size} certificates with keys outside the registered "
+                       f"committee (crypto valid)",
+           "queue": {"max_batch": 65536, "max_delay_us": 200, "idle_launch": 1}}
+    os.environ["COA_QUEUE_IDLE_LAUNCH"] = "1"
+    try:
+        for rate in rates:
+            rounds = max(3, int(rate * seconds))
+            n = rounds * per_round
+            arrive = (np.arange(n) // per_round + (np.arange(n) % per_round) / per_round) / rate
+            kind, item = np.tile(kinds, rounds), np.tile(items, rounds)
+            lat, el, met = paced_queue(arrive, kind, item, vm=msgs, vp=pks, vs=sigs, vexp=vexp, certs=certs,
+                                       cexp=np.zeros(len(certs), np.uint8), max_delay_us=200)
+            done = arrive + lat * 1e-3
+            who = np.tile(authors, rounds)
+            row = {"rounds": rounds, "requests": n, "windows": met["windows"]}
+            unreg = (kind == 1) & (item >= committee_size)
+            for name, sel in (("signature", kind == 0), ("certificate", (kind == 1) & ~unreg),
+                              ("unregistered_certificate", unreg)):
+                row[name] = {"p50_ms": round(float(np.percentile(lat[sel], 50)), 3),
+                             "p99_ms": round(float(np.percentile(lat[sel], 99)), 3)}
+            hol = {}
+            for order, per_author in (("global_fifo_round3", False), ("per_author", True)):
+                rel = np.array(sanitize.release_times(arrive, done, who, per_author=per_author))
+                d = (rel - arrive) * 1e3
+                hol[order] = {"release_p50_ms": round(float(np.percentile(d, 50)), 3),
+                              "release_p99_ms": round(float(np.percentile(d, 99)), 3),
+                              "held_back_share": round(float(np.mean(rel > done + 1e-9)), 4)}
+            row["head_of_line"] = hol
+            row["diag"] = queue_diag(met)
+            res[str(rate)] = row
+    finally:
+        os.environ.pop("COA_QUEUE_IDLE_LAUNCH", None)
+    # Core's engine calls after the stage, replayed over the first rounds
+    calls = {"single": 0, "certificate": 0}
+    real_v, real_c = coa_crypto.engine_verify_strict, coa_crypto.certificate_verify
+
+    def count_v(*a):
+        calls["single"] += 1
+        return real_v(*a)
+
+    def count_c(*a, **k):
+        calls["certificate"] += 1
+        return real_c(*a, **k)
+
+    core = {}
+    coa_crypto.engine_verify_strict, coa_crypto.certificate_verify = count_v, count_c
+    try:
+        for policy, keep_err in (("ok_only_round3", False), ("ok_and_err", True)):
+            coa_crypto.verified.clear()
+            objs = []
+            for j in range(per_round):  # the stage: the verdicts the queue returned, remembered
+                k = int(items[j])
+                if kinds[j] == 0:
+                    ok = vexp[k] == 0
+                    if ok or keep_err:
+                        coa_crypto.verified.remember_signature(msgs[k], pks[k], sigs[k], ok)
+                    objs.append((0, k))
+                else:
+                    c = certs.certificate(k)
+                    coa_crypto.verified.remember_certificate(c.crypto_key(), 0)
+                    objs.append((1, c))
+            calls["single"] = calls["certificate"] = 0
+            errors = 0
+            for r in range(n_core_rounds):
+                if r:  # the next round's messages: remembered again by the stage
+                    for j, (t, o) in enumerate(objs):
+                        if t == 0 and (vexp[o] == 0 or keep_err):
+                            coa_crypto.verified.remember_signature(msgs[o], pks[o], sigs[o], vexp[o] == 0)
+                        elif t == 1:
+                            coa_crypto.verified.remember_certificate(o.crypto_key(), 0)
+                for t, o in objs:  # Core: one message at a time
+                    try:
+                        if t == 0:
+                            coa_crypto.Signature.from_bytes(bytes(sigs[o])).verify(coa_crypto.Digest(bytes(msgs[o])),
+                                                                                    coa_crypto.PublicKey(bytes(pks[o])))
+                        else:
+                            o.verify(committee)
+                    except (coa_crypto.CryptoError, C.DagError):
+                        errors += 1
+            core[policy] = {"engine_calls_per_round": (calls["single"] + calls["certificate"]) / n_core_rounds,
+                            "dag_errors_per_round": errors / n_core_rounds}
+    finally:
+        coa_crypto.engine_verify_strict, coa_crypto.certificate_verify = real_v, real_c
+        coa_crypto.verified.clear()
+    res["core_engine_calls"] = core
+    coa_crypto.committee_register(np.zeros((0, 32), np.uint8))
+    return res
+
+
 def _round_mix_rates(rates, seconds, per_round, kinds, items, msgs, pks, sigs, ns, certs, committee_size, st_cert,
                      st_single, cpu_max_rounds):
     """queue_round_mix's paced runs, one per round rate, under the window
@@ -968,6 +1132,111 @@ def certificate_config(n_certs, latency_samples, cpu_threads, dev, stream, commi
     res["p50_vs_cpu"] = round(res["cpu_baseline"]["p50_ms"] / res["p50_ms"], 2)
     res["c_caller"]["p50_vs_cpu"] = round(res["cpu_baseline"]["p50_ms"] / c50, 2)
     return res
+
+
+def pcie_h2d_gbps(dev, mib=64, reps=10):
+    """Page-locked host -> device copy rate (torch, HIP events): the PCIe
+    bound of every host-pointer line."""
+    import torch
+
+    x = torch.empty(mib << 20, dtype=torch.uint8, pin_memory=True)
+    y = torch.empty(mib << 20, dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        y.copy_(x, non_blocking=True)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            y.copy_(x, non_blocking=True)
+        e1.record(s)
+    torch.cuda.synchronize()
+    return (mib << 20) * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+
+def host_e2e(local, dev, msgs_h, pks_h, sigs_h, n_certs=10000):
+    """End-to-end throughput with host pointers, from a C caller (tools/latc.c),
+    as the Rust binding calls the ABI: inputs in host
+    memory, verdicts back in host memory, packing and PCIe in the clock.
+      c2_host      65,536 triples per coa_ed25519_verify_strict_many call:
+                   one C thread making back-to-back calls, and 2 / 4 threads
+                   at once over 2 / 4 engine contexts on the GPU (a call of
+                   <= 2 x COA_MIN_SHARD items runs on one idle context, so
+                   the threads' calls are in flight together)
+      c3_host      a C3 round (10,000 certificates, committee 100) per
+                   coa_certificate_verify_many call, back to back
+      c3_stream    the same round streamed through the aggregation queue,
+                   one coa_queue_submit_certificate per certificate (what
+                   VerifyService::certificate does), from 1 / 4 / 8 C
+                   producer threads; clock from the first submission to the
+                   last callback
+      pcie_h2d_GBps  the page-locked H2D rate those lines share"""
+    import ctypes
+
+    import numpy as np
+
+    import certificates as C
+    import coa_crypto
+
+    lib = _latc()
+    vp, sz, ci, dp = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double)
+    lib.latc_verify_many.argtypes = [vp, vp, vp, sz, ci, ci, dp]
+    lib.latc_certificates_many.argtypes = [vp] * 9 + [sz, vp, ci, ci, dp]
+    lib.latc_stream_certificates.argtypes = [sz, ctypes.c_uint, ci, ci] + [vp] * 9 + [sz, vp, dp, vp]
+    for f in (lib.latc_verify_many, lib.latc_certificates_many, lib.latc_stream_certificates):
+        f.restype = ci
+    out = {"pcie_h2d_GBps": round(pcie_h2d_gbps(dev), 1)}
+    m, p, s = (np.ascontiguousarray(a) for a in (msgs_h, pks_h, sigs_h))
+    n = len(m)
+    el = ctypes.c_double()
+    c2 = {"items_per_call": n, "bytes_in_per_call": n * 128}
+    for threads in (1, 2, 4):
+        coa_crypto.shutdown()
+        coa_crypto.init_devices([local] * threads)
+        calls = 40 if threads == 1 else 24
+        assert lib.latc_verify_many(m.ctypes.data, p.ctypes.data, s.ctypes.data, n, 2, threads, ctypes.byref(el)) == 0
+        rc = lib.latc_verify_many(m.ctypes.data, p.ctypes.data, s.ctypes.data, n, calls, threads, ctypes.byref(el))
+        assert rc == 0, f"host-pointer verify: {rc} wrong"
+        c2[f"threads_{threads}"] = {"contexts": threads, "calls": calls * threads,
+                                    "verify_per_s": round(n * calls * threads / el.value, 1),
+                                    "ms_per_call": round(el.value / calls * 1e3, 3)}
+    coa_crypto.shutdown()
+    coa_crypto.init_devices([local])
+    out["c2_host"] = c2
+    committee, batch = C.synth_certificates(n_certs, committee_size=100, n_payload=32, seed=3)
+    committee.register()
+    hd = np.frombuffer(b"".join(batch.header_inputs) + bytes(16), np.uint8)
+    hoff = np.zeros(n_certs + 1, np.uint64)
+    hoff[1:] = np.cumsum([len(h) for h in batch.header_inputs])
+    arrs = [hd, hoff, np.ascontiguousarray(batch.ids), np.ascontiguousarray(batch.authors),
+            np.ascontiguousarray(batch.header_sigs), np.full(n_certs, batch.round, np.uint64),
+            np.ascontiguousarray(batch.vote_pks), np.ascontiguousarray(batch.vote_sigs),
+            np.ascontiguousarray(batch.offsets)]
+    expect = np.zeros(n_certs, np.uint8)
+    ptrs = [a.ctypes.data for a in arrs]
+    bytes_per_cert = (len(hd) + n_certs * (32 + 32 + 64 + 8 + 16) + 96 * int(batch.offsets[-1])) / n_certs
+    assert lib.latc_certificates_many(*ptrs, n_certs, expect.ctypes.data, 1, 1, ctypes.byref(el)) == 0
+    calls = 10
+    rc = lib.latc_certificates_many(*ptrs, n_certs, expect.ctypes.data, calls, 1, ctypes.byref(el))
+    assert rc == 0, f"host-pointer certificates: {rc} wrong"
+    out["c3_host"] = {"certificates_per_call": n_certs, "bytes_in_per_certificate": round(bytes_per_cert),
+                      "certs_per_s": round(n_certs * calls / el.value, 1),
+                      "ms_per_round": round(el.value / calls * 1e3, 3)}
+    c3s = {}
+    for producers in (1, 4, 8):
+        met = coa_crypto.QueueMetrics()
+        rounds = 3
+        rc = lib.latc_stream_certificates(65536, 500, producers, rounds, *ptrs, n_certs, expect.ctypes.data,
+                                          ctypes.byref(el), ctypes.addressof(met))
+        assert rc == 0, f"streamed certificates: {rc} wrong"
+        md = {name: getattr(met, name) for name, _ in coa_crypto.QueueMetrics._fields_}
+        c3s[f"producers_{producers}"] = {"certificates": n_certs * rounds,
+                                         "certs_per_s": round(n_certs * rounds / el.value, 1),
+                                         "windows": int(md["windows"]),
+                                         "wait_ms_p50": round(md["wait_us_p50"] * 1e-3, 3),
+                                         "wait_ms_p99": round(md["wait_us_p99"] * 1e-3, 3), "diag": queue_diag(md)}
+    out["c3_stream"] = c3s
+    coa_crypto.committee_register(np.zeros((0, 32), np.uint8))
+    return out
 
 
 # Sources that make up the C2 verify kernels (k_pre_halve, k_verify_main) and
@@ -1295,6 +1564,8 @@ def main():
         section("c4_stream", lambda: c4_stream(secondary.get("c4_sha512", {}).get("single_batch", {})
                                                .get("cpu_one_core_p50_ms")))
         section("queue_round_mix", queue_round_mix)
+        section("queue_round_mix_adversarial", queue_round_mix_adversarial)
+        section("host_e2e", lambda: host_e2e(local, dev, msgs_h, pks.cpu().numpy(), sigs.cpu().numpy()))
 
     if rank == 0:
         line = {

@@ -110,3 +110,65 @@ def test_harness_cpu_mode():
     r = subprocess.run([exe, "cpu"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "abi harness ok (cpu)" in r.stdout
+
+
+WSRC = os.path.join(ROOT, "tests", "c_abi", "wire_queue_harness.c")
+WOUT = os.path.join(ROOT, "tests", "c_abi", "wire_queue_harness")
+WIRE_CERTS = os.path.join(ROOT, "tests", "golden", "wire_certificates.bin")
+
+
+def build_wire_queue_harness():
+    import build
+
+    lib = build.build()
+    libdir = os.path.dirname(lib)
+    tmp = f"{WOUT}.{os.getpid()}"
+    cmd = ["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"),
+           WSRC, "-o", tmp, "-L", libdir, "-lcoa_verify", f"-Wl,-rpath,{libdir}", "-L/opt/rocm/lib",
+           "-Wl,-rpath,/opt/rocm/lib"]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    os.replace(tmp, WOUT)
+    return WOUT
+
+
+def test_wire_certificates_fixture_matches_oracle():
+    """The committed frames decode (test encoder layout) and their expected
+    bits are the C oracle's: regenerating gives the same file."""
+    import hashlib
+
+    with open(WIRE_CERTS, "rb") as f:
+        blob = f.read()
+    assert blob[:4] == b"CQWC"
+    n_keys = struct.unpack_from("<I", blob, 4)[0]
+    n = struct.unpack_from("<I", blob, 8 + 32 * n_keys)[0]
+    assert n_keys == 4 and n == 20
+    # the generator is deterministic: a fresh run reproduces the fixture
+    import runpy
+    import shutil
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as td:
+        gen = os.path.join(td, "gen.py")
+        shutil.copy(os.path.join(ROOT, "tests", "golden", "make_wire_certificates.py"), gen)
+        src = open(gen).read().replace('HERE = os.path.dirname(os.path.abspath(__file__))',
+                                       f'HERE = {os.path.join(ROOT, "tests", "golden")!r}')
+        src = src.replace('os.path.join(HERE, "wire_certificates.bin")', repr(os.path.join(td, "out.bin")))
+        open(gen, "w").write(src)
+        runpy.run_path(gen, run_name="__main__")
+        assert hashlib.sha256(open(os.path.join(td, "out.bin"), "rb").read()).digest() == \
+            hashlib.sha256(blob).digest()
+
+
+def test_wire_queue_harness_cpu_mode():
+    """No GPU: the native decoder still decodes every frame (host-only), and
+    every queued certificate is answered once with the engine error."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: tests/test_gpu_queue_harness.py runs it")
+    exe = build_wire_queue_harness()
+    r = subprocess.run([exe, WIRE_CERTS, "0", "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1, r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["decoded"] and res["frames"] == 20
+    assert res["answered"] == res["submitted"] == 40 and res["bad_status"] == 40, res

@@ -47,10 +47,18 @@ def test_c5_full_size_eight_shards_bit_exact(engine):
     assert (seeds[-2:] == workloads.key_seeds(2, start=n - 2)).all()
     pool = [(bytes.fromhex(v["msg"]), bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]))
             for v in load_golden("mixed_order_pool.json")]
+    import torch
+
     engine.shutdown()
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info(0)
     engine.init_devices([0] * SHARDS)
     try:
         assert engine.device_count() == SHARDS
+        # the 8 contexts share the device's tables: ONE 8.9 GB B comb, not 8
+        # (71 GB in round 3)
+        free1, _ = torch.cuda.mem_get_info(0)
+        assert free0 - free1 < 12e9, (free0 - free1) / 1e9
         pks, sigs = engine.sign_many(seeds, msgs)
         del seeds
         msgs, pks, sigs, cls = workloads.adversarial_mix(msgs, pks, sigs, frac=0.01, seed=0xC0A5, mixed_pool=pool)

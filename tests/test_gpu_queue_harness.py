@@ -46,3 +46,19 @@ def test_queue_harness_recovers_injected_failures(tmp_path):
     assert res["wrong"] == 0 and res["bad_status"] == 0
     assert res["retried_windows"] >= 1 and res["recovered_windows"] == res["retried_windows"], res
     assert res["failed_windows"] == 0
+
+
+@pytest.mark.parametrize("register", [1, 0])
+def test_wire_frames_decoded_and_queued_golden(register):
+    """Raw PrimaryMessage::Certificate frames (tests/golden/wire_certificates.bin)
+    through the native decoder (coa_wire_scan / coa_wire_decode_certificates)
+    into coa_queue_submit_certificate, from C: every status equals the
+    oracle's bits, with the committee registered (fused cached kernel; the
+    outside-key certificates re-decided exactly) and without (uncached path)."""
+    from test_c_abi import WIRE_CERTS, WOUT, build_wire_queue_harness
+
+    exe = WOUT if os.path.exists(WOUT) else build_wire_queue_harness()
+    r = subprocess.run([exe, WIRE_CERTS, str(register), "3"], capture_output=True, text=True, timeout=300)
+    res = json.loads(r.stdout.strip().splitlines()[-1]) if r.stdout.strip() else {}
+    assert r.returncode == 0, (res, r.stderr[-3000:])
+    assert res["decoded"] and res["answered"] == 60 and res["wrong"] == 0 and res["failed_windows"] == 0

@@ -1,10 +1,16 @@
 #!/bin/bash
-# Round-4 GPU session steps, one parameterised script (replaces the one-off
-# tools/gpu_r3_*.sh): tools/gpu_r4.sh <step> [args]
-#   env          box environment relevant to HIP queues
-#   hwq          hardware-queue probe matrix (tools/hwq_probe)
-#   bench HQ ARGS  bench.py with GPU_MAX_HW_QUEUES=HQ ("-" = leave unset)
-#   tests ARGS   the GPU test suite (pytest -m gpu ARGS)
+# One parameterised GPU-session script (it replaces round 3's 26 one-off
+# tools/gpu_r3_*.sh compositions): tools/gpu_session.sh <step> [args]
+#   env              box environment relevant to HIP queues -> gpurun_out/r4_env.txt
+#   hwq              hardware-queue probe matrix (tools/hwq_probe) -> r4_hwq.jsonl
+#   tests [ARGS]     the GPU test suite (pytest -m gpu ARGS) -> r4_tests.log
+#   bench HQ TAG ARGS  bench.py ARGS with GPU_MAX_HW_QUEUES=HQ ("-": as the box
+#                    has it) -> r4_bench_TAG.json
+#   ab ENVS [N]      same-box A/B of runtime switches on the C2 line
+#                    (tools/ab_env.sh; ENVS="name=VAR=value ... default")
+#   probe SCRIPT ARGS  a tools/ probe under its own time limit
+#   smoke            __graft_entry__.smoke()
+# (kernel stats and counter passes: tools/gpu_round.sh prof | verifypmc)
 # Every GPU step runs under its own timeout; the script stops at the first
 # failure.
 set -o pipefail
@@ -44,6 +50,17 @@ case "$step" in
     ;;
   tests)
     timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > gpurun_out/r4_tests.log 2>&1 || exit 1
+    ;;
+  ab)
+    ENVS="$1" N=${2:-65536} REPS=${REPS:-3} bash tools/ab_env.sh || exit 1
+    ;;
+  probe)
+    script=$1
+    shift
+    timeout -k 10 300 python -u "tools/$script" "$@" || exit 1
+    ;;
+  smoke)
+    timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
     ;;
   *)
     echo "unknown step $step" >&2

@@ -8,7 +8,7 @@
  *
  * Built by xrpl-coa-prototype_amd/build.py into lib/liblatc.so (gcc, linked
  * against libcoa_verify.so).  Measurement infrastructure only. */
-#define _POSIX_C_SOURCE 199309L
+#define _POSIX_C_SOURCE 200809L
 #include <stddef.h>
 #include <stdint.h>
 #include <time.h>
@@ -140,5 +140,189 @@ int latc_paced(size_t max_batch, unsigned max_delay_us, size_t n, const double* 
   coa_queue_metrics(q, m);
   coa_queue_destroy(q);
   free(reqs);
+  return atomic_load(&wrong);
+}
+
+/* ------------------------------------------------------------------------
+ * End-to-end throughput of the host-pointer entry points, as the Rust
+ * binding calls them: inputs in host memory, verdicts back in host memory,
+ * H2D / D2H and packing inside the clock.  `threads` C threads each make
+ * `calls` back-to-back calls over the same inputs (each thread its own
+ * output); wall time from the first call to the last return into
+ * *elapsed_s.  Returns the number of wrong outputs (all inputs valid:
+ * verdict 0 / status 0), or a negative engine status. */
+#include <pthread.h>
+
+typedef struct {
+  int what; /* 0 verify_strict_many, 1 certificate_verify_many */
+  int calls;
+  size_t n;
+  const uint8_t *msgs, *pks, *sigs;
+  const uint8_t *hdata, *ids, *origins, *hsigs, *vpks, *vsigs;
+  const uint64_t *hoff, *rounds, *voff;
+  const uint8_t* expect;
+  uint8_t* out;
+  int rc, wrong;
+} ManyJob;
+
+static void* many_thread(void* arg) {
+  ManyJob* j = (ManyJob*)arg;
+  for (int c = 0; c < j->calls && j->rc == 0; c++) {
+    if (j->what == 0)
+      j->rc = coa_ed25519_verify_strict_many(j->msgs, 32, j->pks, j->sigs, j->n, j->out);
+    else
+      j->rc = coa_certificate_verify_many(j->hdata, j->hoff, j->ids, j->origins, j->hsigs, j->rounds, j->vpks,
+                                          j->vsigs, j->voff, j->n, 0, j->out);
+    for (size_t i = 0; i < j->n && j->rc == 0; i++) j->wrong += j->out[i] != (j->expect ? j->expect[i] : 0);
+  }
+  return NULL;
+}
+
+static int run_many(ManyJob* proto, int threads, double* elapsed_s) {
+  if (threads < 1 || threads > 64) return -1;
+  ManyJob jobs[64];
+  pthread_t th[64];
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = *proto;
+    jobs[t].out = (uint8_t*)malloc(proto->n ? proto->n : 1);
+    jobs[t].rc = jobs[t].wrong = 0;
+  }
+  const double t0 = now_us();
+  for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, many_thread, &jobs[t]);
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  *elapsed_s = (now_us() - t0) * 1e-6;
+  int rc = 0, wrong = 0;
+  for (int t = 0; t < threads; t++) {
+    if (jobs[t].rc < 0 && rc == 0) rc = jobs[t].rc;
+    wrong += jobs[t].wrong;
+    free(jobs[t].out);
+  }
+  return rc < 0 ? rc : wrong;
+}
+
+int latc_verify_many(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, size_t n, int calls, int threads,
+                     double* elapsed_s) {
+  ManyJob p;
+  memset(&p, 0, sizeof(p));
+  p.what = 0;
+  p.calls = calls;
+  p.n = n;
+  p.msgs = msgs;
+  p.pks = pks;
+  p.sigs = sigs;
+  return run_many(&p, threads, elapsed_s);
+}
+
+int latc_certificates_many(const uint8_t* hdata, const uint64_t* hoff, const uint8_t* ids, const uint8_t* origins,
+                           const uint8_t* hsigs, const uint64_t* rounds, const uint8_t* vpks, const uint8_t* vsigs,
+                           const uint64_t* voff, size_t n, const uint8_t* expect, int calls, int threads,
+                           double* elapsed_s) {
+  ManyJob p;
+  memset(&p, 0, sizeof(p));
+  p.what = 1;
+  p.calls = calls;
+  p.n = n;
+  p.hdata = hdata;
+  p.hoff = hoff;
+  p.ids = ids;
+  p.origins = origins;
+  p.hsigs = hsigs;
+  p.rounds = rounds;
+  p.vpks = vpks;
+  p.vsigs = vsigs;
+  p.voff = voff;
+  p.expect = expect;
+  return run_many(&p, threads, elapsed_s);
+}
+
+/* A whole certificate round streamed through the aggregation queue, as
+ * VerifyService::certificate submits it (coa_queue_submit_certificate, one
+ * request per certificate): `producers` C threads submit certificates
+ * p, p + producers, ... of the round, `rounds` times over, all at once; the
+ * clock runs from the first submission to the last callback (flush).
+ * Returns wrong answers (>= 0); queue metrics into *m. */
+typedef struct {
+  coa_queue* q;
+  int p, producers, rounds;
+  size_t n;
+  const uint8_t *hdata, *ids, *origins, *hsigs, *vpks, *vsigs, *expect;
+  const uint64_t *hoff, *rounds_of, *voff;
+  atomic_int* wrong;
+  atomic_long* answered;
+} StreamJob;
+
+typedef struct {
+  const uint8_t* expect;
+  atomic_int* wrong;
+  atomic_long* answered;
+} StreamReq;
+
+static void stream_cb(void* user, int status, const uint8_t* v, size_t n) {
+  StreamReq* r = (StreamReq*)user;
+  if (status != COA_OK || n != 1 || v[0] != r->expect[0]) atomic_fetch_add(r->wrong, 1);
+  atomic_fetch_add(r->answered, 1);
+  free(r);
+}
+
+static void* stream_thread(void* arg) {
+  StreamJob* j = (StreamJob*)arg;
+  for (int r = 0; r < j->rounds; r++)
+    for (size_t k = (size_t)j->p; k < j->n; k += (size_t)j->producers) {
+      StreamReq* q = (StreamReq*)malloc(sizeof(StreamReq));
+      q->expect = j->expect + k;
+      q->wrong = j->wrong;
+      q->answered = j->answered;
+      const int rc = coa_queue_submit_certificate(j->q, j->hdata + j->hoff[k], j->hoff[k + 1] - j->hoff[k],
+                                                  j->ids + 32 * k, j->origins + 32 * k, j->hsigs + 64 * k,
+                                                  j->rounds_of[k], j->vpks + 32 * j->voff[k],
+                                                  j->vsigs + 64 * j->voff[k], j->voff[k + 1] - j->voff[k], stream_cb, q);
+      if (rc != COA_OK) {
+        atomic_fetch_add(j->wrong, 1);
+        free(q);
+      }
+    }
+  return NULL;
+}
+
+int latc_stream_certificates(size_t max_batch, unsigned max_delay_us, int producers, int rounds,
+                             const uint8_t* hdata, const uint64_t* hoff, const uint8_t* ids, const uint8_t* origins,
+                             const uint8_t* hsigs, const uint64_t* rounds_of, const uint8_t* vpks,
+                             const uint8_t* vsigs, const uint64_t* voff, size_t n, const uint8_t* expect,
+                             double* elapsed_s, coa_queue_metrics_t* m) {
+  if (producers < 1 || producers > 64) return -1;
+  coa_queue* q = coa_queue_create(max_batch, max_delay_us);
+  if (!q) return -1;
+  atomic_int wrong = 0;
+  atomic_long answered = 0;
+  StreamJob jobs[64];
+  pthread_t th[64];
+  for (int p = 0; p < producers; p++) {
+    StreamJob* j = &jobs[p];
+    j->q = q;
+    j->p = p;
+    j->producers = producers;
+    j->rounds = rounds;
+    j->n = n;
+    j->hdata = hdata;
+    j->hoff = hoff;
+    j->ids = ids;
+    j->origins = origins;
+    j->hsigs = hsigs;
+    j->rounds_of = rounds_of;
+    j->vpks = vpks;
+    j->vsigs = vsigs;
+    j->voff = voff;
+    j->expect = expect;
+    j->wrong = &wrong;
+    j->answered = &answered;
+  }
+  const double t0 = now_us();
+  for (int p = 0; p < producers; p++) pthread_create(&th[p], NULL, stream_thread, &jobs[p]);
+  for (int p = 0; p < producers; p++) pthread_join(th[p], NULL);
+  coa_queue_flush(q);
+  *elapsed_s = (now_us() - t0) * 1e-6;
+  coa_queue_metrics(q, m);
+  coa_queue_destroy(q);
+  if (atomic_load(&answered) != (long)(n * (size_t)rounds)) atomic_fetch_add(&wrong, 1);
   return atomic_load(&wrong);
 }

@@ -73,7 +73,7 @@ def _build_latc():
         return
     if os.path.exists(out) and os.path.getmtime(out) >= _newest([src, LIB, os.path.join(ROOT, "include", "coa_verify.h")]):
         return
-    cmd = ["gcc", "-O2", "-std=c11", "-shared", "-fPIC", "-I" + os.path.join(ROOT, "include"), src, "-o", out,
+    cmd = ["gcc", "-O2", "-std=c11", "-shared", "-fPIC", "-pthread", "-I" + os.path.join(ROOT, "include"), src, "-o", out,
            "-L" + LIBDIR, "-lcoa_verify", "-Wl,-rpath,$ORIGIN"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

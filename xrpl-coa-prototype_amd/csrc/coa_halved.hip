@@ -916,9 +916,11 @@ hipError_t coa_launch_verify_split(const uint8_t* pks, const uint8_t* sigs, cons
   // 0.594 / 0.602 ms per call).  At 32,768 some SIMDs already get two of its
   // waves (0.82 vs 0.65 ms), and at C2's size the doubled doublings cost
   // more than the second wave per SIMD wins back (0.90 vs 0.72 ms).
-  // COA_MAIN_TWO=0/1 forces either (A/B).
+  // COA_MAIN_TWO=0/1 forces either (A/B).  An explicit COA_MAIN_IL (without
+  // COA_MAIN_TWO) selects the one-lane kernel it names at every size, so an
+  // A/B of COA_MAIN_IL alone never measures k_verify_main2 instead.
   const char* two_s = getenv("COA_MAIN_TWO");
-  const int two_env = two_s ? atoi(two_s) : -1;
+  const int two_env = two_s ? atoi(two_s) : (il_env ? 0 : -1);
   const bool two = ebp && (two_env >= 0 ? two_env != 0 : 4ull * n <= one_wave_per_simd_items());
   if (two)
     hipLaunchKernelGGL(k_verify_main2, dim3((n + 63) / 64), dim3(128), 0, s, rec, flags, n, verdicts, scratch, ebp);

@@ -194,15 +194,108 @@ struct DevShared {
   std::mutex reg_mu;  // one registration at a time per device
 };
 
+// Host copies split over a few persistent threads: packing a round of
+// certificates (68 MB at C3) into page-locked staging runs at one core's
+// memcpy rate (~8 GB/s) on one thread -- slower than PCIe.  COA_PACK_THREADS
+// (default 8, at most 16) threads including the caller.
+class CopyPool {
+ public:
+  struct Seg {
+    void* dst;
+    const void* src;
+    size_t bytes;
+  };
+  static CopyPool& get() {
+    static CopyPool pool;
+    return pool;
+  }
+  // Copies every segment, pieces of at most kPiece bytes spread over the pool.
+  void copy(const std::vector<Seg>& segs) {
+    std::vector<Seg> pieces;
+    for (const Seg& g : segs)
+      for (size_t o = 0; o < g.bytes; o += kPiece)
+        pieces.push_back({static_cast<uint8_t*>(g.dst) + o, static_cast<const uint8_t*>(g.src) + o,
+                          std::min(kPiece, g.bytes - o)});
+    if (pieces.size() <= 1 || th_.empty()) {
+      for (const Seg& g : pieces) std::memcpy(g.dst, g.src, g.bytes);
+      return;
+    }
+    std::unique_lock<std::mutex> call(call_mu_);  // one job at a time
+    {
+      std::lock_guard<std::mutex> l(m_);
+      job_ = &pieces;
+      next_ = 0;
+      done_ = 0;
+      gen_++;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> l(m_);
+    done_cv_.wait(l, [&] { return done_ == pieces.size(); });
+    job_ = nullptr;
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+
+ private:
+  static constexpr size_t kPiece = 1 << 20;
+  CopyPool() {
+    const char* e = getenv("COA_PACK_THREADS");
+    const int n = std::max(1, std::min(16, e ? atoi(e) : 8));
+    for (int i = 1; i < n; i++) th_.emplace_back([this] { loop(); });
+  }
+  void work() {
+    for (;;) {
+      Seg g;
+      {
+        std::lock_guard<std::mutex> l(m_);
+        if (!job_ || next_ >= job_->size()) return;
+        g = (*job_)[next_++];
+      }
+      std::memcpy(g.dst, g.src, g.bytes);
+      std::lock_guard<std::mutex> l(m_);
+      if (++done_ == job_->size()) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return stop_ || (gen_ != seen && job_ && next_ < job_->size()); });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::mutex call_mu_, m_;
+  std::condition_variable cv_, done_cv_;
+  const std::vector<Seg>* job_ = nullptr;
+  size_t next_ = 0, done_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  std::vector<std::thread> th_;
+};
+
 struct Dev {
   int id = 0;
   DevShared* sh = nullptr;
   std::unique_ptr<Worker> worker;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // second stream of the pipelined certificate path (created on first use)
   uint32_t* btab = nullptr;  // 128 x (j+1)B, radix-256 fixed-base table (12 KiB)
   uint32_t* comb = nullptr;  // 32 x 128 x (v+1)256^j B comb for k_verify_halved (384 KiB)
   DevBuf msgs, pks, sigs, kbuf, rec, verdicts, scratch, aux, rbuf, seeds, offs, data, out, idx, zs, terms, flags;
   DevBuf cert, cscr;
+  DevBuf certc[2], cscrc[2];  // pipelined certificate path: two chunks in flight
+  PinBuf pinc[2];
   DevBuf msm;  // Pippenger workspace (one large verify_batch group)
   DevBuf lat;  // single-signature latency path: inputs beyond the inline ones
   uint32_t* lat_res = nullptr;  // page-locked result words the latency kernels write
@@ -212,8 +305,9 @@ struct Dev {
   PinBuf pin;
   std::mutex mu;
   std::vector<DevBuf*> all() {
-    return {&msgs, &pks, &sigs, &kbuf, &rec, &verdicts, &scratch, &aux, &rbuf, &seeds, &offs, &data,
-            &out,  &idx, &zs,   &terms, &flags, &cert, &cscr, &msm, &lat};
+    return {&msgs, &pks,  &sigs,  &kbuf, &rec, &verdicts, &scratch,  &aux,     &rbuf,     &seeds,   &offs, &data,
+            &out,  &idx,  &zs,    &terms, &flags, &cert,   &cscr,   &certc[0], &certc[1], &cscrc[0], &cscrc[1],
+            &msm,  &lat};
   }
 };
 
@@ -367,13 +461,49 @@ struct Range {
   size_t lo, hi;
 };
 
-// Contiguous index ranges [g*n/G, (g+1)*n/G) over the opened devices.
-std::vector<Range> shard(size_t n) {
+// Items per shard below which a call uses fewer contexts (COA_MIN_SHARD,
+// default 65,536 = one lane per item, one wave per SIMD on an MI355X: a
+// smaller shard leaves SIMDs idle in the one-wave main kernel, and a call
+// spread over every context cannot overlap with another caller's).
+size_t min_shard() {
+  const char* e = getenv("COA_MIN_SHARD");
+  return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)65536;
+}
+std::atomic<uint32_t> g_shard_rr{0};
+
+// Contiguous index ranges [g*n/G', (g+1)*n/G') over G' of the opened
+// contexts: all of them when every shard keeps min_shard() items (a C5 set
+// over the 8 GPUs of a node), else n / min_shard() of them (at least one),
+// idle ones first, starting one further each call -- so host threads calling
+// at once land on different contexts and their calls run side by side.
+// `work`: the call's size in the min_shard() unit (signatures; a
+// certificate counts its votes too).
+std::vector<Range> shard(size_t n, size_t work) {
   std::vector<Range> r;
   const size_t G = g_devs.size();
-  for (size_t g = 0; g < G; g++) {
-    const size_t lo = n * g / G, hi = n * (g + 1) / G;
-    if (hi > lo) r.push_back({g_devs[g].get(), lo, hi});
+  const size_t ms = min_shard();
+  const size_t want = ms ? std::max<size_t>(1, std::min(G, work / ms)) : G;
+  std::vector<Dev*> pick;
+  if (want == G) {
+    for (auto& d : g_devs) pick.push_back(d.get());
+  } else {
+    const size_t start = g_shard_rr.fetch_add(1, std::memory_order_relaxed) % G;
+    std::vector<bool> taken(G, false);
+    for (size_t k = 0; k < G && pick.size() < want; k++) {
+      const size_t i = (start + k) % G;
+      if (g_devs[i]->mu.try_lock()) {  // idle now
+        g_devs[i]->mu.unlock();
+        pick.push_back(g_devs[i].get());
+        taken[i] = true;
+      }
+    }
+    for (size_t k = 0; k < G && pick.size() < want; k++)
+      if (!taken[(start + k) % G]) pick.push_back(g_devs[(start + k) % G].get());
+  }
+  const size_t P = pick.size();
+  for (size_t g = 0; g < P; g++) {
+    const size_t lo = n * g / P, hi = n * (g + 1) / P;
+    if (hi > lo) r.push_back({pick[g], lo, hi});
   }
   return r;
 }
@@ -641,9 +771,12 @@ int rebuild_context(Dev& d) {
   (void)hipStreamSynchronize(d.stream);
   (void)hipStreamDestroy(d.stream);
   d.stream = nullptr;
-  for (DevBuf* b : {&d.msgs, &d.pks, &d.sigs, &d.kbuf, &d.rec, &d.verdicts, &d.scratch, &d.aux, &d.rbuf, &d.seeds,
-                    &d.offs, &d.data, &d.out, &d.idx, &d.zs, &d.terms, &d.flags, &d.cert, &d.cscr, &d.msm, &d.lat})
-    b->release();
+  if (d.stream2) {
+    (void)hipStreamSynchronize(d.stream2);
+    (void)hipStreamDestroy(d.stream2);
+    d.stream2 = nullptr;
+  }
+  for (DevBuf* b : d.all()) b->release();  // per-call buffers (the tables live in DevShared)
   (void)hipGetLastError();
   HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   g_ctx_rebuilt++;
@@ -659,9 +792,9 @@ int rebuild_context(Dev& d) {
 // context failed it.  body must therefore be re-runnable for its range: it
 // writes only its own slice of the caller's outputs.
 template <class F>
-int for_shards(size_t n, F body) {
+int for_shards(size_t n, F body, size_t work = 0) {
   std::vector<std::pair<Dev*, std::function<int()>>> tasks;
-  const std::vector<Range> ranges = shard(n);
+  const std::vector<Range> ranges = shard(n, work ? work : n);
   std::vector<int> rcs(ranges.size(), COA_OK);
   std::vector<std::string> msgs(ranges.size());
   auto run_on = [&body](Dev& d, size_t lo, size_t hi, bool inject) -> int {
@@ -903,7 +1036,7 @@ int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* si
         return batch_groups_split(msgs, pks, sigs, group_offsets, n_groups, zs_in, eff_seed, verdicts_out, mmin,
                                   gbase);
   }
-  // shard by group index
+  // shard by group index (sized by the votes)
   return for_shards(n_groups, [&](Dev& d, size_t glo, size_t ghi) -> int {
     const size_t vlo = group_offsets[glo], vhi = group_offsets[ghi];
     const size_t nv = vhi - vlo, ng = ghi - glo;
@@ -955,7 +1088,7 @@ int batch_groups_impl(const uint8_t* msgs, const uint8_t* pks, const uint8_t* si
     HIP_TRY(hipMemcpyAsync(verdicts_out + glo, d.verdicts.p, ng, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));  // offs / group_of host vectors die here
     return COA_OK;
-  });
+  }, group_offsets[n_groups]);
 }
 
 // ------------------------------------------------------------------------
@@ -1096,6 +1229,91 @@ int cert_inline(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status
   return lat_res_wait(d, s, nc, tag, status_out + lo);
 }
 
+// Packs certificates [lo, hi) into page-locked staging h laid out as p (the
+// copies spread over the CopyPool).
+void cert_pack(uint8_t* h, const CertPack& p, const CertIn& in, size_t lo, size_t hi) {
+  const size_t nc = hi - lo;
+  const uint64_t h0 = in.hdr_off[lo], hb = in.hdr_off[hi] - h0;
+  const uint64_t v0 = in.voff[lo], nv = in.voff[hi] - v0;
+  std::memset(h + p.status, 0, nc * 4);
+  uint64_t* ho = reinterpret_cast<uint64_t*>(h + p.hoff);
+  uint64_t* vo = reinterpret_cast<uint64_t*>(h + p.voff);
+  for (size_t i = 0; i <= nc; i++) {
+    ho[i] = in.hdr_off[lo + i] - h0;
+    vo[i] = in.voff[lo + i] - v0;
+  }
+  std::vector<CopyPool::Seg> segs = {{h + p.ids, in.ids + lo * 32, nc * 32},
+                                     {h + p.origins, in.origins + lo * 32, nc * 32},
+                                     {h + p.hsigs, in.hsigs + lo * 64, nc * 64},
+                                     {h + p.rounds, in.rounds + lo, nc * 8}};
+  if (nv) {
+    segs.push_back({h + p.vpks, in.vpks + v0 * 32, nv * 32});
+    segs.push_back({h + p.vsigs, in.vsigs + v0 * 64, nv * 64});
+  }
+  if (hb) segs.push_back({h + p.hdata, in.hdr_data + h0, hb});
+  CopyPool::get().copy(segs);
+}
+
+// Jobs (header + votes) per chunk of the pipelined certificate path: ~1,900
+// C3 certificates, ~13 MB of staging, enough jobs for the persistent
+// certificate grid to fill the chip.
+constexpr size_t kCertChunkJobs = 1 << 17;
+
+// Certificates [lo, hi) on one device in chunks, two in flight on the
+// context's two streams: chunk k + 1 is packed (CopyPool) and its copy runs
+// while chunk k's kernel runs, and the PCIe copies of one chunk overlap the
+// other's kernel.  Raw status words out.
+int cert_shard_pipelined(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_out) {
+  std::vector<size_t> cuts{lo};
+  size_t jobs = 0;
+  for (size_t c = lo; c < hi; c++) {
+    jobs += 1 + (in.voff[c + 1] - in.voff[c]);
+    if (jobs >= kCertChunkJobs && c + 1 < hi) {
+      cuts.push_back(c + 1);
+      jobs = 0;
+    }
+  }
+  cuts.push_back(hi);
+  if (!d.stream2) HIP_TRY(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
+  hipStream_t st[2] = {d.stream, d.stream2};
+  const KeySetP ks = keys_now(d);  // held until every chunk is done
+  struct Pending {
+    bool busy = false;
+    size_t lo = 0, hi = 0, status = 0;
+  } pend[2];
+  auto drain = [&](int b) -> int {
+    if (!pend[b].busy) return COA_OK;
+    HIP_TRY(hipStreamSynchronize(st[b]));
+    std::memcpy(status_out + pend[b].lo, static_cast<uint8_t*>(d.pinc[b].p) + pend[b].status,
+                (pend[b].hi - pend[b].lo) * 4);
+    pend[b].busy = false;
+    return COA_OK;
+  };
+  for (size_t k = 0; k + 1 < cuts.size(); k++) {
+    const int b = (int)(k & 1);
+    int rc = drain(b);  // this buffer set's previous chunk
+    if (rc != COA_OK) return rc;
+    const size_t clo = cuts[k], chi = cuts[k + 1], nc = chi - clo;
+    const uint64_t nv = in.voff[chi] - in.voff[clo], hb = in.hdr_off[chi] - in.hdr_off[clo];
+    const CertPack p = cert_layout(nc, nv, hb);
+    HIP_TRY(d.pinc[b].ensure(p.total));
+    HIP_TRY(d.certc[b].ensure(p.total));
+    HIP_TRY(d.cscrc[b].ensure(coa_cert_scratch_bytes(nc + nv)));
+    uint8_t* h = static_cast<uint8_t*>(d.pinc[b].p);
+    cert_pack(h, p, in, clo, chi);
+    HIP_TRY(hipMemcpyAsync(d.certc[b].p, h, p.total, hipMemcpyHostToDevice, st[b]));
+    CertArgs a = cert_args(d, *ks, d.certc[b].as<uint8_t>(), p, nc, nv);
+    HIP_TRY(coa_launch_cert_verify(a, 1, d.cscrc[b].as<uint32_t>(), st[b]));
+    HIP_TRY(hipMemcpyAsync(h + p.status, d.certc[b].as<uint8_t>() + p.status, nc * 4, hipMemcpyDeviceToHost, st[b]));
+    pend[b] = {true, clo, chi, p.status};
+  }
+  for (int b = 0; b < 2; b++) {
+    const int rc = drain(b);
+    if (rc != COA_OK) return rc;
+  }
+  return COA_OK;
+}
+
 int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_out, bool publish = false) {
   const size_t nc = hi - lo;
   const uint64_t h0 = in.hdr_off[lo], hb = in.hdr_off[hi] - h0;
@@ -1104,26 +1322,13 @@ int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_
     const int rc = cert_inline(d, in, lo, hi, status_out);
     if (rc != 1) return rc;
   }
+  if (!publish && nc + nv >= 2 * kCertChunkJobs && !env_is("COA_CERT_PIPELINE", "0"))
+    return cert_shard_pipelined(d, in, lo, hi, status_out);
   const CertPack p = cert_layout(nc, nv, hb);
   HIP_TRY(d.pin.ensure(p.total));
   HIP_TRY(d.cert.ensure(p.total));
   uint8_t* h = static_cast<uint8_t*>(d.pin.p);
-  std::memset(h + p.status, 0, nc * 4);
-  uint64_t* ho = reinterpret_cast<uint64_t*>(h + p.hoff);
-  uint64_t* vo = reinterpret_cast<uint64_t*>(h + p.voff);
-  for (size_t i = 0; i <= nc; i++) {
-    ho[i] = in.hdr_off[lo + i] - h0;
-    vo[i] = in.voff[lo + i] - v0;
-  }
-  std::memcpy(h + p.ids, in.ids + lo * 32, nc * 32);
-  std::memcpy(h + p.origins, in.origins + lo * 32, nc * 32);
-  std::memcpy(h + p.hsigs, in.hsigs + lo * 64, nc * 64);
-  std::memcpy(h + p.rounds, in.rounds + lo, nc * 8);
-  if (nv) {
-    std::memcpy(h + p.vpks, in.vpks + v0 * 32, nv * 32);
-    std::memcpy(h + p.vsigs, in.vsigs + v0 * 64, nv * 64);
-  }
-  if (hb) std::memcpy(h + p.hdata, in.hdr_data + h0, hb);
+  cert_pack(h, p, in, lo, hi);
   hipStream_t s = d.stream;
   HIP_TRY(hipMemcpyAsync(d.cert.p, h, p.total, hipMemcpyHostToDevice, s));
   const KeySetP ks = keys_now(d);  // held until the status words are in
@@ -1219,7 +1424,9 @@ int certificates_impl(const CertIn& in, size_t n, uint64_t rng_seed, uint8_t* st
     HIP_TRY(hipSetDevice(d.id));
     rc = cert_shard(d, in, 0, n, st.data(), true);
   } else {
-    rc = for_shards(n, [&](Dev& d, size_t lo, size_t hi) -> int { return cert_shard(d, in, lo, hi, st.data()); });
+    rc = for_shards(
+        n, [&](Dev& d, size_t lo, size_t hi) -> int { return cert_shard(d, in, lo, hi, st.data()); },
+        n + in.voff[n]);
   }
   if (rc != COA_OK) return rc;
   std::vector<size_t> uncached, rlc;
@@ -1265,7 +1472,19 @@ int sign_enqueue(Dev& d, const uint8_t* d_seeds, const uint8_t* d_msgs, size_t m
 int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys) {
   std::lock_guard<std::mutex> r(sh.reg_mu);
   HIP_TRY(hipSetDevice(sh.id));
-  if (!sh.build) HIP_TRY(hipStreamCreateWithFlags(&sh.build, hipStreamNonBlocking));
+  if (!sh.build) {
+    // the build runs beside live windows: on a CU-masked stream over the
+    // upper COA_REGISTER_CUS (default half) of the CUs, so the windows'
+    // kernels always find the other CUs free (a committee-100 build is
+    // 65 GB of comb entries, ~0.6 s on the whole GPU)
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, sh.id));
+    const char* e = getenv("COA_REGISTER_CUS");
+    const int use = std::max(1, std::min(cus, e ? atoi(e) : cus / 2));
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+    for (int c = cus - use; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
+    HIP_TRY(hipExtStreamCreateWithCUMask(&sh.build, (uint32_t)mask.size(), mask.data()));
+  }
   const size_t nk = keys.size();
   auto ks = std::make_shared<KeySet>();
   ks->dev = sh.id;
@@ -1345,6 +1564,12 @@ int coa_shutdown(void) {
     (void)hipStreamSynchronize(d->stream);
     for (DevBuf* b : d->all()) b->release();
     d->pin.release();
+    for (PinBuf& p : d->pinc) p.release();
+    if (d->stream2) {
+      (void)hipStreamSynchronize(d->stream2);
+      (void)hipStreamDestroy(d->stream2);
+      d->stream2 = nullptr;
+    }
     if (d->lat_res) (void)hipHostFree(d->lat_res);
     d->lat_res = nullptr;
     d->lat_res_cap = 0;
