@@ -59,6 +59,25 @@ case "$step" in
     shift
     timeout -k 10 300 python -u "tools/$script" "$@" || exit 1
     ;;
+  pmcsec)
+    # counter passes of one bench section -> tools/pmc_kernels.py summary:
+    # tools/gpu_session.sh pmcsec SECTION TAG KERNEL...
+    sec=$1
+    tag=$2
+    shift 2
+    d=gpurun_out/pmc_$tag
+    rm -rf $d
+    for pass in "SQ:SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
+                "WAIT:SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_ANY SQ_INSTS_LDS" \
+                "FETCH_SIZE:FETCH_SIZE" "WRITE_SIZE:WRITE_SIZE"; do
+      name=${pass%%:*}
+      ctrs=${pass#*:}
+      timeout -k 10 -s KILL 300 rocprofv3 --pmc $ctrs --kernel-trace -d $d/pmc_$name -o run --output-format csv \
+        -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 --settle-s 0 --sections $sec \
+        > $d.$name.json 2> $d.$name.err || { tail -20 $d.$name.err; exit 1; }
+    done
+    python3 tools/pmc_kernels.py $d gpurun_out/pmc_$tag.json "$@" || exit 1
+    ;;
   smoke)
     timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
     ;;
