@@ -97,11 +97,16 @@ def test_torsion_groups_exact_via_msm(engine, monkeypatch):
     assert [v == 0 for v in got] == [g["expect"] for g in groups]
 
 
-@pytest.mark.parametrize("run", [16, 32, 64, 128])
-def test_large_group_matches_per_vote_path(engine, monkeypatch, run):
+@pytest.mark.parametrize("run,tree,pstride", [(16, 1, 32), (32, 1, 32), (64, 1, 32), (128, 1, 32), (16, 0, 32),
+                                              (128, 0, 24), (32, 1, 24)])
+def test_large_group_matches_per_vote_path(engine, monkeypatch, run, tree, pstride):
     """n = 20,011 (odd point counts across chunk boundaries at every run):
     valid, one corrupted s, one non-canonical s, one undecodable R, and equal
-    weights (every R_i digit in one bucket: a bucket spanning all lanes)."""
+    weights (every R_i digit in one bucket: a bucket spanning all lanes).
+    Both forms of the window sums (COA_MSM_TREE: per chunk, or buckets summed
+    over chunks first) and both point-record strides (COA_MSM_PSTRIDE)."""
+    monkeypatch.setenv("COA_MSM_TREE", str(tree))
+    monkeypatch.setenv("COA_MSM_PSTRIDE", str(pstride))
     n = 20011
     m, pks, sigs = _signed(engine, n, b"large")
     msgs = np.frombuffer(m, np.uint8).reshape(1, 32).copy()

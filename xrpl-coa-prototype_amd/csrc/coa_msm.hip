@@ -182,6 +182,31 @@ COA_DEV void block_sum(ge_p3& acc, uint32_t* tmp) {
   }
 }
 
+// sum_j j·B_j over a workgroup's 256 buckets, lane t holding B_{t+1}:
+// S_t = sum_{t' >= t} B_{t'+1} by a suffix scan inside each wave plus the
+// totals of the waves above, then a block sum; valid in thread 0.
+COA_DEV void bucket_weighted_sum(ge_p3& S, uint32_t* s_tmp) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+#pragma unroll 1
+  for (int delta = 1; delta < 64; delta <<= 1) {
+    ge_p3 q, id;
+    p3_shfl_down(q, S, delta);
+    ge_p3_identity(id);
+    p3_select(q, id, lane + delta >= 64);
+    p3_add(S, S, q);
+  }
+  if (lane == 0) lds_put(s_tmp, 4, wave, S);  // wave totals
+  __syncthreads();
+#pragma unroll 1
+  for (int k = wave + 1; k < 4; k++) {
+    ge_p3 q;
+    lds_get(q, s_tmp, 4, k);
+    p3_add(S, S, q);
+  }
+  __syncthreads();
+  block_sum(S, s_tmp);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ prep
@@ -193,7 +218,7 @@ __global__ void __launch_bounds__(256) k_msm_prep(const uint8_t* __restrict__ pk
                                                   const uint32_t* __restrict__ kbuf, const uint32_t* __restrict__ zs,
                                                   uint32_t n, uint32_t np, uint32_t* __restrict__ pts,
                                                   int16_t* __restrict__ dig, uint32_t* __restrict__ zpart,
-                                                  uint32_t* __restrict__ bad) {
+                                                  uint32_t* __restrict__ bad, uint32_t ps) {
   __shared__ uint32_t red[9 * 256];
   uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   constexpr uint32_t SH = Rows ? 4 : 0;
@@ -216,7 +241,7 @@ __global__ void __launch_bounds__(256) k_msm_prep(const uint8_t* __restrict__ pk
     }
     ge_p3 P;
     bool ok = ge_decompress<Rows>(P, enc);
-    if (leader) niels_store(pts + (uint64_t)(is_r ? i : n + i) * 24, P);
+    if (leader) niels_store(pts + (uint64_t)(is_r ? i : n + i) * ps, P);
     int d[WA];
     if (is_r) {
       uint32_t sw[8];
@@ -279,7 +304,7 @@ __global__ void __launch_bounds__(256) k_msm_prep(const uint8_t* __restrict__ pk
 // ------------------------------------------------------------ B and -b
 __global__ void __launch_bounds__(256) k_msm_bpoint(const uint32_t* __restrict__ zpart, uint32_t nparts, uint32_t n,
                                                     uint32_t np, uint32_t* __restrict__ pts,
-                                                    int16_t* __restrict__ dig) {
+                                                    int16_t* __restrict__ dig, uint32_t ps) {
   __shared__ uint32_t red[10 * 256];
   const int t = threadIdx.x;
   uint32_t acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -309,7 +334,7 @@ __global__ void __launch_bounds__(256) k_msm_bpoint(const uint32_t* __restrict__
     sc_neg(nb, b.v);
     ge_p3 B;
     ge_basepoint(B);
-    niels_store(pts + (uint64_t)2 * n * 24, B);
+    niels_store(pts + (uint64_t)2 * n * ps, B);
     int d[WA];
     recode<WA>(d, nb.v);
 #pragma unroll
@@ -321,7 +346,7 @@ __global__ void __launch_bounds__(256) k_msm_bpoint(const uint32_t* __restrict__
 __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restrict__ pts,
                                                        const int16_t* __restrict__ dig, uint32_t n, uint32_t np,
                                                        uint32_t run, uint32_t nchunks, uint32_t* __restrict__ segs,
-                                                       uint32_t* __restrict__ part) {
+                                                       uint32_t* __restrict__ part, uint32_t ps, uint32_t tree) {
   // 66 KiB of LDS: two workgroups per CU.  The bucket segments go to this
   // block's 64 KiB slice of `segs` (owner segments by bucket, continuation
   // segments by lane): written once, read once, L2-resident.
@@ -345,11 +370,12 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   uint32_t* out = part + ((uint64_t)w * nchunks + ch) * 32;
   if (w >= WR && base + cnt <= n) {  // only R points (weights have 15 windows)
-    if (t == 0) {
-      ge_p3 o;
-      ge_p3_identity(o);
+    ge_p3 o;
+    ge_p3_identity(o);
+    if (tree)  // every bucket of this (chunk, window) is empty
+      gbl_put(segs + ((uint64_t)L * 512 + t) * 32, o);
+    else if (t == 0)
       gbl_put(out, o);
-    }
     return;
   }
   const int16_t* dw = dig + (uint64_t)w * np + base;
@@ -401,7 +427,7 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
     ge_p3 acc;
     ge_p3_identity(acc);
     if (lo < hi) {
-      const uint32_t* pb = pts + (uint64_t)base * 24;
+      const uint32_t* pb = pts + (uint64_t)base * ps;
       uint32_t cur = 1;  // bucket of entry lo: last j with s_off[j] <= lo
 #pragma unroll
       for (uint32_t step = 128; step > 0; step >>= 1)
@@ -411,8 +437,8 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
       uint32_t ent = s_sorted[lo];
       uint32_t entn = s_sorted[lo + 1 < hi ? lo + 1 : lo];
       ge_niels q, qn;
-      niels_load(q, pb + (uint64_t)(ent >> 1) * 24);
-      niels_load(qn, pb + (uint64_t)(entn >> 1) * 24);
+      niels_load(q, pb + (uint64_t)(ent >> 1) * ps);
+      niels_load(qn, pb + (uint64_t)(entn >> 1) * ps);
 #pragma unroll 1
       for (uint32_t e = lo; e < hi; e++) {
         if (e == nxt) {  // bucket cur is complete: flush, move to the bucket of e
@@ -426,7 +452,7 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
         }
         ge_niels qnn;
         const uint32_t entnn = s_sorted[e + 2 < hi ? e + 2 : e];
-        niels_load(qnn, pb + (uint64_t)(entnn >> 1) * 24);
+        niels_load(qnn, pb + (uint64_t)(entnn >> 1) * ps);
         ge_niels_cneg(q, (ent & 1u) != 0);
         ge_p1p1 r;
         ge_madd(r, acc, q);
@@ -457,28 +483,56 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
       }
     }
   }
-  // sum_j j·B_j = sum_t S_t with S_t = sum_{t' >= t} B_{t'+1}: suffix scan
-  // inside each wave ...
-#pragma unroll 1
-  for (int delta = 1; delta < 64; delta <<= 1) {
-    ge_p3 q, id;
-    p3_shfl_down(q, S, delta);
-    ge_p3_identity(id);
-    p3_select(q, id, lane + delta >= 64);
-    p3_add(S, S, q);
+  if (tree) {  // bucket sums of this (chunk, window) to its owner slots; summed over chunks by k_msm_bsum*
+    __syncthreads();  // every lane has read its owner segment
+    gbl_put(seg + t * 32, S);
+    return;
   }
-  if (lane == 0) lds_put(s_tmp, 4, wave, S);  // wave totals
-  __syncthreads();
-  // ... plus the totals of the waves above
-#pragma unroll 1
-  for (int k = wave + 1; k < 4; k++) {
-    ge_p3 q;
-    lds_get(q, s_tmp, 4, k);
-    p3_add(S, S, q);
-  }
-  __syncthreads();
-  block_sum(S, s_tmp);
+  // sum_j j·B_j = sum_t S_t with S_t = sum_{t' >= t} B_{t'+1}
+  bucket_weighted_sum(S, s_tmp);
   if (t == 0) gbl_put(out, S);
+}
+
+// Tree form of the window sums (COA_MSM_TREE): the bucket workgroups leave
+// each (chunk, window)'s 256 bucket sums in their owner slots instead of
+// running sum_j j·B_j per chunk (a 256-lane suffix scan and a block sum, ~20
+// extended additions on every lane of every one of the 29 x nchunks
+// workgroups); the buckets are summed over the chunks first -- one addition
+// per (chunk, window, bucket) -- and the weighted sum runs once per window.
+// Level 1: workgroup (window w, group g) adds bucket t over chunks
+// [16g, 16g + 16) into the slot of chunk 16g.
+constexpr uint32_t kTreeGroup = 16;
+__global__ void __launch_bounds__(256) k_msm_bsum1(uint32_t* __restrict__ segs, uint32_t nchunks) {
+  const uint32_t groups = (nchunks + kTreeGroup - 1) / kTreeGroup;
+  const uint32_t w = blockIdx.x / groups, g = blockIdx.x % groups;
+  const uint32_t t = threadIdx.x;
+  const uint32_t c0 = g * kTreeGroup, c1 = min(nchunks, c0 + kTreeGroup);
+  ge_p3 acc;
+  gbl_get(acc, segs + (((uint64_t)c0 * WA + w) * 512 + t) * 32);
+#pragma unroll 1
+  for (uint32_t c = c0 + 1; c < c1; c++) {
+    ge_p3 q;
+    gbl_get(q, segs + (((uint64_t)c * WA + w) * 512 + t) * 32);
+    p3_add(acc, acc, q);
+  }
+  gbl_put(segs + (((uint64_t)c0 * WA + w) * 512 + t) * 32, acc);
+}
+// Level 2: one workgroup per window: bucket t over the groups, then
+// sum_j j·B_j once -> wsum (the layout k_msm_wsum writes).
+__global__ void __launch_bounds__(256) k_msm_bsum2(const uint32_t* __restrict__ segs, uint32_t nchunks,
+                                                   uint32_t* __restrict__ wsum) {
+  __shared__ uint32_t s_tmp[32 * 4];
+  const uint32_t w = blockIdx.x, t = threadIdx.x;
+  ge_p3 S;
+  gbl_get(S, segs + (((uint64_t)0 * WA + w) * 512 + t) * 32);
+#pragma unroll 1
+  for (uint32_t c = kTreeGroup; c < nchunks; c += kTreeGroup) {
+    ge_p3 q;
+    gbl_get(q, segs + (((uint64_t)c * WA + w) * 512 + t) * 32);
+    p3_add(S, S, q);
+  }
+  bucket_weighted_sum(S, s_tmp);
+  if (t == 0) gbl_put(wsum + (uint64_t)w * 32, S);
 }
 
 // ----------------------------------------------------------- window sums
@@ -557,7 +611,7 @@ uint32_t coa_msm_run(size_t n);
 size_t coa_msm_ws_bytes(size_t n) {
   const size_t np = 2 * n + 1;
   const size_t nc = coa_msm_chunks_run(n, coa_msm_run(n));
-  return al(n * 32) + al(n * 16) + al(np * 96) + al((size_t)WA * np * 2) + al(COA_MSM_PREP_BLOCKS * 36) +
+  return al(n * 32) + al(n * 16) + al(np * 128) + al((size_t)WA * np * 2) + al(COA_MSM_PREP_BLOCKS * 36) +
          al((size_t)WA * nc * 128) + al((size_t)WA * 128) + al(16) + al((size_t)WA * nc * 512 * 128);
 }
 
@@ -572,7 +626,7 @@ MsmWs coa_msm_ws_carve(void* base, size_t n) {
   w.z = reinterpret_cast<uint32_t*>(p);
   p += al(n * 16);
   w.pts = reinterpret_cast<uint32_t*>(p);
-  p += al(np * 96);
+  p += al(np * 128);
   w.dig = reinterpret_cast<int16_t*>(p);
   p += al((size_t)WA * np * 2);
   w.zpart = reinterpret_cast<uint32_t*>(p);
@@ -617,6 +671,15 @@ uint32_t coa_msm_run(size_t n) {
 
 uint32_t coa_msm_chunks(size_t n) { return coa_msm_chunks_run(n, coa_msm_run(n)); }
 
+// Dwords per point record (affine Niels, 24 dwords): padded to 32 by default
+// so every record is one 128-byte line -- the bucket kernel reads them at
+// random, and a 96-byte record straddles two lines three times in four.
+// COA_MSM_PSTRIDE=24 packs them (A/B).
+static uint32_t msm_pstride() {
+  const char* e = getenv("COA_MSM_PSTRIDE");
+  return (e && atoi(e) == 24) ? 24u : 32u;
+}
+
 hipError_t coa_launch_msm(const uint8_t* pks, const uint8_t* sigs, uint32_t n, const MsmWs& ws, uint8_t* verdict,
                           hipStream_t s) {
   if (n == 0) return hipSuccess;
@@ -631,19 +694,29 @@ hipError_t coa_launch_msm(const uint8_t* pks, const uint8_t* sigs, uint32_t n, c
   const bool rows = n <= 2048;
   uint32_t pb = (uint32_t)(((uint64_t)2 * n * (rows ? 16 : 1) + 255) / 256);
   if (pb > COA_MSM_PREP_BLOCKS) pb = COA_MSM_PREP_BLOCKS;
+  const uint32_t ps = msm_pstride();
+  // COA_MSM_TREE=0: sum_j j·B_j per (chunk, window) workgroup, then the chunk
+  // partials per window (k_msm_wsum); default: the tree form (k_msm_bsum*)
+  const char* te = getenv("COA_MSM_TREE");
+  const uint32_t tree = (nc > 1 && !(te && atoi(te) == 0)) ? 1u : 0u;
   if (rows)
     hipLaunchKernelGGL(k_msm_prep<true>, dim3(pb), dim3(256), 0, s, pks, sigs, ws.k, ws.z, n, np, ws.pts, ws.dig,
-                       ws.zpart, ws.bad);
+                       ws.zpart, ws.bad, ps);
   else
     hipLaunchKernelGGL(k_msm_prep<false>, dim3(pb), dim3(256), 0, s, pks, sigs, ws.k, ws.z, n, np, ws.pts, ws.dig,
-                       ws.zpart, ws.bad);
-  hipLaunchKernelGGL(k_msm_bpoint, dim3(1), dim3(256), 0, s, ws.zpart, pb, n, np, ws.pts, ws.dig);
+                       ws.zpart, ws.bad, ps);
+  hipLaunchKernelGGL(k_msm_bpoint, dim3(1), dim3(256), 0, s, ws.zpart, pb, n, np, ws.pts, ws.dig, ps);
   const uint32_t g8 = (nc * WA + 7) & ~7u;
   hipLaunchKernelGGL(k_msm_bucket, dim3(g8), dim3(256), 0, s, ws.pts, ws.dig, n, np, run, nc, ws.segs,
-                     ws.part);
-  // one chunk (small groups): its partials already are the window sums,
-  // laid out as wsum (window w at w * 32 words)
-  if (nc > 1) hipLaunchKernelGGL(k_msm_wsum, dim3(WA), dim3(256), 0, s, ws.part, nc, ws.wsum);
+                     ws.part, ps, tree);
+  if (tree) {
+    hipLaunchKernelGGL(k_msm_bsum1, dim3(WA * ((nc + kTreeGroup - 1) / kTreeGroup)), dim3(256), 0, s, ws.segs, nc);
+    hipLaunchKernelGGL(k_msm_bsum2, dim3(WA), dim3(256), 0, s, ws.segs, nc, ws.wsum);
+  } else if (nc > 1) {
+    // (one chunk, small groups: its partials already are the window sums,
+    // laid out as wsum, window w at w * 32 words)
+    hipLaunchKernelGGL(k_msm_wsum, dim3(WA), dim3(256), 0, s, ws.part, nc, ws.wsum);
+  }
   hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, nc > 1 ? ws.wsum : ws.part, ws.bad, verdict);
   return hipGetLastError();
 }
