@@ -1260,6 +1260,16 @@ def verify_kernel_src_sha256():
     return h.hexdigest()
 
 
+def build_identity():
+    """Which build this line measured: sha256 of the engine library and of
+    the C2 verify kernels' sources (the key the counter profile is tied to)."""
+    import hashlib
+
+    lib = os.path.join(PKG, "lib", "libcoa_verify.so")
+    return {"lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16],
+            "verify_kernel_src_sha256": verify_kernel_src_sha256()[:16]}
+
+
 def load_pmc(n):
     """The counter profile of the verify call (tools/pmc_verify.py output) if
     it was taken on this very library build and batch size, else None and the
@@ -1587,6 +1597,7 @@ def main():
             "kernel_ms": {"verify_call": round(verify_ms, 4)},
             "verdicts_ok": ok,
             "env": HIP_ENV_AT_START,
+            "build": build_identity(),
             "roofline": roof,
             "cpu_baseline": cpu,
             "secondary": secondary,
