@@ -97,6 +97,16 @@ extern "C" void* coa_keycache_pin(int device);  // opaque handle (null: device n
 extern "C" void coa_keycache_unpin(void* pin);  // any thread; null is a no-op
 extern "C" void coa_keycache_use(void* pin);    // this thread's launches read `pin` (null: the current one)
 
+// Host copies spread over the runtime's copy threads (COA_PACK_THREADS):
+// the aggregation queue packs large windows into page-locked staging with
+// it.  Returns when every segment is copied.
+struct CoaCopySeg {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+extern "C" void coa_copy_segments(const CoaCopySeg* segs, size_t n);
+
 hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* flags, hipStream_t s);
 hipError_t coa_launch_key_tables(const uint32_t* keys, uint32_t nk, uint32_t* tabs, hipStream_t s);
 // wide combs from the radix-256 key combs (tabs already built)

@@ -378,6 +378,12 @@ class HipBackend : public coa_q::Backend {
         grow_dev(sl.ws, sl.cap_ws, std::max(ws_v, ws_c) + 256, sl.grave) != hipSuccess)
       return COA_ENOMEM;
     uint8_t* h = static_cast<uint8_t*>(sl.hin);
+    // the bulk copies of a large window go to the runtime's copy threads (a
+    // C3 round is ~68 MB: one thread's memcpy would be slower than PCIe)
+    std::vector<CoaCopySeg> bulk;
+    auto copy = [&bulk](void* dst, const void* src, size_t bytes) {
+      if (bytes) bulk.push_back({dst, src, bytes});
+    };
     size_t v = 0, c = 0, cv = 0, hb = 0, dn = 0, db = 0;
     uint64_t* cho = reinterpret_cast<uint64_t*>(h + i_cho);
     uint64_t* cvo = reinterpret_cast<uint64_t*>(h + i_cvo);
@@ -393,36 +399,41 @@ class HipBackend : public coa_q::Backend {
         }
         v += w->nv;
       } else if (w->nv) {
-        std::memcpy(h + i_vm + v * 32, w->v_msgs.data(), w->nv * 32);
-        std::memcpy(h + i_vp + v * 32, w->v_pks.data(), w->nv * 32);
-        std::memcpy(h + i_vs + v * 64, w->v_sigs.data(), w->nv * 64);
+        copy(h + i_vm + v * 32, w->v_msgs.data(), w->nv * 32);
+        copy(h + i_vp + v * 32, w->v_pks.data(), w->nv * 32);
+        copy(h + i_vs + v * 64, w->v_sigs.data(), w->nv * 64);
         v += w->nv;
       }
       if (w->nc) {
         const size_t nvt = w->c_voff.back();
-        if (!w->c_hdata.empty()) std::memcpy(h + i_ch + hb, w->c_hdata.data(), w->c_hdata.size());
+        copy(h + i_ch + hb, w->c_hdata.data(), w->c_hdata.size());
         for (size_t i = 1; i <= w->nc; i++) {
           cho[c + i] = hb + w->c_hoff[i];
           cvo[c + i] = cv + w->c_voff[i];
         }
-        std::memcpy(h + i_cid + c * 32, w->c_ids.data(), w->nc * 32);
-        std::memcpy(h + i_cor + c * 32, w->c_origins.data(), w->nc * 32);
-        std::memcpy(h + i_chs + c * 64, w->c_hsigs.data(), w->nc * 64);
-        std::memcpy(h + i_crd + c * 8, w->c_rounds.data(), w->nc * 8);
-        if (nvt) {
-          std::memcpy(h + i_cvp + cv * 32, w->c_pks.data(), nvt * 32);
-          std::memcpy(h + i_cvs + cv * 64, w->c_sigs.data(), nvt * 64);
-        }
+        copy(h + i_cid + c * 32, w->c_ids.data(), w->nc * 32);
+        copy(h + i_cor + c * 32, w->c_origins.data(), w->nc * 32);
+        copy(h + i_chs + c * 64, w->c_hsigs.data(), w->nc * 64);
+        copy(h + i_crd + c * 8, w->c_rounds.data(), w->nc * 8);
+        copy(h + i_cvp + cv * 32, w->c_pks.data(), nvt * 32);
+        copy(h + i_cvs + cv * 64, w->c_sigs.data(), nvt * 64);
         c += w->nc;
         cv += nvt;
         hb += w->c_hdata.size();
       }
       if (w->nd) {
-        if (!w->d_data.empty()) std::memcpy(h + i_dd + db, w->d_data.data(), w->d_data.size());
+        copy(h + i_dd + db, w->d_data.data(), w->d_data.size());
         for (size_t i = 1; i <= w->nd; i++) dof[dn + i] = db + w->d_offs[i];
         dn += w->nd;
         db += w->d_data.size();
       }
+    }
+    size_t bulk_bytes = 0;
+    for (const CoaCopySeg& g : bulk) bulk_bytes += g.bytes;
+    if (bulk_bytes >= (1u << 20)) {
+      coa_copy_segments(bulk.data(), bulk.size());
+    } else {
+      for (const CoaCopySeg& g : bulk) std::memcpy(g.dst, g.src, g.bytes);
     }
     if (L.nv + L.nc + L.nd == 0) return COA_OK;  // bare vote batches only: done in complete()
     uint8_t* d = static_cast<uint8_t*>(sl.din);

@@ -216,11 +216,13 @@ class CopyPool {
       for (size_t o = 0; o < g.bytes; o += kPiece)
         pieces.push_back({static_cast<uint8_t*>(g.dst) + o, static_cast<const uint8_t*>(g.src) + o,
                           std::min(kPiece, g.bytes - o)});
-    if (pieces.size() <= 1 || th_.empty()) {
+    // one job at a time on the pool; a caller that finds it busy (another
+    // lane's window, a host call) copies on its own thread instead of waiting
+    std::unique_lock<std::mutex> call(call_mu_, std::try_to_lock);
+    if (pieces.size() <= 1 || th_.empty() || !call.owns_lock()) {
       for (const Seg& g : pieces) std::memcpy(g.dst, g.src, g.bytes);
       return;
     }
-    std::unique_lock<std::mutex> call(call_mu_);  // one job at a time
     {
       std::lock_guard<std::mutex> l(m_);
       job_ = &pieces;
@@ -1955,6 +1957,13 @@ void* coa_keycache_pin(int device) {
 void coa_keycache_unpin(void* pin) { delete static_cast<KeySetP*>(pin); }
 
 void coa_keycache_use(void* pin) { t_keys_pinned = static_cast<const KeySetP*>(pin); }
+
+void coa_copy_segments(const CoaCopySeg* segs, size_t n) {
+  std::vector<CopyPool::Seg> v;
+  v.reserve(n);
+  for (size_t i = 0; i < n; i++) v.push_back({segs[i].dst, segs[i].src, segs[i].bytes});
+  CopyPool::get().copy(v);
+}
 
 size_t coa_lat_max(void) { return lat_max(); }
 
