@@ -736,9 +736,10 @@ hipError_t coa_launch_key_flags(const uint32_t* keys, uint32_t nk, uint32_t* fla
 // (2j, lo) and (2j+1, hi) -- an integer multiple, torsion kept -- made affine.
 __global__ void __launch_bounds__(256) k_key_wcomb(const uint32_t* __restrict__ tabs, uint32_t nk,
                                                    uint32_t* __restrict__ wtabs) {
-  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // grid-stride (a bounded, resident grid: see coa_launch_key_wcombs20)
+  for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < (uint64_t)nk * COA_KWCOMB_ENTRIES;
+       id += (uint64_t)gridDim.x * blockDim.x) {
   const uint32_t key = (uint32_t)(id / COA_KWCOMB_ENTRIES);
-  if (key >= nk) return;
   const uint32_t e = (uint32_t)(id % COA_KWCOMB_ENTRIES);
   const int j = (int)(e >> (COA_KWCOMB_W - 1));
   const int m = (int)(e & ((1u << (COA_KWCOMB_W - 1)) - 1)) + 1;
@@ -759,6 +760,7 @@ __global__ void __launch_bounds__(256) k_key_wcomb(const uint32_t* __restrict__ 
   ge_madd(t, P, q);
   ge_p1p1_to_p3(P, t);
   store_niels(wtabs + (uint64_t)key * COA_KWCOMB_DWORDS + (uint64_t)e * 24, P);
+  }
 }
 
 // Widest comb entry (key, j, m-1) = m * 2^(20 j) * (-A): 20 j = 8 q + r, and
@@ -770,9 +772,10 @@ __global__ void __launch_bounds__(256) k_key_wcomb(const uint32_t* __restrict__ 
 // never read and hold the sum of the first two bytes.
 __global__ void __launch_bounds__(256) k_key_wcomb20(const uint32_t* __restrict__ tabs, uint32_t nk,
                                                      uint32_t* __restrict__ wtabs) {
-  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // grid-stride (a bounded, resident grid: see coa_launch_key_wcombs20)
+  for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < (uint64_t)nk * COA_KWCOMB20_ENTRIES;
+       id += (uint64_t)gridDim.x * blockDim.x) {
   const uint32_t key = (uint32_t)(id / COA_KWCOMB20_ENTRIES);
-  if (key >= nk) return;
   const uint64_t e = id % COA_KWCOMB20_ENTRIES;
   const int j = (int)(e >> (COA_KWCOMB20_W - 1));
   const uint32_t m = (uint32_t)(e & ((1u << (COA_KWCOMB20_W - 1)) - 1)) + 1;
@@ -804,19 +807,34 @@ __global__ void __launch_bounds__(256) k_key_wcomb20(const uint32_t* __restrict_
     ge_p1p1_to_p3(P, t);
   }
   store_niels(wtabs + (uint64_t)key * COA_KWCOMB20_DWORDS + e * 24, P);
+  }
+}
+
+// The wide key combs are built while the device serves live windows (a
+// registration builds the next key-cache generation beside the current one,
+// on a least-priority stream: coa_runtime.cpp build_keyset).  One workgroup
+// per 256 entries by default -- short workgroups, so the scheduler hands the
+// CUs to the windows' workgroups between them; COA_BUILD_BLOCKS=<n> bounds
+// the grid to n resident workgroups striding over the entries (A/B:
+// slower build, p99 0.65 vs 0.89 ms under a 5,000/s certificate stream).
+static uint32_t build_blocks(uint64_t total) {
+  const char* e = getenv("COA_BUILD_BLOCKS");
+  const uint64_t cap = e ? strtoull(e, nullptr, 10) : 0;
+  const uint64_t want = (total + 255) / 256;
+  return (uint32_t)(want < cap ? want : (cap ? cap : want));
 }
 
 hipError_t coa_launch_key_wcombs20(const uint32_t* tabs, uint32_t nk, uint32_t* wtabs, hipStream_t s) {
   if (nk == 0) return hipSuccess;
   const uint64_t total = (uint64_t)nk * COA_KWCOMB20_ENTRIES;
-  hipLaunchKernelGGL(k_key_wcomb20, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, tabs, nk, wtabs);
+  hipLaunchKernelGGL(k_key_wcomb20, dim3(build_blocks(total)), dim3(256), 0, s, tabs, nk, wtabs);
   return hipGetLastError();
 }
 
 hipError_t coa_launch_key_wcombs(const uint32_t* tabs, uint32_t nk, uint32_t* wtabs, hipStream_t s) {
   if (nk == 0) return hipSuccess;
   const uint64_t total = (uint64_t)nk * COA_KWCOMB_ENTRIES;
-  hipLaunchKernelGGL(k_key_wcomb, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, tabs, nk, wtabs);
+  hipLaunchKernelGGL(k_key_wcomb, dim3(build_blocks(total)), dim3(256), 0, s, tabs, nk, wtabs);
   return hipGetLastError();
 }
 

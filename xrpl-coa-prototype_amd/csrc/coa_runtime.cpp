@@ -22,6 +22,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -1475,22 +1476,39 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
   std::lock_guard<std::mutex> r(sh.reg_mu);
   HIP_TRY(hipSetDevice(sh.id));
   if (!sh.build) {
-    // the build runs beside live windows: on a CU-masked stream over the
-    // upper COA_REGISTER_CUS (default half) of the CUs, so the windows'
-    // kernels always find the other CUs free (a committee-100 build is
-    // 65 GB of comb entries, ~0.6 s on the whole GPU)
+    // the build runs beside live windows (a committee-100 build is 65 GB of
+    // comb entries, ~0.6 s on the whole GPU): on a plain stream at the least
+    // priority, so the hardware queue scheduler dispatches the windows'
+    // workgroups first.  tools/regab.sh, a C3 certificate stream at 5,000/s
+    // with two re-registrations (profiles/r04_register_ab.txt): request
+    // latency p99 during the build 0.89 ms (max 1.3 ms), registration 0.61 s;
+    // a CU-masked stream over half the CUs (COA_REGISTER_CUS=128) left the
+    // windows 17 ms (bounded resident grid) to 1.4 s (one workgroup per 256
+    // entries) behind.
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, sh.id));
     const char* e = getenv("COA_REGISTER_CUS");
-    const int use = std::max(1, std::min(cus, e ? atoi(e) : cus / 2));
-    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
-    for (int c = cus - use; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
-    HIP_TRY(hipExtStreamCreateWithCUMask(&sh.build, (uint32_t)mask.size(), mask.data()));
+    const int want = e ? atoi(e) : 0;
+    if (want <= 0) {
+      int least = 0, greatest = 0;
+      HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIP_TRY(hipStreamCreateWithPriority(&sh.build, hipStreamNonBlocking, least));
+    } else {
+      const int use = std::min(cus, want);
+      std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+      for (int c = cus - use; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
+      HIP_TRY(hipExtStreamCreateWithCUMask(&sh.build, (uint32_t)mask.size(), mask.data()));
+    }
   }
   const size_t nk = keys.size();
   auto ks = std::make_shared<KeySet>();
   ks->dev = sh.id;
   hipStream_t s = sh.build;
+  // COA_REGISTER_TRACE=1: phase times of this registration on stderr
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  clk::time_point t_alloc = t0, t_built = t0;
   if (nk) {
     HIP_TRY(ks->ckeys.ensure(nk * 32));
     HIP_TRY(ks->kflags.ensure(nk * 4));
@@ -1505,6 +1523,7 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
     KeySet& k = *ks;
     if ((double)nk * COA_KWCOMB20_DWORDS * 4 <= key_wcomb20_budget()) {
       if (k.kwtabs.ensure(nk * (size_t)COA_KWCOMB20_DWORDS * 4, true) == hipSuccess) {
+        t_alloc = clk::now();
         HIP_TRY(coa_launch_key_wcombs20(k.ktabs.as<uint32_t>(), (uint32_t)nk, k.kwtabs.as<uint32_t>(), s));
         k.kwide = k.kw20 = true;
       } else {
@@ -1523,6 +1542,7 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
     }
     HIP_TRY(hipStreamSynchronize(s));
     k.nkeys = (uint32_t)nk;
+    t_built = clk::now();
   }
   KeySetP old;
   {
@@ -1534,9 +1554,18 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
   // kernels read it until they complete); a device-pointer call on a caller's
   // stream holds it only while it enqueues, so its kernels are waited for
   // below.  Only this thread waits.
+  const auto t_swap = clk::now();
   while (old.use_count() > 1) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  const auto t_unpinned = clk::now();
   HIP_TRY(hipDeviceSynchronize());
+  const auto t_synced = clk::now();
   old.reset();
+  if (env_is("COA_REGISTER_TRACE", "1"))
+    fprintf(stderr,
+            "coa_committee_register dev %d keys %zu: alloc %.1f build %.1f swap %.1f unpinned %.1f sync %.1f free "
+            "%.1f ms\n",
+            sh.id, nk, ms(t0, t_alloc), ms(t_alloc, t_built), ms(t_built, t_swap), ms(t_swap, t_unpinned),
+            ms(t_unpinned, t_synced), ms(t_synced, clk::now()));
   return COA_OK;
 }
 
