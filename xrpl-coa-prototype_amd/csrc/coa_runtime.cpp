@@ -193,6 +193,10 @@ struct DevShared {
   std::mutex mu;  // guards `keys`
   KeySetP keys;   // never null while the device is open
   std::mutex reg_mu;  // one registration at a time per device
+  // (under reg_mu) a generation's buffers no call holds any more, kept for
+  // the next registration: a 65 GB allocation clears its memory on the
+  // device, which held live windows back 2.4-7.6 ms (profiles/r04_register_ab.txt)
+  std::shared_ptr<KeySet> spare;
 };
 
 // Host copies split over a few persistent threads: packing a round of
@@ -1501,8 +1505,14 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
     }
   }
   const size_t nk = keys.size();
-  auto ks = std::make_shared<KeySet>();
+  // the buffers of the generation before the current one, when kept
+  // (COA_KEY_SPARE=0: none kept, every registration allocates)
+  const bool keep_spare = !env_is("COA_KEY_SPARE", "0");
+  std::shared_ptr<KeySet> ks = keep_spare && sh.spare ? std::move(sh.spare) : std::make_shared<KeySet>();
+  sh.spare.reset();
   ks->dev = sh.id;
+  ks->nkeys = 0;
+  ks->kwide = ks->kw20 = false;
   hipStream_t s = sh.build;
   // COA_REGISTER_TRACE=1: phase times of this registration on stderr
   using clk = std::chrono::steady_clock;
@@ -1521,8 +1531,13 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
     // 2^16 (48 MiB per key, 16 additions) within COA_KEY_WCOMB_MB (speed
     // only: without the memory the radix-256 key combs serve)
     KeySet& k = *ks;
+    // an exact fit is reused as it is; a different size is reallocated
+    auto fit = [](DevBuf& b, size_t bytes) {
+      if (b.cap != bytes) b.release();
+      return b.ensure(bytes, true);
+    };
     if ((double)nk * COA_KWCOMB20_DWORDS * 4 <= key_wcomb20_budget()) {
-      if (k.kwtabs.ensure(nk * (size_t)COA_KWCOMB20_DWORDS * 4, true) == hipSuccess) {
+      if (fit(k.kwtabs, nk * (size_t)COA_KWCOMB20_DWORDS * 4) == hipSuccess) {
         t_alloc = clk::now();
         HIP_TRY(coa_launch_key_wcombs20(k.ktabs.as<uint32_t>(), (uint32_t)nk, k.kwtabs.as<uint32_t>(), s));
         k.kwide = k.kw20 = true;
@@ -1532,7 +1547,7 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
       }
     }
     if (!k.kw20 && (double)nk * COA_KWCOMB_DWORDS * 4 <= key_wcomb_budget()) {
-      if (k.kwtabs.ensure(nk * (size_t)COA_KWCOMB_DWORDS * 4, true) == hipSuccess) {
+      if (fit(k.kwtabs, nk * (size_t)COA_KWCOMB_DWORDS * 4) == hipSuccess) {
         HIP_TRY(coa_launch_key_wcombs(k.ktabs.as<uint32_t>(), (uint32_t)nk, k.kwtabs.as<uint32_t>(), s));
         k.kwide = true;
       } else {
@@ -1559,6 +1574,31 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
   const auto t_unpinned = clk::now();
   HIP_TRY(hipDeviceSynchronize());
   const auto t_synced = clk::now();
+  // the replaced generation's buffers become the spare of the next
+  // registration; after the first registration of a device (nothing to
+  // replace yet) a spare of the same size is allocated now, while the
+  // committee is being set up rather than under load later
+  if (keep_spare && nk) {
+    const KeySet& cur = *sh.keys;
+    // the next registration of a committee this size finds its buffers ready
+    auto fits = [&](const KeySet& k) {
+      return k.ckeys.cap >= nk * 32 && k.kflags.cap >= nk * 4 && k.ktabs.cap >= nk * (size_t)COA_KEY_TAB_DWORDS * 4 &&
+             k.kwtabs.cap == cur.kwtabs.cap;
+    };
+    if (old && fits(*old)) {
+      sh.spare = std::const_pointer_cast<KeySet>(old);
+    } else {
+      old.reset();  // another size: freed now, and a spare of this size made
+      auto sp = std::make_shared<KeySet>();
+      sp->dev = sh.id;
+      if (sp->ckeys.ensure(cur.ckeys.cap, true) == hipSuccess && sp->kflags.ensure(cur.kflags.cap, true) == hipSuccess &&
+          sp->ktabs.ensure(cur.ktabs.cap, true) == hipSuccess &&
+          (!cur.kwtabs.cap || sp->kwtabs.ensure(cur.kwtabs.cap, true) == hipSuccess))
+        sh.spare = std::move(sp);
+      else
+        (void)hipGetLastError();  // no spare: the next registration allocates
+    }
+  }
   old.reset();
   if (env_is("COA_REGISTER_TRACE", "1"))
     fprintf(stderr,
