@@ -98,13 +98,15 @@ def test_torsion_groups_exact_via_msm(engine, monkeypatch):
 
 
 @pytest.mark.parametrize("run,tree,pstride", [(16, 1, 32), (32, 1, 32), (64, 1, 32), (128, 1, 32), (16, 0, 32),
-                                              (128, 0, 24), (32, 1, 24)])
+                                              (128, 0, 24), (32, 1, 24), (4, 1, 32), (4, 0, 32)])
 def test_large_group_matches_per_vote_path(engine, monkeypatch, run, tree, pstride):
     """n = 20,011 (odd point counts across chunk boundaries at every run):
     valid, one corrupted s, one non-canonical s, one undecodable R, and equal
     weights (every R_i digit in one bucket: a bucket spanning all lanes).
     Both forms of the window sums (COA_MSM_TREE: per chunk, or buckets summed
-    over chunks first) and both point-record strides (COA_MSM_PSTRIDE)."""
+    over chunks first) and both point-record strides (COA_MSM_PSTRIDE).  At
+    run 4 (1,024 points per chunk) 19 of the 40 chunks hold R points only and
+    get no workgroup in windows 15..28, across the tree groups' boundaries."""
     monkeypatch.setenv("COA_MSM_TREE", str(tree))
     monkeypatch.setenv("COA_MSM_PSTRIDE", str(pstride))
     n = 20011
@@ -239,3 +241,39 @@ def test_device_entry_resident(engine):
     # a workspace smaller than verify_batch_workspace_bytes(n) is refused
     with pytest.raises(engine.EngineError):
         engine.verify_batch_device(0, msg, pk, sg, out, rng_seed=1, workspace=ws[:4096])
+
+
+@pytest.mark.parametrize("n", [600_000, 1 << 21])
+def test_large_groups_resident(engine, n):
+    """Large groups (run 128: 18 / 64 chunks of R points alone without
+    workgroups in windows 15..28) on HBM-resident votes: valid with seeded and with equal weights (every
+    R_i digit in one bucket), and one corrupted s in an R-only chunk, in the
+    chunk where the A points start and in the last vote, each an Err."""
+    import torch
+
+    from workloads import key_seeds, messages
+
+    dev = torch.device("cuda", 0)
+    m = torch.from_numpy(np.tile(messages(1), (n, 1))).to(dev)
+    seeds = torch.from_numpy(key_seeds(n)).to(dev)
+    pk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    sg = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    engine.sign_many_device(0, seeds, m, pk, sg)
+    del seeds
+    msg = m[0].contiguous()
+    del m
+    out = torch.full((1,), 7, dtype=torch.uint8, device=dev)
+    ws = torch.empty(engine.verify_batch_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    engine.verify_batch_device(0, msg, pk, sg, out, rng_seed=3, workspace=ws)
+    torch.cuda.synchronize()
+    assert int(out[0]) == 0
+    zs = torch.randint(0, 256, (1, 16), dtype=torch.uint8, device=dev).repeat(n, 1)
+    engine.verify_batch_device(0, msg, pk, sg, out, zs=zs, workspace=ws)
+    torch.cuda.synchronize()
+    assert int(out[0]) == 0
+    for i in (5, n // 2 - 3, n - 1):
+        sg[i, 40] ^= 2
+        engine.verify_batch_device(0, msg, pk, sg, out, rng_seed=4, workspace=ws)
+        torch.cuda.synchronize()
+        assert int(out[0]) == 1, i
+        sg[i, 40] ^= 2

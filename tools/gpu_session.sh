@@ -9,6 +9,8 @@
 #   ab ENVS [N]      same-box A/B of runtime switches on the C2 line
 #                    (tools/ab_env.sh; ENVS="name=VAR=value ... default")
 #   probe SCRIPT ARGS  a tools/ probe under its own time limit
+#   pmcsec SECTION TAG KERNEL...  counter passes of one bench section
+#   kstats TAG ARGS  rocprofv3 kernel trace + stats of bench.py ARGS
 #   smoke            __graft_entry__.smoke()
 # (kernel stats and counter passes: tools/gpu_round.sh prof | verifypmc)
 # Every GPU step runs under its own timeout; the script stops at the first
@@ -77,6 +79,33 @@ case "$step" in
         > $d.$name.json 2> $d.$name.err || { tail -20 $d.$name.err; exit 1; }
     done
     python3 tools/pmc_kernels.py $d gpurun_out/pmc_$tag.json "$@" || exit 1
+    ;;
+  pmcx)
+    # raw counter passes of one bench section: tools/gpu_session.sh pmcx
+    # SECTION TAG "NAME:CTR CTR ..." ... -> medians per (kernel, grid)
+    sec=$1
+    tag=$2
+    shift 2
+    d=gpurun_out/pmcx_$tag
+    rm -rf $d
+    for pass in "$@"; do
+      name=${pass%%:*}
+      ctrs=${pass#*:}
+      timeout -k 10 -s KILL 300 rocprofv3 --pmc $ctrs --kernel-trace -d $d/pmc_$name -o run --output-format csv \
+        -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 --settle-s 0 --sections $sec \
+        > $d.$name.json 2> $d.$name.err || { tail -20 $d.$name.err; exit 1; }
+    done
+    python3 tools/pmc_kernels.py --raw $d gpurun_out/pmcx_$tag.json || exit 1
+    ;;
+  kstats)
+    # per-kernel durations of a bench run: tools/gpu_session.sh kstats TAG ARGS
+    # (runtime switches come in through the environment)
+    tag=$1
+    shift
+    rm -rf gpurun_out/kstats_$tag
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kstats_$tag -o run --output-format csv \
+      -- python3 bench.py --no-cpu-baseline --settle-s 0 "$@" > gpurun_out/kstats_$tag.json \
+      2> gpurun_out/kstats_$tag.err || { tail -20 gpurun_out/kstats_$tag.err; exit 1; }
     ;;
   smoke)
     timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1

@@ -18,7 +18,10 @@ and the kernel trace of the same passes (durations).  Groups dispatches by
   wait_any_share / vmem_share   SQ_WAIT_ANY, SQ_INST_CYCLES_VMEM / SQ_WAVE_CYCLES
   fetch_bytes / write_bytes     FETCH_SIZE x 2 (gfx950 calibration) and
                  WRITE_SIZE, KiB -> bytes
-usage: python tools/pmc_kernels.py <root> <out.json> <kernel> [kernel ...]"""
+usage: python tools/pmc_kernels.py <root> <out.json> <kernel> [kernel ...]
+       python tools/pmc_kernels.py --raw <root> <out.json>   (every counter of
+       every pass directory, medians per (kernel, grid), dispatches with a
+       grid of at least 20,000 work-items)"""
 import collections
 import csv
 import glob
@@ -61,7 +64,29 @@ def durations(root, kernels):
     return out
 
 
+def raw(root, dst):
+    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                g = int(r["Grid_Size"])
+                if g >= 20000:
+                    per[(_name(r["Kernel_Name"]), g, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+        for (k, g, _), cs in per.items():
+            for c, v in cs.items():
+                out[f"{k}@{g}"][c].append(v)
+    res = {k: {c: statistics.median(v) for c, v in cs.items()} for k, cs in out.items()}
+    with open(dst, "w") as fh:
+        json.dump(res, fh, indent=1)
+    for k, cs in sorted(res.items()):
+        print(k, {c: round(v, 1) for c, v in sorted(cs.items())})
+
+
 def main():
+    if sys.argv[1] == "--raw":
+        raw(sys.argv[2], sys.argv[3])
+        return
     root, dst, kernels = sys.argv[1], sys.argv[2], set(sys.argv[3:])
     sq = counters(root, "pmc_SQ", kernels)
     wt = counters(root, "pmc_WAIT", kernels)

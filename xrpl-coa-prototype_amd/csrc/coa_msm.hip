@@ -46,6 +46,8 @@ constexpr int WA = COA_MSM_WA;
 constexpr int WR = COA_MSM_WR;
 constexpr int MAXRUN = COA_MSM_RUN;
 constexpr int CHUNK = COA_MSM_CHUNK;
+// bucket segment slots per (chunk, window): 256 owners + 256 continuations
+constexpr uint32_t SEG_SLOTS = 512;
 
 // Signed radix-2^9 recoding of an 8-word little-endian scalar: W digits in
 // [-256, 255] (a digit of value 256 never occurs: 511 + carry = 512 is 0
@@ -213,6 +215,10 @@ COA_DEV void bucket_weighted_sum(ge_p3& S, uint32_t* s_tmp) {
 // Rows: one 16-lane DPP row per point instead of one lane (small batches,
 // where the decompression chain's latency is the whole kernel): the power
 // chain runs on the row (coa_fe_wave.h), the row's lane 0 writes.
+// Bound by the field products' issue (the decompressions' power chains):
+// capping it at 128 VGPRs for four waves per SIMD instead of three, or
+// sizing the grid to one resident round, left it at 4.2 ms for 2^22 points
+// (profiles/r04_msm_ab.txt).
 template <bool Rows>
 __global__ void __launch_bounds__(256) k_msm_prep(const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
                                                   const uint32_t* __restrict__ kbuf, const uint32_t* __restrict__ zs,
@@ -345,39 +351,38 @@ __global__ void __launch_bounds__(256) k_msm_bpoint(const uint32_t* __restrict__
 // ------------------------------------------------------- bucket phase
 __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restrict__ pts,
                                                        const int16_t* __restrict__ dig, uint32_t n, uint32_t np,
-                                                       uint32_t run, uint32_t nchunks, uint32_t* __restrict__ segs,
-                                                       uint32_t* __restrict__ part, uint32_t ps, uint32_t tree) {
+                                                       uint32_t run, uint32_t nchunks, uint32_t nrc,
+                                                       uint32_t* __restrict__ segs, uint32_t* __restrict__ part,
+                                                       uint32_t ps, uint32_t tree) {
   // 66 KiB of LDS: two workgroups per CU.  The bucket segments go to this
-  // block's 64 KiB slice of `segs` (owner segments by bucket, continuation
-  // segments by lane): written once, read once, L2-resident.
+  // (chunk, window)'s 64 KiB slice of `segs` (owner segments by bucket,
+  // continuation segments by lane): written once, read once, L2-resident.
   __shared__ uint16_t s_sorted[CHUNK];     // (local << 1) | negative, grouped by |digit|
   __shared__ uint32_t s_tmp[32 * 4];       // wave totals / block sum
   __shared__ uint32_t s_hist[NB + 2];      // histogram, then scatter cursors
   __shared__ uint32_t s_off[NB + 2];       // s_off[j] = first sorted entry of bucket j
   __shared__ uint32_t s_wtot[4];
 
+  // Only (chunk, window) pairs with points get a workgroup: the nrc chunks
+  // of R points alone have WR windows (the weights z_i are 128-bit), the
+  // others WA.  Logical block L runs over those pairs chunk by chunk.
   // XCD-aware order: consecutive hardware blocks go round-robin over the 8
-  // XCDs, so hardware block h takes logical block (h % 8) * (G8 / 8) + h / 8
-  // and each XCD works through whole chunks, window after window (the
-  // chunk's points stay in that XCD's L2).
-  const uint32_t G = nchunks * WA, per = gridDim.x >> 3;
+  // XCDs, so hardware block h takes logical block (h % 8) * (G8 / 8) + h / 8:
+  // every XCD gets the same number of pairs (a grid over all WA windows of
+  // every chunk gave the XCDs holding R chunks half the work of the others)
+  // and works through whole chunks, window after window (the chunk's points
+  // stay in that XCD's L2).
+  const uint32_t G = nrc * WR + (nchunks - nrc) * WA, per = gridDim.x >> 3;
   const uint32_t L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
   if (L >= G) return;
-  const uint32_t ch = L / WA, w = L % WA;
+  const uint32_t ch = L < nrc * WR ? L / WR : nrc + (L - nrc * WR) / WA;
+  const uint32_t w = L < nrc * WR ? L % WR : (L - nrc * WR) % WA;
+  const uint32_t slot = ch * WA + w;  // segment slice of this (chunk, window)
   const uint32_t chunk = 256 * run;
   const uint32_t base = ch * chunk;
   const uint32_t cnt = min(chunk, np - base);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   uint32_t* out = part + ((uint64_t)w * nchunks + ch) * 32;
-  if (w >= WR && base + cnt <= n) {  // only R points (weights have 15 windows)
-    ge_p3 o;
-    ge_p3_identity(o);
-    if (tree)  // every bucket of this (chunk, window) is empty
-      gbl_put(segs + ((uint64_t)L * 512 + t) * 32, o);
-    else if (t == 0)
-      gbl_put(out, o);
-    return;
-  }
   const int16_t* dw = dig + (uint64_t)w * np + base;
   const uint32_t rlo = (w >= WR && base < n) ? n - base : 0;  // skip R points above their windows
 
@@ -418,14 +423,14 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
   const uint32_t nnz = s_off[NB + 1];
 
   // balanced accumulation: lane t adds sorted entries [t·run, (t+1)·run),
-  // the loads of the next two points in flight during each addition (the
-  // points are random 96-byte reads from the whole point array; with one
-  // load ahead the waves spent 29 % of their cycles waiting on memory)
-  uint32_t* const seg = segs + (uint64_t)L * 512 * 32;  // [bucket - 1] owners, [256 + lane] continuations
+  // the load of the next point in flight during each addition (the points
+  // are random 128-byte reads from the chunk's 4 MiB of points).  Two
+  // independent chains per lane, and the products interleaved column by
+  // column (ge_madd_il), both measured slower: 5.85 / 6.83 / 5.30 ms against
+  // 5.17 for the 2^21-signature group (profiles/r04_msm_ab.txt).
+  uint32_t* const seg = segs + (uint64_t)slot * SEG_SLOTS * 32;  // [bucket - 1] owners, [256 + lane] continuations
   {
     const uint32_t lo = t * run, hi = min(lo + run, nnz);
-    ge_p3 acc;
-    ge_p3_identity(acc);
     if (lo < hi) {
       const uint32_t* pb = pts + (uint64_t)base * ps;
       uint32_t cur = 1;  // bucket of entry lo: last j with s_off[j] <= lo
@@ -435,10 +440,10 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
       bool owner = s_off[cur] == lo;
       uint32_t nxt = s_off[cur + 1];
       uint32_t ent = s_sorted[lo];
-      uint32_t entn = s_sorted[lo + 1 < hi ? lo + 1 : lo];
-      ge_niels q, qn;
+      ge_niels q;
       niels_load(q, pb + (uint64_t)(ent >> 1) * ps);
-      niels_load(qn, pb + (uint64_t)(entn >> 1) * ps);
+      ge_p3 acc;
+      ge_p3_identity(acc);
 #pragma unroll 1
       for (uint32_t e = lo; e < hi; e++) {
         if (e == nxt) {  // bucket cur is complete: flush, move to the bucket of e
@@ -450,17 +455,15 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
             nxt = s_off[cur + 1];
           } while (nxt == e);
         }
-        ge_niels qnn;
-        const uint32_t entnn = s_sorted[e + 2 < hi ? e + 2 : e];
-        niels_load(qnn, pb + (uint64_t)(entnn >> 1) * ps);
+        const uint32_t entn = s_sorted[e + 1 < hi ? e + 1 : e];
+        ge_niels qn;
+        niels_load(qn, pb + (uint64_t)(entn >> 1) * ps);
         ge_niels_cneg(q, (ent & 1u) != 0);
         ge_p1p1 r;
         ge_madd(r, acc, q);
         ge_p1p1_to_p3(acc, r);
         q = qn;
         ent = entn;
-        qn = qnn;
-        entn = entnn;
       }
       gbl_put(seg + (owner ? cur - 1 : 256 + t) * 32, acc);
     }
@@ -502,20 +505,26 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
 // Level 1: workgroup (window w, group g) adds bucket t over chunks
 // [16g, 16g + 16) into the slot of chunk 16g.
 constexpr uint32_t kTreeGroup = 16;
-__global__ void __launch_bounds__(256) k_msm_bsum1(uint32_t* __restrict__ segs, uint32_t nchunks) {
+// The nrc chunks of R points alone have no workgroup (and no segments) in
+// windows >= WR: their buckets are empty there and are skipped.
+__global__ void __launch_bounds__(256) k_msm_bsum1(uint32_t* __restrict__ segs, uint32_t nchunks, uint32_t nrc) {
   const uint32_t groups = (nchunks + kTreeGroup - 1) / kTreeGroup;
   const uint32_t w = blockIdx.x / groups, g = blockIdx.x % groups;
   const uint32_t t = threadIdx.x;
   const uint32_t c0 = g * kTreeGroup, c1 = min(nchunks, c0 + kTreeGroup);
+  const uint32_t first = w >= WR ? max(c0, nrc) : c0;
   ge_p3 acc;
-  gbl_get(acc, segs + (((uint64_t)c0 * WA + w) * 512 + t) * 32);
+  if (first < c1)
+    gbl_get(acc, segs + (((uint64_t)first * WA + w) * SEG_SLOTS + t) * 32);
+  else
+    ge_p3_identity(acc);
 #pragma unroll 1
-  for (uint32_t c = c0 + 1; c < c1; c++) {
+  for (uint32_t c = first + 1; c < c1; c++) {
     ge_p3 q;
-    gbl_get(q, segs + (((uint64_t)c * WA + w) * 512 + t) * 32);
+    gbl_get(q, segs + (((uint64_t)c * WA + w) * SEG_SLOTS + t) * 32);
     p3_add(acc, acc, q);
   }
-  gbl_put(segs + (((uint64_t)c0 * WA + w) * 512 + t) * 32, acc);
+  gbl_put(segs + (((uint64_t)c0 * WA + w) * SEG_SLOTS + t) * 32, acc);
 }
 // Level 2: one workgroup per window: bucket t over the groups, then
 // sum_j j·B_j once -> wsum (the layout k_msm_wsum writes).
@@ -524,11 +533,11 @@ __global__ void __launch_bounds__(256) k_msm_bsum2(const uint32_t* __restrict__ 
   __shared__ uint32_t s_tmp[32 * 4];
   const uint32_t w = blockIdx.x, t = threadIdx.x;
   ge_p3 S;
-  gbl_get(S, segs + (((uint64_t)0 * WA + w) * 512 + t) * 32);
+  gbl_get(S, segs + (((uint64_t)0 * WA + w) * SEG_SLOTS + t) * 32);
 #pragma unroll 1
   for (uint32_t c = kTreeGroup; c < nchunks; c += kTreeGroup) {
     ge_p3 q;
-    gbl_get(q, segs + (((uint64_t)c * WA + w) * 512 + t) * 32);
+    gbl_get(q, segs + (((uint64_t)c * WA + w) * SEG_SLOTS + t) * 32);
     p3_add(S, S, q);
   }
   bucket_weighted_sum(S, s_tmp);
@@ -536,13 +545,13 @@ __global__ void __launch_bounds__(256) k_msm_bsum2(const uint32_t* __restrict__ 
 }
 
 // ----------------------------------------------------------- window sums
-__global__ void __launch_bounds__(256) k_msm_wsum(const uint32_t* __restrict__ part, uint32_t nchunks,
+__global__ void __launch_bounds__(256) k_msm_wsum(const uint32_t* __restrict__ part, uint32_t nchunks, uint32_t nrc,
                                                   uint32_t* __restrict__ wsum) {
   __shared__ uint32_t tmp[32 * 4];
   const uint32_t w = blockIdx.x;
   ge_p3 acc;
   ge_p3_identity(acc);
-  for (uint32_t c = threadIdx.x; c < nchunks; c += 256) {
+  for (uint32_t c = threadIdx.x + (w >= WR ? nrc : 0); c < nchunks; c += 256) {
     ge_p3 q;
     gbl_get(q, part + ((uint64_t)w * nchunks + c) * 32);
     p3_add(acc, acc, q);
@@ -612,7 +621,7 @@ size_t coa_msm_ws_bytes(size_t n) {
   const size_t np = 2 * n + 1;
   const size_t nc = coa_msm_chunks_run(n, coa_msm_run(n));
   return al(n * 32) + al(n * 16) + al(np * 128) + al((size_t)WA * np * 2) + al(COA_MSM_PREP_BLOCKS * 36) +
-         al((size_t)WA * nc * 128) + al((size_t)WA * 128) + al(16) + al((size_t)WA * nc * 512 * 128);
+         al((size_t)WA * nc * 128) + al((size_t)WA * 128) + al(16) + al((size_t)WA * nc * SEG_SLOTS * 128);
 }
 
 MsmWs coa_msm_ws_carve(void* base, size_t n) {
@@ -643,13 +652,22 @@ MsmWs coa_msm_ws_carve(void* base, size_t n) {
 
 // Sorted entries per lane: 128 (32,768 points per workgroup) once that still
 // gives >= 512 bucket workgroups (two per CU), else fewer (down to 16) so
-// small batches fill the 256 CUs.  A group whose points fit one workgroup at
+// small batches fill the 256 CUs.  (A run chosen in 64..128 to fill each
+// XCD's last round -- 118 for 2^21 signatures, 6.0 rounds against 5.6 --
+// measured 4.42 ms against 4.38: the tails are not whole rounds.)  A group whose points fit one workgroup at
 // run 16 takes the shortest run of at least 4 that still holds them: one
 // certificate's 135 points, one group through these kernels, p50 0.388 ms at
 // run 16, 0.353 at 8, 0.347 at 4, 0.374 at 2, 0.432 at 1 (tools/gpu_r3_k.sh:
 // the lane runs are the serial part of a one-chunk window, but below 4 more
 // entries become continuation segments the gather adds one by one).
 // COA_MSM_RUN overrides (A/B runs).
+// (chunk, window) pairs with points: the k_msm_bucket grid
+static size_t bucket_pairs(size_t n, uint32_t run) {
+  const size_t chunk = 256 * (size_t)run;
+  const size_t nrc = n / chunk, nc = (2 * n + chunk) / chunk;
+  return nrc * WR + (nc - nrc) * WA;
+}
+
 uint32_t coa_msm_run(size_t n) {
   const char* e = getenv("COA_MSM_RUN");
   if (e) {
@@ -661,11 +679,8 @@ uint32_t coa_msm_run(size_t n) {
     while (256 * run < 2 * n + 1) run <<= 1;
     return run;
   }
-  for (uint32_t run = MAXRUN; run > 16; run >>= 1) {
-    const size_t chunk = 256 * (size_t)run;
-    const size_t heavy = ((2 * n + chunk - 1) / chunk) * WR + ((n + chunk - 1) / chunk) * (WA - WR);
-    if (heavy >= 512) return run;
-  }
+  for (uint32_t run = MAXRUN; run > 16; run >>= 1)
+    if (bucket_pairs(n, run) >= 512) return run;
   return 16;
 }
 
@@ -706,16 +721,19 @@ hipError_t coa_launch_msm(const uint8_t* pks, const uint8_t* sigs, uint32_t n, c
     hipLaunchKernelGGL(k_msm_prep<false>, dim3(pb), dim3(256), 0, s, pks, sigs, ws.k, ws.z, n, np, ws.pts, ws.dig,
                        ws.zpart, ws.bad, ps);
   hipLaunchKernelGGL(k_msm_bpoint, dim3(1), dim3(256), 0, s, ws.zpart, pb, n, np, ws.pts, ws.dig, ps);
-  const uint32_t g8 = (nc * WA + 7) & ~7u;
-  hipLaunchKernelGGL(k_msm_bucket, dim3(g8), dim3(256), 0, s, ws.pts, ws.dig, n, np, run, nc, ws.segs,
-                     ws.part, ps, tree);
+  // chunks holding R points only (z_i weights: WR windows)
+  const uint32_t nrc = (uint32_t)(n / (256 * (size_t)run));
+  const uint32_t g8 = (nrc * WR + (nc - nrc) * WA + 7) & ~7u;
+  hipLaunchKernelGGL(k_msm_bucket, dim3(g8), dim3(256), 0, s, ws.pts, ws.dig, n, np, run, nc, nrc, ws.segs, ws.part,
+                     ps, tree);
   if (tree) {
-    hipLaunchKernelGGL(k_msm_bsum1, dim3(WA * ((nc + kTreeGroup - 1) / kTreeGroup)), dim3(256), 0, s, ws.segs, nc);
+    hipLaunchKernelGGL(k_msm_bsum1, dim3(WA * ((nc + kTreeGroup - 1) / kTreeGroup)), dim3(256), 0, s, ws.segs, nc,
+                       nrc);
     hipLaunchKernelGGL(k_msm_bsum2, dim3(WA), dim3(256), 0, s, ws.segs, nc, ws.wsum);
   } else if (nc > 1) {
     // (one chunk, small groups: its partials already are the window sums,
     // laid out as wsum, window w at w * 32 words)
-    hipLaunchKernelGGL(k_msm_wsum, dim3(WA), dim3(256), 0, s, ws.part, nc, ws.wsum);
+    hipLaunchKernelGGL(k_msm_wsum, dim3(WA), dim3(256), 0, s, ws.part, nc, nrc, ws.wsum);
   }
   hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, s, nc > 1 ? ws.wsum : ws.part, ws.bad, verdict);
   return hipGetLastError();

@@ -296,13 +296,13 @@ struct Dev {
   DevShared* sh = nullptr;
   std::unique_ptr<Worker> worker;
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // second stream of the pipelined certificate path (created on first use)
+  hipStream_t cstreams[3] = {};  // further streams of the pipelined certificate path (created on first use)
   uint32_t* btab = nullptr;  // 128 x (j+1)B, radix-256 fixed-base table (12 KiB)
   uint32_t* comb = nullptr;  // 32 x 128 x (v+1)256^j B comb for k_verify_halved (384 KiB)
   DevBuf msgs, pks, sigs, kbuf, rec, verdicts, scratch, aux, rbuf, seeds, offs, data, out, idx, zs, terms, flags;
   DevBuf cert, cscr;
-  DevBuf certc[2], cscrc[2];  // pipelined certificate path: two chunks in flight
-  PinBuf pinc[2];
+  DevBuf certc[4], cscrc[4];  // pipelined certificate path: up to four chunks in flight
+  PinBuf pinc[4];
   DevBuf msm;  // Pippenger workspace (one large verify_batch group)
   DevBuf lat;  // single-signature latency path: inputs beyond the inline ones
   uint32_t* lat_res = nullptr;  // page-locked result words the latency kernels write
@@ -313,8 +313,8 @@ struct Dev {
   std::mutex mu;
   std::vector<DevBuf*> all() {
     return {&msgs, &pks,  &sigs,  &kbuf, &rec, &verdicts, &scratch,  &aux,     &rbuf,     &seeds,   &offs, &data,
-            &out,  &idx,  &zs,    &terms, &flags, &cert,   &cscr,   &certc[0], &certc[1], &cscrc[0], &cscrc[1],
-            &msm,  &lat};
+            &out,  &idx,  &zs,    &terms, &flags, &cert,   &cscr,   &certc[0], &certc[1], &certc[2], &certc[3],
+            &cscrc[0], &cscrc[1], &cscrc[2], &cscrc[3], &msm, &lat};
   }
 };
 
@@ -778,11 +778,12 @@ int rebuild_context(Dev& d) {
   (void)hipStreamSynchronize(d.stream);
   (void)hipStreamDestroy(d.stream);
   d.stream = nullptr;
-  if (d.stream2) {
-    (void)hipStreamSynchronize(d.stream2);
-    (void)hipStreamDestroy(d.stream2);
-    d.stream2 = nullptr;
-  }
+  for (hipStream_t& cs : d.cstreams)
+    if (cs) {
+      (void)hipStreamSynchronize(cs);
+      (void)hipStreamDestroy(cs);
+      cs = nullptr;
+    }
   for (DevBuf* b : d.all()) b->release();  // per-call buffers (the tables live in DevShared)
   (void)hipGetLastError();
   HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
@@ -1261,43 +1262,67 @@ void cert_pack(uint8_t* h, const CertPack& p, const CertIn& in, size_t lo, size_
   CopyPool::get().copy(segs);
 }
 
-// Jobs (header + votes) per chunk of the pipelined certificate path: ~1,900
-// C3 certificates, ~13 MB of staging, enough jobs for the persistent
-// certificate grid to fill the chip.
-constexpr size_t kCertChunkJobs = 1 << 17;
+// Jobs (header + votes) per chunk of the pipelined certificate path
+// (COA_CERT_CHUNK_JOBS, read per call; default 2^17: ~1,900 C3
+// certificates, ~19 MB of staging, enough jobs for the persistent
+// certificate grid to fill the chip) and chunks in flight
+// (COA_CERT_BUFFERS, 2..4, default 3).
+size_t cert_chunk_jobs() {
+  const char* e = getenv("COA_CERT_CHUNK_JOBS");
+  const long v = e ? atol(e) : 0;
+  return v >= (1 << 12) ? (size_t)v : ((size_t)1 << 17);
+}
+int cert_buffers() {
+  const char* e = getenv("COA_CERT_BUFFERS");
+  const int v = e ? atoi(e) : 3;
+  return v < 2 ? 2 : (v > 4 ? 4 : v);
+}
 
-// Certificates [lo, hi) on one device in chunks, two in flight on the
-// context's two streams: chunk k + 1 is packed (CopyPool) and its copy runs
-// while chunk k's kernel runs, and the PCIe copies of one chunk overlap the
-// other's kernel.  Raw status words out.
+// Certificates [lo, hi) on one device in chunks, up to cert_buffers() in
+// flight on as many streams, each with its own page-locked staging and
+// device buffers: while the GPU runs chunk k's kernel, chunk k + 1's copy
+// crosses PCIe and the host packs chunk k + 2 (CopyPool).  With two buffer
+// sets the host could only pack chunk k + 2 once chunk k had finished, so a
+// round took about (pack + copy + kernel) / 2 per chunk.  Raw status words
+// out.  COA_CERT_TRACE=1 prints the host's pack and wait time per call.
 int cert_shard_pipelined(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_out) {
+  const size_t chunk_jobs = cert_chunk_jobs();
+  const int nb = cert_buffers();
   std::vector<size_t> cuts{lo};
   size_t jobs = 0;
   for (size_t c = lo; c < hi; c++) {
     jobs += 1 + (in.voff[c + 1] - in.voff[c]);
-    if (jobs >= kCertChunkJobs && c + 1 < hi) {
+    if (jobs >= chunk_jobs && c + 1 < hi) {
       cuts.push_back(c + 1);
       jobs = 0;
     }
   }
   cuts.push_back(hi);
-  if (!d.stream2) HIP_TRY(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
-  hipStream_t st[2] = {d.stream, d.stream2};
+  hipStream_t st[4] = {d.stream, nullptr, nullptr, nullptr};
+  for (int b = 1; b < nb; b++) {
+    if (!d.cstreams[b - 1]) HIP_TRY(hipStreamCreateWithFlags(&d.cstreams[b - 1], hipStreamNonBlocking));
+    st[b] = d.cstreams[b - 1];
+  }
   const KeySetP ks = keys_now(d);  // held until every chunk is done
   struct Pending {
     bool busy = false;
     size_t lo = 0, hi = 0, status = 0;
-  } pend[2];
+  } pend[4];
+  const bool trace = env_is("COA_CERT_TRACE", "1");
+  double t_pack = 0, t_wait = 0;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   auto drain = [&](int b) -> int {
     if (!pend[b].busy) return COA_OK;
+    const double t0 = trace ? now() : 0;
     HIP_TRY(hipStreamSynchronize(st[b]));
+    if (trace) t_wait += now() - t0;
     std::memcpy(status_out + pend[b].lo, static_cast<uint8_t*>(d.pinc[b].p) + pend[b].status,
                 (pend[b].hi - pend[b].lo) * 4);
     pend[b].busy = false;
     return COA_OK;
   };
   for (size_t k = 0; k + 1 < cuts.size(); k++) {
-    const int b = (int)(k & 1);
+    const int b = (int)(k % nb);
     int rc = drain(b);  // this buffer set's previous chunk
     if (rc != COA_OK) return rc;
     const size_t clo = cuts[k], chi = cuts[k + 1], nc = chi - clo;
@@ -1307,17 +1332,22 @@ int cert_shard_pipelined(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_
     HIP_TRY(d.certc[b].ensure(p.total));
     HIP_TRY(d.cscrc[b].ensure(coa_cert_scratch_bytes(nc + nv)));
     uint8_t* h = static_cast<uint8_t*>(d.pinc[b].p);
+    const double t0 = trace ? now() : 0;
     cert_pack(h, p, in, clo, chi);
+    if (trace) t_pack += now() - t0;
     HIP_TRY(hipMemcpyAsync(d.certc[b].p, h, p.total, hipMemcpyHostToDevice, st[b]));
     CertArgs a = cert_args(d, *ks, d.certc[b].as<uint8_t>(), p, nc, nv);
     HIP_TRY(coa_launch_cert_verify(a, 1, d.cscrc[b].as<uint32_t>(), st[b]));
     HIP_TRY(hipMemcpyAsync(h + p.status, d.certc[b].as<uint8_t>() + p.status, nc * 4, hipMemcpyDeviceToHost, st[b]));
     pend[b] = {true, clo, chi, p.status};
   }
-  for (int b = 0; b < 2; b++) {
-    const int rc = drain(b);
+  for (size_t k = 0; k < (size_t)nb; k++) {
+    const int rc = drain((int)((cuts.size() - 1 + k) % nb));  // oldest first
     if (rc != COA_OK) return rc;
   }
+  if (trace)
+    fprintf(stderr, "[coa] cert pipeline: %zu chunks x %d buffers, pack %.3f ms, wait %.3f ms\n", cuts.size() - 1, nb,
+            t_pack * 1e3, t_wait * 1e3);
   return COA_OK;
 }
 
@@ -1329,7 +1359,7 @@ int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_
     const int rc = cert_inline(d, in, lo, hi, status_out);
     if (rc != 1) return rc;
   }
-  if (!publish && nc + nv >= 2 * kCertChunkJobs && !env_is("COA_CERT_PIPELINE", "0"))
+  if (!publish && nc + nv >= 2 * cert_chunk_jobs() && !env_is("COA_CERT_PIPELINE", "0"))
     return cert_shard_pipelined(d, in, lo, hi, status_out);
   const CertPack p = cert_layout(nc, nv, hb);
   HIP_TRY(d.pin.ensure(p.total));
@@ -1636,11 +1666,12 @@ int coa_shutdown(void) {
     for (DevBuf* b : d->all()) b->release();
     d->pin.release();
     for (PinBuf& p : d->pinc) p.release();
-    if (d->stream2) {
-      (void)hipStreamSynchronize(d->stream2);
-      (void)hipStreamDestroy(d->stream2);
-      d->stream2 = nullptr;
-    }
+    for (hipStream_t& cs : d->cstreams)
+      if (cs) {
+        (void)hipStreamSynchronize(cs);
+        (void)hipStreamDestroy(cs);
+        cs = nullptr;
+      }
     if (d->lat_res) (void)hipHostFree(d->lat_res);
     d->lat_res = nullptr;
     d->lat_res_cap = 0;
