@@ -425,16 +425,27 @@ def batch_alg_int32_ops_survey(n):
 MSM_WA, MSM_WR = 29, 15  # radix-2^9 windows of the A/B scalars and of the 128-bit weights (coa_msm.h)
 
 
-def msm_chunks(n):
-    """Bucket chunks of one group (coa_msm.hip coa_msm_run / coa_msm_chunks_run)."""
-    run = 16
-    for r in (128, 64, 32):
-        chunk = 256 * r
-        heavy = -(-2 * n // chunk) * MSM_WR + -(-n // chunk) * (MSM_WA - MSM_WR)
-        if heavy >= 512:
-            run = r
-            break
-    return -(-(2 * n + 1) // (256 * run))
+def msm_run(n):
+    """Sorted points per lane of the bucket kernel (coa_msm.hip coa_msm_run:
+    64 for large groups, down to 16; groups that fit one workgroup at run 16
+    take the shortest run >= 4 that holds them)."""
+    if 2 * n + 1 <= 256 * 16:
+        run = 4
+        while 256 * run < 2 * n + 1:
+            run *= 2
+        return run
+    for r in (64, 32):
+        if msm_pairs(n, r) >= 512:
+            return r
+    return 16
+
+
+def msm_pairs(n, run):
+    """(chunk, window) pairs with points: the k_msm_bucket grid (chunks of R
+    points alone have the 15 windows of the 128-bit weights, the rest 29)."""
+    chunk = 256 * run
+    nrc, nc = n // chunk, (2 * n + chunk) // chunk
+    return nrc * MSM_WR + (nc - nrc) * MSM_WA
 
 
 def batch_alg_int32_ops(n):
@@ -445,13 +456,16 @@ def batch_alg_int32_ops(n):
                     one mixed (affine Niels) addition per point per window:
                     R_i over the 15 windows of the 128-bit weights, A_i and B
                     over 29 radix-2^9 windows
-      9 x 29 x nc x (256 + 2 x 256)
-                    per (chunk, window): <= 256 segment merges, the 256-lane
-                    suffix scan and the block reduction (extended additions)
-      9 x 29 x (nc - 1)   window sums over chunks
+      9 x 512 x pairs
+                    per (chunk, window) pair with points: <= 256 segment
+                    merges in the workgroup and its 256 bucket sums added
+                    over the chunks (k_msm_bsum1/2, extended additions)
+      9 x 29 x 256 x 18
+                    per window, once: sum_j j·B_j (a 256-lane suffix scan and
+                    a block reduction, ~18 additions per lane)
       7 x 252 + 9 x 29    the final Horner pass (doublings, window additions)"""
-    nc = msm_chunks(n)
-    fops = (2 * n * 276 + 7 * (44 * n + 29) + 9 * 29 * nc * (256 + 512) + 9 * 29 * (nc - 1) + 7 * 252 + 9 * 29)
+    pairs = msm_pairs(n, msm_run(n))
+    fops = (2 * n * 276 + 7 * (44 * n + 29) + 9 * 512 * pairs + 9 * 29 * 256 * 18 + 7 * 252 + 9 * 29)
     return fops * INT32_OPS_PER_FIELD_OP
 
 

@@ -97,8 +97,8 @@ def test_torsion_groups_exact_via_msm(engine, monkeypatch):
     assert [v == 0 for v in got] == [g["expect"] for g in groups]
 
 
-@pytest.mark.parametrize("run,tree,pstride", [(16, 1, 32), (32, 1, 32), (64, 1, 32), (128, 1, 32), (16, 0, 32),
-                                              (128, 0, 24), (32, 1, 24), (4, 1, 32), (4, 0, 32)])
+@pytest.mark.parametrize("run,tree,pstride", [(16, 1, 32), (32, 1, 32), (64, 1, 32), (16, 0, 32), (64, 0, 24),
+                                              (32, 1, 24), (4, 1, 32), (4, 0, 32)])
 def test_large_group_matches_per_vote_path(engine, monkeypatch, run, tree, pstride):
     """n = 20,011 (odd point counts across chunk boundaries at every run):
     valid, one corrupted s, one non-canonical s, one undecodable R, and equal
@@ -245,10 +245,11 @@ def test_device_entry_resident(engine):
 
 @pytest.mark.parametrize("n", [600_000, 1 << 21])
 def test_large_groups_resident(engine, n):
-    """Large groups (run 128: 18 / 64 chunks of R points alone without
-    workgroups in windows 15..28) on HBM-resident votes: valid with seeded and with equal weights (every
-    R_i digit in one bucket), and one corrupted s in an R-only chunk, in the
-    chunk where the A points start and in the last vote, each an Err."""
+    """Large groups (2^21 at run 64: 128 of 257 chunks hold R points alone
+    and get no workgroups in windows 15..28) on HBM-resident votes: valid
+    with seeded and with equal weights (every R_i digit in one bucket), and
+    one corrupted s in an R-only chunk, in the chunk where the A points
+    start and in the last vote, each an Err."""
     import torch
 
     from workloads import key_seeds, messages

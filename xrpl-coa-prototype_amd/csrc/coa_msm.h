@@ -8,7 +8,7 @@
 #define COA_MSM_NB 256                   // buckets per window
 #define COA_MSM_WA 29                    // windows of a 253-bit scalar (A_i, B)
 #define COA_MSM_WR 15                    // windows of a 128-bit weight z_i (R_i)
-#define COA_MSM_RUN 128                  // max sorted entries per lane in k_msm_bucket
+#define COA_MSM_RUN 64                   // max sorted entries per lane in k_msm_bucket
 #define COA_MSM_CHUNK (256 * COA_MSM_RUN)  // points per bucket workgroup
 #define COA_MSM_PREP_BLOCKS 1024         // k_msm_prep grid (partial sums of z_i s_i)
 

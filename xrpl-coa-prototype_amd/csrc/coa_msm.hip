@@ -49,6 +49,10 @@ constexpr int CHUNK = COA_MSM_CHUNK;
 // bucket segment slots per (chunk, window): 256 owners + 256 continuations
 constexpr uint32_t SEG_SLOTS = 512;
 
+// Digit rows (one per window) padded to whole 16-byte vectors, so the bucket
+// kernel reads its chunk's digits with 16-byte loads.
+__host__ __device__ inline uint32_t dig_stride(uint32_t np) { return (np + 7) & ~7u; }
+
 // Signed radix-2^9 recoding of an 8-word little-endian scalar: W digits in
 // [-256, 255] (a digit of value 256 never occurs: 511 + carry = 512 is 0
 // with carry).  The scalars are < 2^253 (W = 29) or < 2^128 (W = 15), so
@@ -267,7 +271,7 @@ __global__ void __launch_bounds__(256) k_msm_prep(const uint8_t* __restrict__ pk
       recode<WR>(d, z);
       if (leader) {
 #pragma unroll
-        for (int w = 0; w < WR; w++) dig[(uint64_t)w * np + i] = (int16_t)d[w];
+        for (int w = 0; w < WR; w++) dig[(uint64_t)w * dig_stride(np) + i] = (int16_t)d[w];
         uint32_t cy = 0;
 #pragma unroll
         for (int w = 0; w < 8; w++) acc[w] = addc32(acc[w], zsv.v[w], cy, cy);
@@ -286,7 +290,7 @@ __global__ void __launch_bounds__(256) k_msm_prep(const uint8_t* __restrict__ pk
       recode<WA>(d, a.v);
       if (leader) {
 #pragma unroll
-        for (int w = 0; w < WA; w++) dig[(uint64_t)w * np + n + i] = (int16_t)d[w];
+        for (int w = 0; w < WA; w++) dig[(uint64_t)w * dig_stride(np) + n + i] = (int16_t)d[w];
       }
     }
     if (!ok && leader) atomicOr(bad, 1u);
@@ -344,17 +348,21 @@ __global__ void __launch_bounds__(256) k_msm_bpoint(const uint32_t* __restrict__
     int d[WA];
     recode<WA>(d, nb.v);
 #pragma unroll
-    for (int w = 0; w < WA; w++) dig[(uint64_t)w * np + 2 * n] = (int16_t)d[w];
+    for (int w = 0; w < WA; w++) dig[(uint64_t)w * dig_stride(np) + 2 * n] = (int16_t)d[w];
   }
 }
 
 // ------------------------------------------------------- bucket phase
-__global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restrict__ pts,
+// Tree: the large-group form (bucket sums left for k_msm_bsum*), three
+// workgroups per CU; else one chunk's sum_j j·B_j in the workgroup (small
+// groups), two per CU (no spills).
+template <bool Tree>
+__global__ void __launch_bounds__(256, Tree ? 3 : 2) k_msm_bucket(const uint32_t* __restrict__ pts,
                                                        const int16_t* __restrict__ dig, uint32_t n, uint32_t np,
                                                        uint32_t run, uint32_t nchunks, uint32_t nrc,
                                                        uint32_t* __restrict__ segs, uint32_t* __restrict__ part,
-                                                       uint32_t ps, uint32_t tree) {
-  // 66 KiB of LDS: two workgroups per CU.  The bucket segments go to this
+                                                       uint32_t ps, uint32_t probe) {
+  // 34 KiB of LDS and <= 168 VGPRs: three workgroups per CU.  The bucket segments go to this
   // (chunk, window)'s 64 KiB slice of `segs` (owner segments by bucket,
   // continuation segments by lane): written once, read once, L2-resident.
   __shared__ uint16_t s_sorted[CHUNK];     // (local << 1) | negative, grouped by |digit|
@@ -383,15 +391,37 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
   const uint32_t cnt = min(chunk, np - base);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   uint32_t* out = part + ((uint64_t)w * nchunks + ch) * 32;
-  const int16_t* dw = dig + (uint64_t)w * np + base;
   const uint32_t rlo = (w >= WR && base < n) ? n - base : 0;  // skip R points above their windows
+  // The chunk's digits, eight per 16-byte load, all loads in flight at once
+  // and kept in registers for both passes of the counting sort (one load per
+  // entry and pass, each waiting out its latency, took 1.45 ms of the 2^21
+  // group's bucket phase).
+  constexpr int VPT = CHUNK / 8 / 256;  // 16-byte vectors per thread
+  const uint4* dv = reinterpret_cast<const uint4*>(dig + (uint64_t)w * dig_stride(np) + base);
+  const uint32_t nvec = (cnt + 7) / 8;
+  uint4 dgt[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; k++) {
+    const uint32_t j = t + 256 * k;
+    dgt[k] = j < nvec ? dv[j] : make_uint4(0, 0, 0, 0);
+  }
+  // digit q (0..7) of vector k, 0 outside [rlo, cnt)
+  auto digit = [&](int k, int q) -> int {
+    const uint32_t l = (t + 256 * k) * 8 + q;
+    const uint32_t word = q < 2 ? dgt[k].x : q < 4 ? dgt[k].y : q < 6 ? dgt[k].z : dgt[k].w;
+    const int d = (int16_t)(q & 1 ? word >> 16 : word & 0xffffu);
+    return (l < cnt && l >= rlo) ? d : 0;
+  };
 
   for (int j = t; j < NB + 2; j += 256) s_hist[j] = 0;
   __syncthreads();
-  for (uint32_t l = t; l < cnt; l += 256) {
-    const int d = l < rlo ? 0 : dw[l];
-    if (d) atomicAdd(&s_hist[d < 0 ? -d : d], 1u);
-  }
+#pragma unroll
+  for (int k = 0; k < VPT; k++)
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int d = digit(k, q);
+      if (d) atomicAdd(&s_hist[d < 0 ? -d : d], 1u);
+    }
   __syncthreads();
   {  // exclusive scan of hist[1..256] (thread t: bucket t + 1)
     const uint32_t v = s_hist[t + 1];
@@ -412,26 +442,34 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
     s_hist[t + 1] = excl;
   }
   __syncthreads();
-  for (uint32_t l = t; l < cnt; l += 256) {
-    const int d = l < rlo ? 0 : dw[l];
-    if (d) {
-      const uint32_t pos = atomicAdd(&s_hist[d < 0 ? -d : d], 1u);
-      s_sorted[pos] = (uint16_t)((l << 1) | (d < 0 ? 1u : 0u));
+#pragma unroll
+  for (int k = 0; k < VPT; k++)
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int d = digit(k, q);
+      if (d) {
+        const uint32_t l = (t + 256 * k) * 8 + q;
+        const uint32_t pos = atomicAdd(&s_hist[d < 0 ? -d : d], 1u);
+        s_sorted[pos] = (uint16_t)((l << 1) | (d < 0 ? 1u : 0u));
+      }
     }
-  }
   __syncthreads();
   const uint32_t nnz = s_off[NB + 1];
 
   // balanced accumulation: lane t adds sorted entries [t·run, (t+1)·run),
   // the load of the next point in flight during each addition (the points
-  // are random 128-byte reads from the chunk's 4 MiB of points).  Two
-  // independent chains per lane, and the products interleaved column by
-  // column (ge_madd_il), both measured slower: 5.85 / 6.83 / 5.30 ms against
-  // 5.17 for the 2^21-signature group (profiles/r04_msm_ab.txt).
+  // are random 128-byte reads from the chunk's 2 MiB of points).  Iteration
+  // e loads entry e and adds entry e - 1; no point is loaded before the loop:
+  // with a load there, InstCombine folded the header's phi(load before the
+  // loop, load in the loop) into one load of phi(addresses) at the top of
+  // each iteration, consumed at once -- the prefetch gone, every addition
+  // waiting out its miss (`s_waitcnt vmcnt(0)` ahead of each one in the
+  // ISA).  Two independent chains per lane, and the products interleaved
+  // column by column (ge_madd_il), were no faster (profiles/r04_msm_ab.txt).
   uint32_t* const seg = segs + (uint64_t)slot * SEG_SLOTS * 32;  // [bucket - 1] owners, [256 + lane] continuations
   {
     const uint32_t lo = t * run, hi = min(lo + run, nnz);
-    if (lo < hi) {
+    if (lo < hi && probe < 3) {
       const uint32_t* pb = pts + (uint64_t)base * ps;
       uint32_t cur = 1;  // bucket of entry lo: last j with s_off[j] <= lo
 #pragma unroll
@@ -439,29 +477,40 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
         if (s_off[cur + step] <= lo) cur += step;
       bool owner = s_off[cur] == lo;
       uint32_t nxt = s_off[cur + 1];
-      uint32_t ent = s_sorted[lo];
       ge_niels q;
-      niels_load(q, pb + (uint64_t)(ent >> 1) * ps);
+      ge_niels_identity(q);
+      uint32_t ent = 0;
       ge_p3 acc;
       ge_p3_identity(acc);
 #pragma unroll 1
-      for (uint32_t e = lo; e < hi; e++) {
-        if (e == nxt) {  // bucket cur is complete: flush, move to the bucket of e
-          gbl_put(seg + (owner ? cur - 1 : 256 + t) * 32, acc);
-          ge_p3_identity(acc);
-          owner = true;
-          do {
-            cur++;
-            nxt = s_off[cur + 1];
-          } while (nxt == e);
-        }
-        const uint32_t entn = s_sorted[e + 1 < hi ? e + 1 : e];
+      for (uint32_t e = lo; e <= hi; e++) {
         ge_niels qn;
-        niels_load(qn, pb + (uint64_t)(entn >> 1) * ps);
-        ge_niels_cneg(q, (ent & 1u) != 0);
-        ge_p1p1 r;
-        ge_madd(r, acc, q);
-        ge_p1p1_to_p3(acc, r);
+        uint32_t entn = 0;
+        if (e < hi && probe < 2) {
+          entn = s_sorted[e];
+          niels_load(qn, pb + (uint64_t)(entn >> 1) * ps);
+        } else {
+          ge_niels_identity(qn);
+        }
+        if (e > lo) {  // add entry e - 1 (e - lo is the same on every lane)
+          if (e - 1 == nxt) {  // bucket cur is complete: flush, move to the bucket of e - 1
+            gbl_put(seg + (owner ? cur - 1 : 256 + t) * 32, acc);
+            ge_p3_identity(acc);
+            owner = true;
+            do {
+              cur++;
+              nxt = s_off[cur + 1];
+            } while (nxt == e - 1);
+          }
+          if (probe == 0) {
+            ge_niels_cneg(q, (ent & 1u) != 0);
+            ge_p1p1 r;
+            ge_madd(r, acc, q);
+            ge_p1p1_to_p3(acc, r);
+          } else {
+            acc.X.v[0] ^= q.yplusx.v[0];
+          }
+        }
         q = qn;
         ent = entn;
       }
@@ -476,17 +525,17 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(const uint32_t* __restric
   ge_p3_identity(S);
   {
     const uint32_t o0 = s_off[t + 1], o1 = s_off[t + 2];
-    if (o1 > o0) {
+    if (o1 > o0 && (probe < 4 || probe == 5)) {
       gbl_get(S, seg + t * 32);
 #pragma unroll 1
-      for (uint32_t l = o0 / run + 1; l * run < o1; l++) {
+      for (uint32_t l = o0 / run + 1; l * run < o1 && probe != 5; l++) {
         ge_p3 h;
         gbl_get(h, seg + (256 + l) * 32);
         p3_add(S, S, h);
       }
     }
   }
-  if (tree) {  // bucket sums of this (chunk, window) to its owner slots; summed over chunks by k_msm_bsum*
+  if constexpr (Tree) {  // bucket sums of this (chunk, window) to its owner slots; summed over chunks by k_msm_bsum*
     __syncthreads();  // every lane has read its owner segment
     gbl_put(seg + t * 32, S);
     return;
@@ -620,7 +669,7 @@ uint32_t coa_msm_run(size_t n);
 size_t coa_msm_ws_bytes(size_t n) {
   const size_t np = 2 * n + 1;
   const size_t nc = coa_msm_chunks_run(n, coa_msm_run(n));
-  return al(n * 32) + al(n * 16) + al(np * 128) + al((size_t)WA * np * 2) + al(COA_MSM_PREP_BLOCKS * 36) +
+  return al(n * 32) + al(n * 16) + al(np * 128) + al((size_t)WA * dig_stride(np) * 2) + al(COA_MSM_PREP_BLOCKS * 36) +
          al((size_t)WA * nc * 128) + al((size_t)WA * 128) + al(16) + al((size_t)WA * nc * SEG_SLOTS * 128);
 }
 
@@ -637,7 +686,7 @@ MsmWs coa_msm_ws_carve(void* base, size_t n) {
   w.pts = reinterpret_cast<uint32_t*>(p);
   p += al(np * 128);
   w.dig = reinterpret_cast<int16_t*>(p);
-  p += al((size_t)WA * np * 2);
+  p += al((size_t)WA * dig_stride(np) * 2);
   w.zpart = reinterpret_cast<uint32_t*>(p);
   p += al(COA_MSM_PREP_BLOCKS * 36);
   w.part = reinterpret_cast<uint32_t*>(p);
@@ -650,11 +699,14 @@ MsmWs coa_msm_ws_carve(void* base, size_t n) {
   return w;
 }
 
-// Sorted entries per lane: 128 (32,768 points per workgroup) once that still
-// gives >= 512 bucket workgroups (two per CU), else fewer (down to 16) so
-// small batches fill the 256 CUs.  (A run chosen in 64..128 to fill each
-// XCD's last round -- 118 for 2^21 signatures, 6.0 rounds against 5.6 --
-// measured 4.42 ms against 4.38: the tails are not whole rounds.)  A group whose points fit one workgroup at
+// Sorted entries per lane: MAXRUN = 64 (16,384 points per workgroup, 36 KiB
+// of LDS: three workgroups per CU at k_msm_bucket's 149 VGPRs) once that
+// still gives >= 512 bucket workgroups, else fewer (down to 16) so small
+// batches fill the 256 CUs.  For 2^21 signatures run 64 at three waves per
+// SIMD took 4.07 ms against run 128 (32,768 points, 68 KiB, two workgroups
+// per CU) at 4.28 ms.  (A run chosen in 64..128 to fill each XCD's last
+// round -- 118, 6.0 rounds against 5.6 -- measured 4.42 ms against 4.38 at
+// the two-wave build: the tails are not whole rounds.)  A group whose points fit one workgroup at
 // run 16 takes the shortest run of at least 4 that still holds them: one
 // certificate's 135 points, one group through these kernels, p50 0.388 ms at
 // run 16, 0.353 at 8, 0.347 at 4, 0.374 at 2, 0.432 at 1 (tools/gpu_r3_k.sh:
@@ -724,8 +776,14 @@ hipError_t coa_launch_msm(const uint8_t* pks, const uint8_t* sigs, uint32_t n, c
   // chunks holding R points only (z_i weights: WR windows)
   const uint32_t nrc = (uint32_t)(n / (256 * (size_t)run));
   const uint32_t g8 = (nrc * WR + (nc - nrc) * WA + 7) & ~7u;
-  hipLaunchKernelGGL(k_msm_bucket, dim3(g8), dim3(256), 0, s, ws.pts, ws.dig, n, np, run, nc, nrc, ws.segs, ws.part,
-                     ps, tree);
+  const char* pe = getenv("COA_MSM_PROBE");  // timing probe only: 1 skips the additions, 2 the loads too
+  const uint32_t probe = pe ? (uint32_t)atoi(pe) : 0u;
+  if (tree)
+    hipLaunchKernelGGL(k_msm_bucket<true>, dim3(g8), dim3(256), 0, s, ws.pts, ws.dig, n, np, run, nc, nrc, ws.segs,
+                       ws.part, ps, probe);
+  else
+    hipLaunchKernelGGL(k_msm_bucket<false>, dim3(g8), dim3(256), 0, s, ws.pts, ws.dig, n, np, run, nc, nrc, ws.segs,
+                       ws.part, ps, probe);
   if (tree) {
     hipLaunchKernelGGL(k_msm_bsum1, dim3(WA * ((nc + kTreeGroup - 1) / kTreeGroup)), dim3(256), 0, s, ws.segs, nc,
                        nrc);
