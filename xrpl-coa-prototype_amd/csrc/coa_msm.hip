@@ -17,14 +17,16 @@
 //                 encoding checks, decompression to Niels form, z h mod l,
 //                 digits, block partial sums of z s (288-bit integers)
 //   k_msm_bpoint  one workgroup: b = -(sum z s) mod l, B and its digits
-//   k_msm_bucket  one workgroup per (chunk of 256·run points, window):
-//                 LDS counting sort of the chunk's points by |digit|; every
-//                 lane then adds `run` consecutive sorted points (balanced
-//                 whatever the digit distribution), flushing each completed
-//                 bucket segment to LDS; lane t gathers bucket t+1 from its
-//                 owner's segment and the continuation segments of the lanes
-//                 after it; sum_j j·B_j by a 256-lane suffix scan plus a
-//                 reduction (wave shuffles, LDS across the four waves)
+//   k_msm_bucket  one workgroup per (chunk of 256·run points, window) pair
+//                 with points: LDS counting sort of the chunk's points by
+//                 |digit|; every lane then adds `run` consecutive sorted
+//                 points (balanced whatever the digit distribution),
+//                 flushing each completed bucket segment; the segments of
+//                 a bucket meet in a segmented scan over the lanes (LDS);
+//                 large groups leave the 256 bucket sums for k_msm_bsum*,
+//                 one chunk computes sum_j j·B_j by a 256-lane suffix scan
+//                 plus a reduction (wave shuffles, LDS across the four waves)
+//   k_msm_bsum1/2 bucket sums over the chunks, then sum_j j·B_j per window
 //   k_msm_wsum    one workgroup per window: sum of the chunk partials
 //   k_msm_final   one wave: Horner over the windows (9 doublings each) in
 //                 row form (coa_fe_wave.h): each step's four products on the
@@ -361,7 +363,7 @@ __global__ void __launch_bounds__(256, Tree ? 3 : 2) k_msm_bucket(const uint32_t
                                                        const int16_t* __restrict__ dig, uint32_t n, uint32_t np,
                                                        uint32_t run, uint32_t nchunks, uint32_t nrc,
                                                        uint32_t* __restrict__ segs, uint32_t* __restrict__ part,
-                                                       uint32_t ps, uint32_t probe) {
+                                                       uint32_t ps) {
   // 34 KiB of LDS and <= 168 VGPRs: three workgroups per CU.  The bucket segments go to this
   // (chunk, window)'s 64 KiB slice of `segs` (owner segments by bucket,
   // continuation segments by lane): written once, read once, L2-resident.
@@ -413,6 +415,9 @@ __global__ void __launch_bounds__(256, Tree ? 3 : 2) k_msm_bucket(const uint32_t
     return (l < cnt && l >= rlo) ? d : 0;
   };
 
+  // the sort is a latency chain (loads, LDS atomics, barriers): at raised
+  // priority beside the other workgroups' addition loops (-2.3 %)
+  __builtin_amdgcn_s_setprio(2);
   for (int j = t; j < NB + 2; j += 256) s_hist[j] = 0;
   __syncthreads();
 #pragma unroll
@@ -454,6 +459,7 @@ __global__ void __launch_bounds__(256, Tree ? 3 : 2) k_msm_bucket(const uint32_t
       }
     }
   __syncthreads();
+  __builtin_amdgcn_s_setprio(0);
   const uint32_t nnz = s_off[NB + 1];
 
   // balanced accumulation: lane t adds sorted entries [t·run, (t+1)·run),
@@ -469,7 +475,7 @@ __global__ void __launch_bounds__(256, Tree ? 3 : 2) k_msm_bucket(const uint32_t
   uint32_t* const seg = segs + (uint64_t)slot * SEG_SLOTS * 32;  // [bucket - 1] owners, [256 + lane] continuations
   {
     const uint32_t lo = t * run, hi = min(lo + run, nnz);
-    if (lo < hi && probe < 3) {
+    if (lo < hi) {
       const uint32_t* pb = pts + (uint64_t)base * ps;
       uint32_t cur = 1;  // bucket of entry lo: last j with s_off[j] <= lo
 #pragma unroll
@@ -486,7 +492,7 @@ __global__ void __launch_bounds__(256, Tree ? 3 : 2) k_msm_bucket(const uint32_t
       for (uint32_t e = lo; e <= hi; e++) {
         ge_niels qn;
         uint32_t entn = 0;
-        if (e < hi && probe < 2) {
+        if (e < hi) {
           entn = s_sorted[e];
           niels_load(qn, pb + (uint64_t)(entn >> 1) * ps);
         } else {
@@ -502,14 +508,10 @@ __global__ void __launch_bounds__(256, Tree ? 3 : 2) k_msm_bucket(const uint32_t
               nxt = s_off[cur + 1];
             } while (nxt == e - 1);
           }
-          if (probe == 0) {
-            ge_niels_cneg(q, (ent & 1u) != 0);
-            ge_p1p1 r;
-            ge_madd(r, acc, q);
-            ge_p1p1_to_p3(acc, r);
-          } else {
-            acc.X.v[0] ^= q.yplusx.v[0];
-          }
+          ge_niels_cneg(q, (ent & 1u) != 0);
+          ge_p1p1 r;
+          ge_madd(r, acc, q);
+          ge_p1p1_to_p3(acc, r);
         }
         q = qn;
         ent = entn;
@@ -517,26 +519,71 @@ __global__ void __launch_bounds__(256, Tree ? 3 : 2) k_msm_bucket(const uint32_t
       gbl_put(seg + (owner ? cur - 1 : 256 + t) * 32, acc);
     }
   }
-  __syncthreads();
 
-  // lane t gathers bucket t + 1: its owner's segment plus the continuation
-  // segments of the lanes whose runs start inside it
+  // Merge: bucket b's sum is its owner segment plus the continuation
+  // segments ("pieces") of the lanes whose runs start strictly inside it,
+  // lanes f_b .. g_b (contiguous).  Pieces are summed by a segmented
+  // Hillis-Steele scan over the 256 lanes in LDS (the sorted entries' 32 KiB,
+  // free now), ceil(log2(longest piece list)) rounds, so a bucket holding
+  // most of the chunk -- the top window's digits (z_i < 2^128: |d| <= 4;
+  // z h mod l < 2^253: |d| <= 1), or equal weights -- costs ~8 dependent
+  // additions instead of one lane adding up to 255 pieces in a row (that
+  // chain, in the top windows' workgroups, was 0.76 ms of the 2^21 group's
+  // bucket phase: profiles/r04_msm_ab.txt).
+  __syncthreads();  // every flush is out; s_sorted is free
+  uint32_t* const s_pc = reinterpret_cast<uint32_t*>(s_sorted);  // [32 words][256 lanes]
+  static_assert(CHUNK * 2 >= 256 * 128, "piece scratch");
+  ge_p3 C;
+  ge_p3_identity(C);
+  uint32_t pf = t + 1;  // first piece lane of this lane's bucket (t + 1: no piece)
+  {
+    const uint32_t e = t * run;
+    if (e < nnz) {
+      uint32_t b = 1;
+#pragma unroll
+      for (uint32_t step = 128; step > 0; step >>= 1)
+        if (s_off[b + step] <= e) b += step;
+      if (s_off[b] != e) {  // this lane's run starts inside bucket b: a piece
+        pf = s_off[b] / run + 1;
+        gbl_get(C, seg + (256 + t) * 32);
+      }
+    }
+  }
+  uint32_t len = t + 1 - pf;  // this lane's position in its piece list (0: none)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) len = max(len, (uint32_t)__shfl_xor((int)len, o, 64));
+  if ((t & 63) == 0) s_wtot[wave] = len;
+  __syncthreads();
+  const uint32_t maxlen = max(max(s_wtot[0], s_wtot[1]), max(s_wtot[2], s_wtot[3]));
+#pragma unroll 1
+  for (uint32_t st = 1; st < maxlen; st <<= 1) {
+    lds_put(s_pc, 256, t, C);
+    __syncthreads();
+    if (t >= pf + st && t < 256) {  // t - st is a piece of the same bucket
+      ge_p3 h;
+      lds_get(h, s_pc, 256, t - st);
+      p3_add(C, C, h);
+    }
+    __syncthreads();
+  }
+  lds_put(s_pc, 256, t, C);  // lane g_b now holds the sum of bucket b's pieces
+  __syncthreads();
+  // lane t: bucket t + 1 = owner segment + its pieces' sum (lane g)
   ge_p3 S;
   ge_p3_identity(S);
   {
     const uint32_t o0 = s_off[t + 1], o1 = s_off[t + 2];
-    if (o1 > o0 && (probe < 4 || probe == 5)) {
+    if (o1 > o0) {
       gbl_get(S, seg + t * 32);
-#pragma unroll 1
-      for (uint32_t l = o0 / run + 1; l * run < o1 && probe != 5; l++) {
+      const uint32_t f = o0 / run + 1, g = (o1 - 1) / run;
+      if (g >= f) {
         ge_p3 h;
-        gbl_get(h, seg + (256 + l) * 32);
+        lds_get(h, s_pc, 256, g);
         p3_add(S, S, h);
       }
     }
   }
   if constexpr (Tree) {  // bucket sums of this (chunk, window) to its owner slots; summed over chunks by k_msm_bsum*
-    __syncthreads();  // every lane has read its owner segment
     gbl_put(seg + t * 32, S);
     return;
   }
@@ -552,7 +599,10 @@ __global__ void __launch_bounds__(256, Tree ? 3 : 2) k_msm_bucket(const uint32_t
 // workgroups); the buckets are summed over the chunks first -- one addition
 // per (chunk, window, bucket) -- and the weighted sum runs once per window.
 // Level 1: workgroup (window w, group g) adds bucket t over chunks
-// [16g, 16g + 16) into the slot of chunk 16g.
+// [16g, 16g + 16) into the slot of chunk 16g.  (One wave per (window,
+// bucket) with a 64-lane shuffle tree instead -- a 10-addition chain against
+// 33 -- took 196 us against 105: twenty times the additions, at three waves
+// per SIMD, made it throughput-bound.)
 constexpr uint32_t kTreeGroup = 16;
 // The nrc chunks of R points alone have no workgroup (and no segments) in
 // windows >= WR: their buckets are empty there and are skipped.
@@ -776,14 +826,12 @@ hipError_t coa_launch_msm(const uint8_t* pks, const uint8_t* sigs, uint32_t n, c
   // chunks holding R points only (z_i weights: WR windows)
   const uint32_t nrc = (uint32_t)(n / (256 * (size_t)run));
   const uint32_t g8 = (nrc * WR + (nc - nrc) * WA + 7) & ~7u;
-  const char* pe = getenv("COA_MSM_PROBE");  // timing probe only: 1 skips the additions, 2 the loads too
-  const uint32_t probe = pe ? (uint32_t)atoi(pe) : 0u;
   if (tree)
     hipLaunchKernelGGL(k_msm_bucket<true>, dim3(g8), dim3(256), 0, s, ws.pts, ws.dig, n, np, run, nc, nrc, ws.segs,
-                       ws.part, ps, probe);
+                       ws.part, ps);
   else
     hipLaunchKernelGGL(k_msm_bucket<false>, dim3(g8), dim3(256), 0, s, ws.pts, ws.dig, n, np, run, nc, nrc, ws.segs,
-                       ws.part, ps, probe);
+                       ws.part, ps);
   if (tree) {
     hipLaunchKernelGGL(k_msm_bsum1, dim3(WA * ((nc + kTreeGroup - 1) / kTreeGroup)), dim3(256), 0, s, ws.segs, nc,
                        nrc);
