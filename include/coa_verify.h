@@ -382,7 +382,7 @@ typedef struct {
   uint32_t window_max_kinds;  /* COA_QUEUE_KIND_* bits */
   int32_t stream_kind;        /* COA_QUEUE_STREAM_*: how the slots' streams were made */
   double slot_wait_us_max;
-  uint64_t staging_grows;
+  uint64_t staging_grows;     /* windows that had to enlarge a slot's staging or workspace (warm-up not counted) */
   uint32_t slots_verify, slots_digest; /* device slots of each lane, over all devices */
 } coa_queue_metrics_t;
 #define COA_QUEUE_KIND_SIGNATURES 1u

@@ -98,8 +98,6 @@ struct Slot {
   size_t o_v = 0, o_c = 0, o_d = 0;
 };
 
-std::atomic<uint64_t> g_grows{0};  // staging reallocations (all backends)
-
 // A slot's staging grows geometrically (twice what a window needs) and an
 // outgrown buffer is not freed on the launch path: hipFree / hipHostFree wait
 // for the whole device, i.e. for every other slot's window in flight (round
@@ -108,7 +106,6 @@ std::atomic<uint64_t> g_grows{0};  // staging reallocations (all backends)
 // the slot; the geometric growth bounds them to the final size.
 hipError_t grow_pinned(void*& p, size_t& cap, size_t want, std::vector<Grave>& grave) {
   if (want <= cap) return hipSuccess;
-  g_grows++;
   if (p) grave.push_back({p, true});
   p = nullptr;
   cap = 0;
@@ -119,7 +116,6 @@ hipError_t grow_pinned(void*& p, size_t& cap, size_t want, std::vector<Grave>& g
 }
 hipError_t grow_dev(void*& p, size_t& cap, size_t want, std::vector<Grave>& grave) {
   if (want <= cap) return hipSuccess;
-  g_grows++;
   if (p) grave.push_back({p, false});
   p = nullptr;
   cap = 0;
@@ -206,7 +202,9 @@ class HipBackend : public coa_q::Backend {
 
   int slots() const override { return (int)slots_.size(); }
   int devices() const override { return std::max<int>(1, (int)devs_.size()); }
-  uint64_t grows() const override { return g_grows.load(); }
+  // windows of this queue lane that had to enlarge a slot's staging or
+  // workspace (the warm-up at creation not counted)
+  uint64_t grows() const override { return grows_.load(); }
 
   // Everything a first window would otherwise pay for, done at queue
   // creation: the slots' streams, their page-locked and device staging, and
@@ -371,12 +369,14 @@ class HipBackend : public coa_q::Backend {
     const size_t out_bytes = o;
     const size_t ws_v = L.nv ? coa_verify_workspace_bytes(L.nv) : 0;
     const size_t ws_c = L.nc ? coa_certificate_workspace_bytes(L.nc, L.nvotes) : 0;
+    const size_t caps0 = sl.cap_hin + sl.cap_hout + sl.cap_din + sl.cap_dout + sl.cap_ws;
     if (grow_pinned(sl.hin, sl.cap_hin, in_bytes, sl.grave) != hipSuccess ||
         grow_pinned(sl.hout, sl.cap_hout, out_bytes, sl.grave) != hipSuccess ||
         grow_dev(sl.din, sl.cap_din, in_bytes, sl.grave) != hipSuccess ||
         grow_dev(sl.dout, sl.cap_dout, out_bytes, sl.grave) != hipSuccess ||
         grow_dev(sl.ws, sl.cap_ws, std::max(ws_v, ws_c) + 256, sl.grave) != hipSuccess)
       return COA_ENOMEM;
+    if (sl.cap_hin + sl.cap_hout + sl.cap_din + sl.cap_dout + sl.cap_ws != caps0) grows_++;
     uint8_t* h = static_cast<uint8_t*>(sl.hin);
     // the bulk copies of a large window go to the runtime's copy threads (a
     // C3 round is ~68 MB: one thread's memcpy would be slower than PCIe)
@@ -544,6 +544,7 @@ class HipBackend : public coa_q::Backend {
   std::vector<int> devs_;     // distinct device ids
   const int lane_;
   int kind_ = COA_QUEUE_STREAM_PLAIN;
+  std::atomic<uint64_t> grows_{0};
   size_t next_ = 0;
   std::mutex m_;
   std::condition_variable cv_;
