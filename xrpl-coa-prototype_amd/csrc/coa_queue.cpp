@@ -553,6 +553,17 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
   for (int k = 0; k < coa_q::LANES; k++) {
     Lane& L = q->lanes[k];
     L.max_batch = max_batch ? max_batch : 65536;
+    if (k == coa_q::LANE_DIGEST) {
+      // Digest windows hold whole ~500 KB worker batches: at most
+      // COA_QUEUE_DIGEST_MAX (default 96, ~49 MB) per window, so a backlog
+      // is split over the lane's slots and the staging warmed at creation
+      // (2 x 32 MB per slot) is never regrown on the launch path.  Unbounded,
+      // a backlog at 4,000 batches/s became windows of up to 920 batches
+      // (467 MB) whose page-locked regrowth held a window 218-234 ms.
+      const char* e = getenv("COA_QUEUE_DIGEST_MAX");
+      const size_t cap = e ? (size_t)std::max(1, atoi(e)) : 96;
+      L.max_batch = std::min(L.max_batch, cap);
+    }
     L.max_delay = std::chrono::microseconds(max_delay_us);
     if (const char* e = getenv("COA_QUEUE_HELPERS")) L.n_helpers = std::max(0, std::min(15, atoi(e)));
     if (const char* e = getenv("COA_QUEUE_IDLE_LAUNCH")) L.idle_launch = (size_t)std::max(0, std::min(64, atoi(e)));

@@ -216,7 +216,8 @@ class HipBackend : public coa_q::Backend {
     for (Slot& sl : slots_) {
       const size_t pre_din = lane_ == coa_q::LANE_DIGEST ? (32u << 20) : (4u << 20);
       if (hipSetDevice(sl.dev) != hipSuccess || grow_dev(sl.din, sl.cap_din, pre_din, sl.grave) != hipSuccess ||
-          grow_dev(sl.dout, sl.cap_dout, 256u << 10, sl.grave) != hipSuccess)
+          grow_dev(sl.dout, sl.cap_dout, 256u << 10, sl.grave) != hipSuccess ||
+          grow_dev(sl.ws, sl.cap_ws, 256, sl.grave) != hipSuccess)
         continue;  // the first launch regrows and reports any failure
       (void)hipMemcpyAsync(sl.din, sl.hin, 4096, hipMemcpyHostToDevice, sl.s);
       (void)hipMemsetAsync(sl.dout, 0, 4096, sl.s);
