@@ -648,11 +648,23 @@ int coa_queue_submit_certificate(coa_queue* q, const uint8_t* header_data, size_
 
 int coa_queue_submit_digest(coa_queue* q, const uint8_t* data, size_t len, coa_verdict_cb cb, void* user) {
   if (!q || (len && !data) || !cb) return COA_EINVAL;
-  COA_Q_INTAKE(q, K_DIGEST)
-  if (len) w.d_data.insert(w.d_data.end(), data, data + len);
-  w.d_offs.push_back(w.d_data.size());
-  submitted(ln, sh, sl, K_DIGEST, (uint32_t)w.nd++, 1, cb, user, 1);
-  return COA_OK;
+  // A shard's window holds at most the lane's max_batch digests (the
+  // collector takes whole shards): a producer whose shard is full moves on to
+  // the next one, so one busy producer thread cannot build a window of
+  // hundreds of batches behind a backlog (the last shard takes the overflow).
+  Lane* ln = &q->lane_of(K_DIGEST);
+  const size_t home = thread_ordinal() % kShards;
+  for (size_t k = 0;; k++) {
+    Shard& sh = ln->shards[(home + k) % kShards];
+    std::unique_lock<std::mutex> sl(sh.mu);
+    if (ln->stop.load()) return COA_EINVAL;
+    if (sh.items >= ln->max_batch && k + 1 < kShards) continue;
+    Window& w = *sh.w;
+    if (len) w.d_data.insert(w.d_data.end(), data, data + len);
+    w.d_offs.push_back(w.d_data.size());
+    submitted(ln, sh, sl, K_DIGEST, (uint32_t)w.nd++, 1, cb, user, 1);
+    return COA_OK;
+  }
 }
 
 int coa_queue_flush(coa_queue* q) {
