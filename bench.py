@@ -427,16 +427,24 @@ MSM_WA, MSM_WR = 29, 15  # radix-2^9 windows of the A/B scalars and of the 128-b
 
 def msm_run(n):
     """Sorted points per lane of the bucket kernel (coa_msm.hip coa_msm_run:
-    64 for large groups, down to 16; groups that fit one workgroup at run 16
-    take the shortest run >= 4 that holds them)."""
+    48..64 for large groups, down to 16; groups that fit one workgroup at run
+    16 take the shortest run >= 4 that holds them)."""
     if 2 * n + 1 <= 256 * 16:
         run = 4
         while 256 * run < 2 * n + 1:
             run *= 2
         return run
-    for r in (64, 32):
-        if msm_pairs(n, r) >= 512:
-            return r
+    if msm_pairs(n, 64) >= 512:
+        # large groups: the run in [48, 64] with the fewest lane steps over
+        # three resident workgroups per CU (256 CUs), as coa_msm_run picks
+        best, best_cost = 64, None
+        for r in range(64, 47, -1):
+            cost = -(-msm_pairs(n, r) // (3 * 256)) * (r + 6)
+            if best_cost is None or cost < best_cost:
+                best, best_cost = r, cost
+        return best
+    if msm_pairs(n, 32) >= 512:
+        return 32
     return 16
 
 

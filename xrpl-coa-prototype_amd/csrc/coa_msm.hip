@@ -34,6 +34,7 @@
 //                 identity test, encoding flag -> verdict
 #include "coa_msm.h"
 
+#include <atomic>
 #include <cstdlib>
 
 #include "coa_fe.h"
@@ -770,18 +771,48 @@ static size_t bucket_pairs(size_t n, uint32_t run) {
   return nrc * WR + (nc - nrc) * WA;
 }
 
+static uint32_t device_cus() {
+  static std::atomic<uint32_t> cached{0};
+  if (const uint32_t c = cached.load(std::memory_order_relaxed)) return c;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  cached.store((uint32_t)cus, std::memory_order_relaxed);
+  return (uint32_t)cus;
+}
+
 uint32_t coa_msm_run(size_t n) {
   const char* e = getenv("COA_MSM_RUN");
   if (e) {
     const int r = atoi(e);
-    if (r >= 1 && r <= MAXRUN && (r & (r - 1)) == 0) return (uint32_t)r;
+    if (r >= 1 && r <= MAXRUN) return (uint32_t)r;
   }
   if (2 * n + 1 <= 256 * 16) {
     uint32_t run = 4;
     while (256 * run < 2 * n + 1) run <<= 1;
     return run;
   }
-  for (uint32_t run = MAXRUN; run > 16; run >>= 1)
+  if (bucket_pairs(n, MAXRUN) >= 512) {
+    // Large groups: the run in [3/4 MAXRUN, MAXRUN] with the fewest lane
+    // steps, rounds x (run + 6), rounds = pairs over the workgroups resident
+    // at once (three per CU): the workgroups now take equal time, so a last
+    // round barely started costs nearly a whole one.  2^21 signatures: run
+    // 59, 6,130 pairs in 7.98 rounds of 768, against run 64's 5,661 in 7.37
+    // (k_msm_bucket 3.26 against 3.38 ms, the call 8.08 against 8.17 ms).
+    const size_t slots = 3 * (size_t)device_cus();
+    uint32_t best = MAXRUN;
+    size_t best_cost = ~(size_t)0;
+    for (uint32_t run = MAXRUN; run >= MAXRUN * 3 / 4; run--) {
+      const size_t cost = (bucket_pairs(n, run) + slots - 1) / slots * (run + 6);
+      if (cost < best_cost) {
+        best_cost = cost;
+        best = run;
+      }
+    }
+    return best;
+  }
+  for (uint32_t run = MAXRUN / 2; run > 16; run >>= 1)
     if (bucket_pairs(n, run) >= 512) return run;
   return 16;
 }
