@@ -270,7 +270,20 @@ struct Lane {
     completer = std::thread([this] { answer(); });
   }
 
-  Shard& my_shard() { return shards[thread_ordinal() % kShards]; }
+  // The calling thread's shard, locked into `sl`; a shard whose window already
+  // holds max_batch items sends the request on to the next one (the
+  // collector takes whole shards, so one busy producer thread would otherwise
+  // build a window of any size behind a backlog: 254,184 items of streamed
+  // certificates, 920 worker batches at 4,000 batches/s).  The last shard
+  // tried takes the overflow.
+  Shard& intake(std::unique_lock<std::mutex>& sl) {
+    const size_t home = thread_ordinal() % kShards;
+    for (size_t k = 0;; k++) {
+      Shard& sh = shards[(home + k) % kShards];
+      sl = std::unique_lock<std::mutex>(sh.mu);
+      if (sh.items < max_batch || k + 1 == kShards) return sh;
+    }
+  }
 
   // `items` more items were reported by a shard (its lock released).  Wakes
   // the collector only on the two edges it waits for: the first pending item
@@ -577,11 +590,11 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
 // The submissions: the request goes into the calling thread's shard of the
 // kind's lane under that shard's lock; then the lane's pending count (and, on
 // an edge, its collector) learns of it.
-#define COA_Q_INTAKE(q, kind)                  \
-  Lane* ln = &(q)->lane_of(kind);              \
-  Shard& sh = ln->my_shard();                  \
-  std::unique_lock<std::mutex> sl(sh.mu);      \
-  if (ln->stop.load()) return COA_EINVAL;      \
+#define COA_Q_INTAKE(q, kind)              \
+  Lane* ln = &(q)->lane_of(kind);          \
+  std::unique_lock<std::mutex> sl;         \
+  Shard& sh = ln->intake(sl);              \
+  if (ln->stop.load()) return COA_EINVAL;  \
   Window& w = *sh.w;
 
 
@@ -648,23 +661,11 @@ int coa_queue_submit_certificate(coa_queue* q, const uint8_t* header_data, size_
 
 int coa_queue_submit_digest(coa_queue* q, const uint8_t* data, size_t len, coa_verdict_cb cb, void* user) {
   if (!q || (len && !data) || !cb) return COA_EINVAL;
-  // A shard's window holds at most the lane's max_batch digests (the
-  // collector takes whole shards): a producer whose shard is full moves on to
-  // the next one, so one busy producer thread cannot build a window of
-  // hundreds of batches behind a backlog (the last shard takes the overflow).
-  Lane* ln = &q->lane_of(K_DIGEST);
-  const size_t home = thread_ordinal() % kShards;
-  for (size_t k = 0;; k++) {
-    Shard& sh = ln->shards[(home + k) % kShards];
-    std::unique_lock<std::mutex> sl(sh.mu);
-    if (ln->stop.load()) return COA_EINVAL;
-    if (sh.items >= ln->max_batch && k + 1 < kShards) continue;
-    Window& w = *sh.w;
-    if (len) w.d_data.insert(w.d_data.end(), data, data + len);
-    w.d_offs.push_back(w.d_data.size());
-    submitted(ln, sh, sl, K_DIGEST, (uint32_t)w.nd++, 1, cb, user, 1);
-    return COA_OK;
-  }
+  COA_Q_INTAKE(q, K_DIGEST)
+  if (len) w.d_data.insert(w.d_data.end(), data, data + len);
+  w.d_offs.push_back(w.d_data.size());
+  submitted(ln, sh, sl, K_DIGEST, (uint32_t)w.nd++, 1, cb, user, 1);
+  return COA_OK;
 }
 
 int coa_queue_flush(coa_queue* q) {
