@@ -167,8 +167,8 @@ def test_register_while_queue_saturated_with_certificates(engine):
 
 def test_registration_never_holds_a_window_back(engine):
     """coa_committee_register builds the next key-cache
-    generation beside the current one (on a CU-masked stream over half the
-    CUs) and swaps it in; windows in flight keep the generation they pinned.
+    generation beside the current one (on a least-priority stream) and swaps
+    it in; windows in flight keep the generation they pinned.
     A committee-100 re-registration (65 GB of radix-2^20 combs, ~1 s) under
     a steady certificate stream: every verdict exact, and no window takes
     longer than 5 ms from its launch call to its outputs (round 3's write
@@ -219,3 +219,62 @@ def test_registration_never_holds_a_window_back(engine):
     assert len(reg_s) == 2 and len(results) > 1000, (reg_s, len(results))
     assert m["failed_windows"] == 0 and m["certificates"] == len(results)
     assert m["window_us_max"] < 5000, (m["window_us_max"], m["window_max_items"], reg_s)
+
+
+def test_failed_windows_retried_while_registering(engine, monkeypatch):
+    """a window whose launch fails is re-run on the recovery
+    context by the completer while coa_committee_register runs.  With round
+    3's key-cache gate that could deadlock (the retry waiting for readers only
+    the completer could release); with generation pins the retry takes the
+    current generation and nothing waits.  Every 3rd window fails
+    (COA_QUEUE_FAULT, read at queue creation) while a registrar alternates
+    clear / register; every verdict exact, every failed window recovered."""
+    import certificates as C
+
+    monkeypatch.setenv("COA_QUEUE_FAULT", "3")
+    committee, batch = C.synth_certificates(48, committee_size=12, n_payload=3, seed=37)
+    batch.vote_sigs[int(batch.offsets[4]) + 2, 40] ^= 1   # certificate 4: bad vote
+    want = {4: engine.CERT_BAD_VOTES}
+    committee.register()
+    stop = threading.Event()
+    regs = [0]
+
+    def registrar():
+        while not stop.is_set():
+            engine.committee_register(np.zeros((0, 32), np.uint8))
+            committee.register()
+            regs[0] += 1
+
+    results = []
+    lock = threading.Lock()
+    with engine.AggregationQueue(max_batch=256, max_delay_us=200) as q:
+        def producer(t):
+            out = []
+            for rnd in range(5):
+                for c in range(t, len(batch), 2):
+                    lo, hi = int(batch.offsets[c]), int(batch.offsets[c + 1])
+                    votes = [(engine.PublicKey(bytes(batch.vote_pks[j])),
+                              engine.Signature.from_bytes(bytes(batch.vote_sigs[j]))) for j in range(lo, hi)]
+                    out.append((c, q.submit_certificate(batch.header_inputs[c], bytes(batch.ids[c]),
+                                                        bytes(batch.authors[c]), bytes(batch.header_sigs[c]),
+                                                        batch.round, votes)))
+            with lock:
+                results.extend(out)
+
+        reg = threading.Thread(target=registrar)
+        reg.start()
+        th = [threading.Thread(target=producer, args=(t,)) for t in range(2)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=180)
+        q.flush()
+        stop.set()
+        reg.join(timeout=180)
+        assert not reg.is_alive() and not any(x.is_alive() for x in th)
+        for c, f in results:
+            assert f.result(timeout=120) == want.get(c, 0), c
+        m = q.metrics()
+    committee.register()
+    assert regs[0] >= 1 and m["certificates"] == len(results)
+    assert m["retried_windows"] >= 1 and m["recovered_windows"] == m["retried_windows"] and m["failed_windows"] == 0, m
