@@ -7,7 +7,10 @@ one JSON line: the registration windows (start/end, s from the stream's
 start), the slowest requests (arrival, latency) and the latency percentiles
 inside and outside the registrations.
 
-usage: python tools/register_probe.py [rate_per_s] [seconds] [registrations]"""
+usage: python tools/register_probe.py [rate_per_s] [seconds] [registrations] [reopen]
+(reopen = 1: shut the engine down and re-open it with eight contexts, then
+with one, and register a committee of 12 first -- the order of
+tests/test_gpu_recovery.py run on its own)"""
 import json
 import os
 import sys
@@ -33,6 +36,15 @@ def main():
     import coa_crypto
 
     coa_crypto.init(0)
+    if len(sys.argv) > 4 and sys.argv[4] == "1":
+        coa_crypto.shutdown()
+        coa_crypto.init_devices([0] * 8)
+        coa_crypto.shutdown()
+        coa_crypto.init(0)
+        small, _ = C.synth_certificates(4, committee_size=12, n_payload=3, seed=31)
+        for _ in range(3):
+            coa_crypto.committee_register(np.zeros((0, 32), np.uint8))
+            small.register()
     committee, certs = C.synth_certificates(100, committee_size=100, n_payload=32, seed=41)
     committee.register()
     n = int(rate * seconds)
