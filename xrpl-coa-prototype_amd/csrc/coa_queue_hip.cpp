@@ -215,9 +215,17 @@ class HipBackend : public coa_q::Backend {
     if (!ready()) return;
     for (Slot& sl : slots_) {
       const size_t pre_din = lane_ == coa_q::LANE_DIGEST ? (32u << 20) : (4u << 20);
+      // the verify lane's workspace for the usual windows (a committee-100
+      // round's: up to ~16K signatures, 256 certificates of 67 votes): each
+      // regrowth is a hipMalloc on the launch path (the round mix showed 6-9
+      // per queue, with windows held 3-12 ms)
+      const size_t pre_ws = lane_ == coa_q::LANE_DIGEST
+                                ? 256
+                                : std::max(coa_verify_workspace_bytes(16384),
+                                           coa_certificate_workspace_bytes(256, 256 * 67)) + 256;
       if (hipSetDevice(sl.dev) != hipSuccess || grow_dev(sl.din, sl.cap_din, pre_din, sl.grave) != hipSuccess ||
           grow_dev(sl.dout, sl.cap_dout, 256u << 10, sl.grave) != hipSuccess ||
-          grow_dev(sl.ws, sl.cap_ws, 256, sl.grave) != hipSuccess)
+          grow_dev(sl.ws, sl.cap_ws, pre_ws, sl.grave) != hipSuccess)
         continue;  // the first launch regrows and reports any failure
       (void)hipMemcpyAsync(sl.din, sl.hin, 4096, hipMemcpyHostToDevice, sl.s);
       (void)hipMemsetAsync(sl.dout, 0, 4096, sl.s);
