@@ -384,7 +384,29 @@ typedef struct {
   double slot_wait_us_max;
   uint64_t staging_grows;     /* windows that had to enlarge a slot's staging or workspace (warm-up not counted) */
   uint32_t slots_verify, slots_digest; /* device slots of each lane, over all devices */
+  /* Two-step answers: certificates the fused kernel could not decide alone
+   * (a key outside the registered committee, an inconclusive vote) and bare
+   * vote batches go to the lane's resolver thread, which decides them exactly
+   * (coa_certificate_verify_many's semantics); the rest of their window is
+   * answered at once.  So one open certificate never holds back the requests
+   * it shares a window with, nor the windows behind it. */
+  uint64_t deferred_requests; /* requests answered by the resolver */
+  uint64_t resolver_passes;   /* resolver passes (each decides every open request queued by then) */
+  double resolve_us_max;      /* the longest resolver pass */
+  /* Where the time goes, summed over every window (microseconds, COA_QSTAGE_*
+   * indices; divide by `windows` for a mean per window). */
+  double stage_us[12];
 } coa_queue_metrics_t;
+#define COA_QSTAGE_INTAKE 0      /* producers: shard lock + copy of the request into the shard */
+#define COA_QSTAGE_GATHER 1      /* collector: taking the shards' windows */
+#define COA_QSTAGE_SLOT_WAIT 2   /* launch: waiting for a free device slot */
+#define COA_QSTAGE_PACK 3        /* launch: parts -> page-locked staging */
+#define COA_QSTAGE_ENQUEUE 4     /* launch: H2D copy, kernels and D2H copy enqueued */
+#define COA_QSTAGE_DEVICE_WAIT 5 /* completer: blocked on the window's event */
+#define COA_QSTAGE_SCATTER 6     /* completer: outputs -> the parts' verdicts */
+#define COA_QSTAGE_CALLBACKS 7   /* completer (and helpers): the callbacks */
+#define COA_QSTAGE_RESOLVE 8     /* resolver: exact decision of the deferred requests */
+#define COA_QSTAGES 9
 #define COA_QUEUE_KIND_SIGNATURES 1u
 #define COA_QUEUE_KIND_BATCHES 2u
 #define COA_QUEUE_KIND_CERTIFICATES 4u

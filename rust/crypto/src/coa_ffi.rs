@@ -63,6 +63,12 @@ pub struct CoaQueueMetrics {
     pub staging_grows: u64,
     pub slots_verify: u32,
     pub slots_digest: u32,
+    pub deferred_requests: u64,
+    pub resolver_passes: u64,
+    pub resolve_us_max: f64,
+    /// COA_QSTAGE_* (intake, gather, slot_wait, pack, enqueue, device_wait,
+    /// scatter, callbacks, resolve), microseconds summed over windows
+    pub stage_us: [f64; 12],
 }
 
 /// void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n)

@@ -9,15 +9,26 @@
 //! every message the receiver delivers is submitted at once to the
 //! `VerifyService` (the engine's aggregation queue, which coalesces the
 //! requests of the window into a few launches), and each message is passed
-//! on to `Core` as soon as its verdict is in AND every earlier message from
-//! the same authority has been passed on: per-author arrival order, the only
-//! order the reference's network delivers anyway (one connection per peer;
-//! messages of different peers interleave arbitrarily in `Core`'s channel).
-//! A slow request -- a certificate with a key outside the registered
-//! committee, or one the exact random-linear-combination check re-decides
-//! (0.35-1.4 ms) -- therefore holds back only its own author's later
-//! messages, not every message behind it (bench.py
-//! secondary.queue_round_mix.adversarial measures both orderings).
+//! on to `Core` as soon as its verdict is in AND every earlier message with
+//! the same CLAIMED author has been passed on (the message's own author
+//! field, read before it is verified; for a certificate the header's author).
+//! That is neither the connection order nor the round-3 stage's global FIFO:
+//! a certificate the `Helper` sends in reply to a `CertificatesRequest`
+//! arrives over the replying peer's connection yet is ordered behind its
+//! header author's messages, and a message that lies about its author can
+//! only hold back (never reorder or change the verdict of) that author's
+//! later messages, by at most its own verification time.  `Core` does not
+//! depend on any order across authors or connections: the reference's
+//! network interleaves peers arbitrarily on `Core`'s one channel, the
+//! `Helper`'s replies come over other connections, and `Core` waits for
+//! missing parents through its synchronizer whatever the arrival order
+//! (primary/src/core.rs:276-303, synchronizer.rs).  A slow request -- a
+//! certificate with a key outside the registered committee, or one the
+//! exact random-linear-combination check re-decides (0.35-1.4 ms) --
+//! therefore holds back only its claimed author's later messages, not every
+//! message behind it (bench.py secondary.queue_round_mix.adversarial
+//! measures both orderings; tests/test_pre_verify_host.py covers forwarded
+//! certificates interleaved with the forwarding peer's headers).
 //!
 //! `Core` is not changed.  Its verify calls find the verdicts this stage
 //! computed in `crypto::verified`, keyed by every byte the verdict depends on
@@ -50,8 +61,8 @@ const MAX_IN_FLIGHT: usize = 16_384;
 
 pub struct PreVerifier;
 
-/// The authority whose connection delivered the message (the order this
-/// stage keeps).
+/// The message's claimed author (the order this stage keeps; unauthenticated
+/// until the message is verified -- see the module doc).
 fn author_of(message: &PrimaryMessage) -> PublicKey {
     match message {
         PrimaryMessage::Header(header) => header.author,

@@ -15,7 +15,7 @@
 // ~1,000 batches/s per worker) the queue's windows carry the batches of the
 // previous launch's ~14 ms, so one launch covers many batches and the rate
 // is sustained with ~15-30 ms of added latency per batch (bench.py
-// secondary.c4_paced measures it).
+// secondary.c4_stream measures it).
 use crate::worker::SerializedBatchDigestMessage;
 use config::WorkerId;
 use futures::stream::{FuturesOrdered, StreamExt as _};

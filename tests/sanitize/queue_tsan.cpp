@@ -30,7 +30,7 @@
 // outputs, COA_EHIP), as a HIP error would; the queue must then re-run it
 // through retry(), which succeeds -- unless argv[4] = 1, when every retry
 // fails too and the callbacks must get the engine error.
-static std::atomic<long> g_engine_calls{0}, g_injected{0};
+static std::atomic<long> g_engine_calls{0}, g_injected{0}, g_resolver_passes{0}, g_resolved{0};
 static unsigned long g_fault_every = 0;
 static bool g_fault_all = false;
 static uint8_t v_single(const uint8_t* msg, const uint8_t* sig) { return (uint8_t)((msg[0] ^ sig[0]) & 1u); }
@@ -45,8 +45,15 @@ void run_launch(coa_q::Launch& L) {
   for (coa_q::Window* wp : L.parts) {
     coa_q::Window& w = *wp;
     for (size_t i = 0; i < w.nv; i++) w.v_out[i] = v_single(&w.v_msgs[i * 32], &w.v_sigs[i * 64]);
-    for (size_t g = 0; g < w.ng; g++) w.g_out[g] = v_group(&w.g_msgs[g * 32], w.g_offs[g + 1] - w.g_offs[g]);
-    for (size_t c = 0; c < w.nc; c++) w.c_out[c] = v_cert(&w.c_ids[c * 32], w.c_voff[c + 1] - w.c_voff[c]);
+    // as the HIP backend does: bare vote batches, and the certificates the
+    // "kernel" cannot decide alone (here: id[3] odd), are left to resolve()
+    w.g_defer = w.ng > 0;
+    for (size_t c = 0; c < w.nc; c++) {
+      if (w.c_ids[c * 32 + 3] & 1u)
+        w.c_defer.push_back((uint32_t)c);
+      else
+        w.c_out[c] = v_cert(&w.c_ids[c * 32], w.c_voff[c + 1] - w.c_voff[c]);
+    }
     for (size_t i = 0; i < w.nd; i++)
       for (int j = 0; j < 32; j++)
         w.d_out[i * 32 + j] = v_digest(w.d_data.data() + w.d_offs[i], w.d_offs[i + 1] - w.d_offs[i], j);
@@ -91,6 +98,22 @@ class StubBackend : public coa_q::Backend {
       return;
     }
     run_launch(L);
+  }
+  int resolve(const std::vector<coa_q::Window*>& ws) override {
+    g_resolver_passes++;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));  // slower than a window: the rest must not wait
+    for (coa_q::Window* w : ws) {
+      for (uint32_t c : w->c_defer) {
+        w->c_out[c] = v_cert(&w->c_ids[c * 32], w->c_voff[c + 1] - w->c_voff[c]);
+        g_resolved++;
+      }
+      if (w->g_defer)
+        for (size_t g = 0; g < w->ng; g++) {
+          w->g_out[g] = v_group(&w->g_msgs[g * 32], w->g_offs[g + 1] - w->g_offs[g]);
+          g_resolved++;
+        }
+    }
+    return COA_OK;
   }
 
  private:
@@ -203,18 +226,25 @@ int main(int argc, char** argv) {
   coa_queue_destroy(q);
   const long total = (long)producers * per;
   std::printf("queue tsan: %ld/%ld answered, %ld wrong, %llu launches, %ld windows completed, max in flight %llu, "
-              "wait p50 %.0f us p99 %.0f us, injected %ld, retried %llu, recovered %llu, failed %llu, engine errors %ld\n",
+              "wait p50 %.0f us p99 %.0f us, injected %ld, retried %llu, recovered %llu, failed %llu, engine errors %ld, "
+              "deferred %llu in %llu passes\n",
               done, total, bad, (unsigned long long)launches, g_engine_calls.load(),
               (unsigned long long)m.max_in_flight, m.wait_us_p50, m.wait_us_p99, g_injected.load(),
               (unsigned long long)m.retried_windows, (unsigned long long)m.recovered_windows,
-              (unsigned long long)m.failed_windows, g_engine_errors.load());
+              (unsigned long long)m.failed_windows, g_engine_errors.load(), (unsigned long long)m.deferred_requests,
+              (unsigned long long)m.resolver_passes);
   // every injected failure was retried; retries succeed unless told not to
   const bool recovery_ok =
       m.retried_windows == (uint64_t)g_injected.load() &&
       (g_fault_all ? (m.recovered_windows == 0 && m.failed_windows == m.retried_windows &&
                       (g_injected.load() == 0 || g_engine_errors.load() > 0))
                    : (m.recovered_windows == m.retried_windows && m.failed_windows == 0 && g_engine_errors.load() == 0));
+  // every deferred request was answered by a resolver pass (none when every
+  // window failed), and the passes the queue counted are the backend's
+  const bool defer_ok = m.deferred_requests == (uint64_t)g_resolved.load() &&
+                        m.resolver_passes == (uint64_t)g_resolver_passes.load() &&
+                        m.deferred_requests > 0;
   const bool metrics_ok = m.requests == (uint64_t)total && m.batches + m.certificates + m.digests <= (uint64_t)total &&
-                          m.windows == launches && recovery_ok;
+                          m.windows == launches && recovery_ok && defer_ok;
   return (done == total && bad == 0 && items + groups + digests == (uint64_t)total && metrics_ok) ? 0 : 1;
 }

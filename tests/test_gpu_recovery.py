@@ -13,9 +13,12 @@ registration under load.
   call takes an idle context (no longer always the first), every verdict
   equals the golden expectation.
 * coa_committee_register while the aggregation queue is saturated with
-  certificate windows: registration waits for in-flight windows
-  and holds new ones back, so every certificate verdict stays exact whether
-  the committee is registered, re-registered or cleared meanwhile."""
+  certificate windows: registration builds the next key-cache generation
+  beside the current one and swaps it in, while every window keeps the
+  generation it pinned at launch (coa_keycache_pin) -- no gate, so no window
+  is held back (test_registration_never_holds_a_window_back: none above
+  5 ms) and every certificate verdict stays exact whether the committee is
+  registered, re-registered or cleared meanwhile."""
 import os
 import threading
 

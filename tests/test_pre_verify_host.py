@@ -210,3 +210,38 @@ def test_release_order_per_author_bounds_head_of_line():
     authors = ["a", "b", "c", "a"]
     assert sanitize.release_times(arrival, done, authors, per_author=True) == [5.0, 0.2, 0.3, 5.5]
     assert sanitize.release_times(arrival, done, authors, per_author=False) == [5.0, 5.0, 5.0, 5.5]
+
+
+def test_forwarded_certificates_interleaved_with_forwarder_headers():
+    """the stage orders by CLAIMED author (sanitize.message_author,
+    rust/primary/src/pre_verify.rs author_of), not by connection.  Peer B's
+    connection delivers B's own headers interleaved with certificates of
+    authors A and C that B's Helper forwards (replies to a
+    CertificatesRequest, primary/src/helper.rs).  A forwarded certificate
+    whose exact re-decision is slow holds back only later messages claiming
+    ITS author -- never B's headers behind it on the same connection -- and
+    every message is released at its own verdict time or later, in its
+    claimed author's arrival order."""
+    A, B, Cc = (PublicKey(bytes([k]) * 32) for k in (1, 2, 3))
+    hdr = lambda a: C.Header(author=a, round_=3)  # noqa: E731
+    cert = lambda a: C.Certificate(hdr(a), [])  # noqa: E731
+    # one connection (B's), in arrival order: (message, verify time in s)
+    stream = [(hdr(B), 0.05), (cert(A), 1.40), (hdr(B), 0.05), (cert(Cc), 0.05),
+              (hdr(B), 0.05), (cert(A), 0.05), (hdr(B), 0.05)]
+    claimed = [sanitize.message_author(m) for m, _ in stream]
+    assert claimed == [B, A, B, Cc, B, A, B]  # a certificate's header author, whoever forwards it
+    arrival = [0.01 * i for i in range(len(stream))]
+    done = [t + v for t, (_, v) in zip(arrival, stream)]
+    rel = sanitize.release_times(arrival, done, claimed, per_author=True)
+    for i, a in enumerate(claimed):
+        if a == B:  # B's headers never wait behind the slow forwarded certificate
+            assert rel[i] == pytest.approx(done[i])
+    assert rel[1] == pytest.approx(done[1]) and rel[5] == pytest.approx(rel[1])  # A's order kept
+    assert rel[3] == pytest.approx(done[3])  # C's certificate is independent of A's
+    for a in (A, B, Cc):
+        idx = [i for i, x in enumerate(claimed) if x == a]
+        assert all(rel[i] >= done[i] for i in idx)
+        assert all(rel[i] <= rel[j] for i, j in zip(idx, idx[1:]))
+    # the round-3 global FIFO would hold B's later headers behind A's certificate
+    fifo = sanitize.release_times(arrival, done, claimed, per_author=False)
+    assert fifo[2] == pytest.approx(done[1]) and fifo[2] > rel[2]

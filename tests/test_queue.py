@@ -211,3 +211,62 @@ def test_queue_idle_launch_gpu(engine, monkeypatch, mode):
         m = q.metrics()
     assert el < 2.0, el  # the deadline policy would take 24 x 2 s
     assert m["windows"] == len(vecs)
+
+
+@pytest.mark.gpu
+def test_open_certificate_does_not_hold_its_window_gpu(engine):
+    """A window holding one certificate with a vote key outside the registered
+    committee (validly signed: the fused kernel cannot decide it, the exact
+    path says Ok) answers every other request first: the open certificate
+    goes to the lane's resolver (coa_certificate_resolve_raw), and every
+    verdict still equals the C oracle's (oracle/coa_oracle.c, dalek's checks
+    run per certificate -- primary/src/messages.rs:189-215)."""
+    import os
+
+    import certificates as C
+    import coa_oracle as co
+    import workloads
+
+    committee, b = C.synth_certificates(16, committee_size=10, n_payload=2, seed=9)
+    committee.register()
+    lo = int(b.offsets[6])
+    p_out, s_out = engine.sign_many(workloads.key_seeds(1, 77_777), b.cert_digests[6:7])
+    b.vote_pks[lo], b.vote_sigs[lo] = p_out[0], s_out[0]   # certificate 6: open, Ok
+    b.vote_sigs[int(b.offsets[11]) + 2, 45] ^= 1             # certificate 11: bad vote (decided by the kernel)
+    zs = np.random.default_rng(3).integers(0, 256, (int(b.offsets[-1]), 16), dtype=np.uint8)
+    exp = co.certificate_verify_many(list(b.header_inputs), b.ids, b.authors, b.header_sigs, b.round, b.vote_pks,
+                                     b.vote_sigs, b.offsets, zs, min(8, os.cpu_count() or 1))
+    n = 64
+    seeds, msgs = workloads.key_seeds(n, 50_000), workloads.messages(n, 50_000)
+    pks, sigs = engine.sign_many(seeds, msgs)
+    sigs[::9, 40] ^= 1
+    order, lock = [], threading.Lock()
+
+    def done(tag):
+        def cb(_f):
+            with lock:
+                order.append(tag)
+        return cb
+
+    with engine.AggregationQueue(max_batch=1 << 20, max_delay_us=2_000_000) as q:
+        futs = []
+        for i in range(len(b)):
+            votes = [(engine.PublicKey(bytes(b.vote_pks[j])), engine.Signature.from_bytes(bytes(b.vote_sigs[j])))
+                     for j in range(int(b.offsets[i]), int(b.offsets[i + 1]))]
+            f = q.submit_certificate(b.header_inputs[i], bytes(b.ids[i]), bytes(b.authors[i]),
+                                     bytes(b.header_sigs[i]), b.round, votes)
+            f.add_done_callback(done(("cert", i)))
+            futs.append((f, int(exp[i])))
+        for i in range(n):
+            f = q.submit_verify(bytes(msgs[i]), bytes(pks[i]), engine.Signature.from_bytes(bytes(sigs[i])))
+            f.add_done_callback(done(("sig", i)))
+            futs.append((f, i % 9 != 0))
+        q.flush()
+        for f, want in futs:
+            assert f.result(timeout=60) == want
+        m = q.metrics()
+    assert exp[6] == 0 and exp[11] == engine.CERT_BAD_VOTES
+    assert m["windows"] == 1 and m["deferred_requests"] == 1 and m["resolver_passes"] == 1
+    # the open certificate is the last answer of its window
+    assert order[-1] == ("cert", 6), order[-5:]
+    assert len(order) == len(futs)

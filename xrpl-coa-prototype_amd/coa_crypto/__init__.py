@@ -61,7 +61,19 @@ class QueueMetrics(ctypes.Structure):
                [("window_us_max", ctypes.c_double), ("window_max_items", ctypes.c_uint64),
                 ("window_max_kinds", ctypes.c_uint32), ("stream_kind", ctypes.c_int32),
                 ("slot_wait_us_max", ctypes.c_double), ("staging_grows", ctypes.c_uint64),
-                ("slots_verify", ctypes.c_uint32), ("slots_digest", ctypes.c_uint32)]
+                ("slots_verify", ctypes.c_uint32), ("slots_digest", ctypes.c_uint32),
+                ("deferred_requests", ctypes.c_uint64), ("resolver_passes", ctypes.c_uint64),
+                ("resolve_us_max", ctypes.c_double), ("stage_us", ctypes.c_double * 12)]
+
+    # COA_QSTAGE_* indices of stage_us
+    STAGES = ("intake", "gather", "slot_wait", "pack", "enqueue", "device_wait", "scatter", "callbacks", "resolve")
+
+
+def metrics_dict(m):
+    """A QueueMetrics as a dict; stage_us becomes {stage name: microseconds}."""
+    d = {name: getattr(m, name) for name, _ in QueueMetrics._fields_ if name != "stage_us"}
+    d["stage_us"] = {k: m.stage_us[i] for i, k in enumerate(QueueMetrics.STAGES)}
+    return d
 
 
 # void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n)
@@ -786,7 +798,7 @@ class AggregationQueue:
         times in microseconds."""
         m = QueueMetrics()
         _check(lib().coa_queue_metrics(self._q, ctypes.byref(m)))
-        return {name: getattr(m, name) for name, _ in QueueMetrics._fields_}
+        return metrics_dict(m)
 
     def close(self):
         if self._q:

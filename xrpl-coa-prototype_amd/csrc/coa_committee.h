@@ -97,6 +97,17 @@ extern "C" void* coa_keycache_pin(int device);  // opaque handle (null: device n
 extern "C" void coa_keycache_unpin(void* pin);  // any thread; null is a no-op
 extern "C" void coa_keycache_use(void* pin);    // this thread's launches read `pin` (null: the current one)
 
+// The exact decision of certificates the fused kernel left open (raw status
+// words with COA_CST_UNCACHED or COA_CST_VOTES_INCONCLUSIVE; the others pass
+// through): host arrays as coa_certificate_verify_many takes them, minus the
+// header bytes.  `raw` is updated in place; status_out gets the COA_CERT_*
+// bits.  The aggregation queue's resolver calls it off the completion thread
+// (coa_queue.cpp), so an open certificate never holds its window back.
+extern "C" int coa_certificate_resolve_raw(const uint8_t* ids, const uint8_t* origins, const uint8_t* header_sigs,
+                                           const uint64_t* rounds, const uint8_t* vote_pks, const uint8_t* vote_sigs,
+                                           const uint64_t* vote_offsets, size_t n, uint32_t* raw,
+                                           uint8_t* status_out);
+
 // Host copies spread over the runtime's copy threads (COA_PACK_THREADS):
 // the aggregation queue packs large windows into page-locked staging with
 // it.  Returns when every segment is copied.

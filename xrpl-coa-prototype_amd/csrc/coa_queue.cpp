@@ -117,6 +117,18 @@ struct Flight {
   int64_t t_launch = 0;  // ns, when the collector handed the window to the backend
 };
 
+// A part's requests the backend left open (Window::c_defer, g_defer), with
+// the part's window (moved out of the flight, not recycled): the resolver
+// thread decides them and answers their callbacks.
+struct Deferred {
+  std::unique_ptr<Window> w;
+  std::vector<Req> reqs;
+};
+
+inline bool is_deferred(const Req& r, const Window& w) {
+  return (r.kind == K_CERT && w.is_deferred_cert(r.idx)) || (r.kind == K_BATCH && w.g_defer);
+}
+
 std::atomic<uint64_t> g_queue_ids{1};
 std::atomic<uint32_t> g_thread_ord{0};
 
@@ -230,12 +242,17 @@ struct Lane {
   std::condition_variable cv;         // collector: requests arrived / flush / stop
   std::condition_variable flight_cv;  // completer: a window was launched / stop
   std::condition_variable idle_cv;    // flush: everything answered
+  std::condition_variable resolve_cv; // resolver: open requests deferred / stop
   std::atomic<int64_t> pend{0};  // reported items not yet taken (briefly < 0 while a take races a report)
   std::atomic<bool> stop{false};
   std::chrono::steady_clock::time_point oldest;
   std::deque<Flight> flight;  // launched, not yet answered (launch order)
   size_t busy = 0;            // windows taken by the collector and not yet answered
   bool flush = false, collector_done = false;
+  std::deque<Deferred> open;  // deferred parts waiting for the resolver
+  size_t resolving = 0;       // deferred parts not yet answered (queued or in a pass)
+  bool resolver_stop = false;
+  bool idle() const { return pend.load() <= 0 && busy == 0 && resolving == 0; }
 
   // metrics (under mu, except m_max_pending)
   uint64_t m_requests = 0, m_windows = 0, m_sig = 0, m_batch = 0, m_cert = 0, m_dig = 0;
@@ -249,8 +266,11 @@ struct Lane {
   double m_window_us_max = 0.0, m_slot_wait_us_max = 0.0;
   uint64_t m_window_max_items = 0;
   uint32_t m_window_max_kinds = 0;
+  uint64_t m_deferred = 0, m_passes = 0;
+  double m_resolve_us_max = 0.0;
+  double m_stage_us[COA_QSTAGES] = {};
 
-  std::thread collector, completer;
+  std::thread collector, completer, resolver;
   AnswerPool helpers;  // started lazily by the first large launch
   int n_helpers = kHelpersDefault;
   bool helpers_on = false;
@@ -268,6 +288,7 @@ struct Lane {
   void start() {
     collector = std::thread([this] { collect(); });
     completer = std::thread([this] { answer(); });
+    resolver = std::thread([this] { resolve_loop(); });
   }
 
   // The calling thread's shard, locked into `sl`; a shard whose window already
@@ -337,7 +358,10 @@ struct Lane {
       f.parts.push_back(std::move(p));
     }
     f.L.parts.clear();
-    for (Part& p : f.parts) f.L.parts.push_back(p.w.get());
+    for (Part& p : f.parts) {
+      f.L.parts.push_back(p.w.get());
+      f.L.stage_ns[COA_QSTAGE_INTAKE] += p.w->intake_ns;
+    }
     f.L.tally();
   }
 
@@ -356,11 +380,13 @@ struct Lane {
       busy++;  // before the take: flush must not see pend == 0 and busy == 0 meanwhile
       Flight f;
       l.unlock();
+      const int64_t tg = now_ns();
       gather(f);
+      f.L.stage_ns[COA_QSTAGE_GATHER] += now_ns() - tg;
       l.lock();
       if (f.parts.empty()) {  // every pending item was taken by an earlier window
         busy--;
-        if (busy == 0 && pend.load() <= 0) idle_cv.notify_all();
+        if (idle()) idle_cv.notify_all();
         continue;
       }
       m_max_window = std::max<uint64_t>(m_max_window, f.L.items());
@@ -369,6 +395,7 @@ struct Lane {
       f.L.attempts = 1;
       f.t_launch = now_ns();
       be->launch(f.L);  // stages and enqueues; blocks only while every slot is busy
+      f.L.stage_ns[COA_QSTAGE_SLOT_WAIT] += f.L.slot_wait_ns;
       l.lock();
       m_windows++;
       flight.push_back(std::move(f));
@@ -406,6 +433,18 @@ struct Lane {
       const bool retried = recoverable(f.L.rc);
       if (retried) recover(f.L);
       const int rc = f.L.rc;
+      // requests the backend left open go to the resolver, the rest are
+      // answered now (a failed window leaves nothing open: every request
+      // gets the error)
+      bool any_defer = false;
+      for (Part& p : f.parts) {
+        if (rc != COA_OK) {
+          p.w->c_defer.clear();
+          p.w->g_defer = false;
+        }
+        any_defer = any_defer || p.w->deferred();
+      }
+      const int64_t tcb = now_ns();
       // callbacks, in runs of contiguous requests (helpers join for large
       // launches); wait times from a clock read every 32 requests
       struct Seg {
@@ -430,6 +469,7 @@ struct Lane {
         int64_t tnow = now_ns();
         for (size_t k = g.lo; k < g.hi; k++) {
           const Req& r = g.p->reqs[k];
+          if (any_defer && is_deferred(r, w)) continue;  // the resolver answers it
           if (((k - g.lo) & 31) == 31) tnow = now_ns();
           const double us = (double)(tnow - r.t0) * 1e-3;
           t.wsum += us;
@@ -452,6 +492,7 @@ struct Lane {
       } else {
         for (size_t si = 0; si < segs.size(); si++) answer_seg(si);
       }
+      f.L.stage_ns[COA_QSTAGE_CALLBACKS] += now_ns() - tcb;
       uint64_t hist[HB] = {};
       double wsum = 0.0, wmax = 0.0;
       for (const Tally& t : tallies) {
@@ -459,20 +500,36 @@ struct Lane {
         wsum += t.wsum;
         wmax = std::max(wmax, t.wmax);
       }
-      // recycle each part's window and request vector into its shard
+      // the open requests, with their windows, for the resolver
+      std::vector<Deferred> jobs;
+      size_t ndef = 0;
+      if (any_defer) {
+        for (Part& p : f.parts) {
+          if (!p.w->deferred()) continue;
+          Deferred d;
+          for (const Req& r : p.reqs)
+            if (is_deferred(r, *p.w)) d.reqs.push_back(r);
+          ndef += d.reqs.size();
+          d.w = std::move(p.w);
+          jobs.push_back(std::move(d));
+        }
+      }
+      // recycle each part's window (unless the resolver has it) and request
+      // vector into its shard
       for (Part& p : f.parts) {
-        p.w->reset();
+        if (p.w) p.w->reset();
         p.reqs.clear();
         Shard& sh = shards[p.shard];
         std::lock_guard<std::mutex> g(sh.mu);
-        if (!sh.spare) sh.spare = std::move(p.w);
+        if (!sh.spare && p.w) sh.spare = std::move(p.w);
         if (sh.spare_reqs.capacity() < p.reqs.capacity()) sh.spare_reqs.swap(p.reqs);
       }
       l.lock();
       for (int b = 0; b < HB; b++) m_hist[b] += hist[b];
       m_wait_sum += wsum;
       m_wait_max = std::max(m_wait_max, wmax);
-      m_requests += nreq;
+      m_requests += nreq - ndef;
+      for (int k = 0; k < COA_QSTAGES; k++) m_stage_us[k] += (double)f.L.stage_ns[k] * 1e-3;
       m_sig += f.L.nv;
       m_batch += f.L.ng;
       m_cert += f.L.nc;
@@ -488,9 +545,73 @@ struct Lane {
       }
       m_slot_wait_us_max = std::max(m_slot_wait_us_max, (double)f.L.slot_wait_ns * 1e-3);
       if (rc != COA_OK) m_failed++;
+      if (!jobs.empty()) {
+        resolving += jobs.size();
+        for (Deferred& d : jobs) open.push_back(std::move(d));
+        resolve_cv.notify_one();
+      }
       busy--;
-      if (busy == 0 && pend.load() <= 0) idle_cv.notify_all();
+      if (idle()) idle_cv.notify_all();
       if (idle_launch && busy < idle_launch && pend.load() > 0) cv.notify_one();
+    }
+  }
+
+  // The resolver: takes every deferred part queued so far, has the backend
+  // decide them in one pass (one engine call per kind for all of them), and
+  // answers their callbacks -- off the completion thread, so the windows
+  // behind an open certificate are answered while it is being decided.
+  void resolve_loop() {
+    std::unique_lock<std::mutex> l(mu);
+    for (;;) {
+      resolve_cv.wait(l, [&] { return !open.empty() || resolver_stop; });
+      if (open.empty()) return;
+      std::vector<Deferred> jobs;
+      while (!open.empty()) {
+        jobs.push_back(std::move(open.front()));
+        open.pop_front();
+      }
+      l.unlock();
+      const int64_t t0 = now_ns();
+      std::vector<Window*> ws;
+      for (Deferred& d : jobs) ws.push_back(d.w.get());
+      const int rc = be->resolve(ws);
+      if (rc != COA_OK) {
+        for (Window* w : ws) {  // "failed" outputs with the engine error
+          for (uint32_t c : w->c_defer) w->c_out[c] = 7;
+          if (w->g_defer) w->g_out.assign(w->ng, 1);
+        }
+      }
+      const int64_t t1 = now_ns();
+      uint64_t hist[HB] = {};
+      double wsum = 0.0, wmax = 0.0;
+      size_t n = 0;
+      for (const Deferred& d : jobs) {
+        const Window& w = *d.w;
+        for (const Req& r : d.reqs) {
+          const double us = (double)(now_ns() - r.t0) * 1e-3;
+          wsum += us;
+          wmax = std::max(wmax, us);
+          hist[wait_bucket(us)]++;
+          if (r.kind == K_CERT)
+            r.cb(r.user, rc, w.c_out.data() + r.idx, 1);
+          else
+            r.cb(r.user, rc, w.g_out.data() + r.idx, 1);
+          n++;
+        }
+      }
+      const int64_t t2 = now_ns();
+      l.lock();
+      for (int b = 0; b < HB; b++) m_hist[b] += hist[b];
+      m_wait_sum += wsum;
+      m_wait_max = std::max(m_wait_max, wmax);
+      m_requests += n;
+      m_deferred += n;
+      m_passes++;
+      m_resolve_us_max = std::max(m_resolve_us_max, (double)(t1 - t0) * 1e-3);
+      m_stage_us[COA_QSTAGE_RESOLVE] += (double)(t1 - t0) * 1e-3;
+      m_stage_us[COA_QSTAGE_CALLBACKS] += (double)(t2 - t1) * 1e-3;
+      resolving -= jobs.size();
+      if (idle()) idle_cv.notify_all();
     }
   }
 
@@ -502,16 +623,22 @@ struct Lane {
     }
     collector.join();
     completer.join();
+    {
+      std::lock_guard<std::mutex> l(mu);
+      resolver_stop = true;
+      resolve_cv.notify_one();
+    }
+    resolver.join();
   }
 
   int flush_all() {
     std::unique_lock<std::mutex> l(mu);
-    if (pend.load() <= 0 && busy == 0) return COA_OK;
+    if (idle()) return COA_OK;
     if (pend.load() > 0) {
       flush = true;
       cv.notify_one();
     }
-    idle_cv.wait(l, [&] { return pend.load() <= 0 && busy == 0; });
+    idle_cv.wait(l, [&] { return idle(); });
     return COA_OK;
   }
 };
@@ -539,8 +666,9 @@ struct coa_queue {
 
 namespace {
 void submitted(Lane* q, Shard& sh, std::unique_lock<std::mutex>& sl, Kind kind, uint32_t idx, uint32_t n,
-               coa_verdict_cb cb, void* user, size_t items) {
-  sh.reqs.push_back(Req{cb, user, now_ns(), idx, n, kind});
+               coa_verdict_cb cb, void* user, size_t items, int64_t t_in) {
+  sh.reqs.push_back(Req{cb, user, t_in, idx, n, kind});
+  sh.w->intake_ns += now_ns() - t_in;
   sh.items += items;
   size_t delta = 0;
   if (sh.reported == 0 || sh.items - sh.reported >= kReport) {
@@ -581,7 +709,7 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
     if (const char* e = getenv("COA_QUEUE_HELPERS")) L.n_helpers = std::max(0, std::min(15, atoi(e)));
     if (const char* e = getenv("COA_QUEUE_IDLE_LAUNCH")) L.idle_launch = (size_t)std::max(0, std::min(64, atoi(e)));
     L.be.reset(coa_q::make_backend(k));
-    L.be->prepare();
+    L.be->prepare(L.max_batch);
     L.start();
   }
   return q;
@@ -591,6 +719,7 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
 // kind's lane under that shard's lock; then the lane's pending count (and, on
 // an edge, its collector) learns of it.
 #define COA_Q_INTAKE(q, kind)              \
+  const int64_t t_in = now_ns();           \
   Lane* ln = &(q)->lane_of(kind);          \
   std::unique_lock<std::mutex> sl;         \
   Shard& sh = ln->intake(sl);              \
@@ -605,7 +734,7 @@ int coa_queue_submit_verify(coa_queue* q, const uint8_t msg[32], const uint8_t p
   put<32>(w.v_msgs, msg);
   put<32>(w.v_pks, pk);
   put<64>(w.v_sigs, sig);
-  submitted(ln, sh, sl, K_VERIFY, (uint32_t)w.nv++, 1, cb, user, 1);
+  submitted(ln, sh, sl, K_VERIFY, (uint32_t)w.nv++, 1, cb, user, 1, t_in);
   return COA_OK;
 }
 
@@ -618,7 +747,7 @@ int coa_queue_submit_verify_many(coa_queue* q, const uint8_t* msgs, const uint8_
   w.v_sigs.insert(w.v_sigs.end(), sigs, sigs + n * 64);
   const uint32_t idx = (uint32_t)w.nv;
   w.nv += n;
-  submitted(ln, sh, sl, K_VERIFY, idx, (uint32_t)n, cb, user, n);
+  submitted(ln, sh, sl, K_VERIFY, idx, (uint32_t)n, cb, user, n, t_in);
   return COA_OK;
 }
 
@@ -632,7 +761,7 @@ int coa_queue_submit_batch(coa_queue* q, const uint8_t msg[32], const uint8_t* p
     w.g_sigs.insert(w.g_sigs.end(), sigs, sigs + n * 64);
   }
   w.g_offs.push_back(w.g_offs.back() + n);
-  submitted(ln, sh, sl, K_BATCH, (uint32_t)w.ng++, 1, cb, user, n ? n : 1);
+  submitted(ln, sh, sl, K_BATCH, (uint32_t)w.ng++, 1, cb, user, n ? n : 1, t_in);
   return COA_OK;
 }
 
@@ -655,7 +784,7 @@ int coa_queue_submit_certificate(coa_queue* q, const uint8_t* header_data, size_
     w.c_sigs.insert(w.c_sigs.end(), vote_sigs, vote_sigs + n_votes * 64);
   }
   w.c_voff.push_back(w.c_voff.back() + n_votes);
-  submitted(ln, sh, sl, K_CERT, (uint32_t)w.nc++, 1, cb, user, 1 + n_votes);
+  submitted(ln, sh, sl, K_CERT, (uint32_t)w.nc++, 1, cb, user, 1 + n_votes, t_in);
   return COA_OK;
 }
 
@@ -664,7 +793,7 @@ int coa_queue_submit_digest(coa_queue* q, const uint8_t* data, size_t len, coa_v
   COA_Q_INTAKE(q, K_DIGEST)
   if (len) w.d_data.insert(w.d_data.end(), data, data + len);
   w.d_offs.push_back(w.d_data.size());
-  submitted(ln, sh, sl, K_DIGEST, (uint32_t)w.nd++, 1, cb, user, 1);
+  submitted(ln, sh, sl, K_DIGEST, (uint32_t)w.nd++, 1, cb, user, 1, t_in);
   return COA_OK;
 }
 
@@ -739,6 +868,10 @@ int coa_queue_metrics(coa_queue* q, coa_queue_metrics_t* out) {
     out->staging_grows += L.be->grows();
     out->stream_kind = std::max(out->stream_kind, (int32_t)L.be->stream_kind());
     (k == coa_q::LANE_DIGEST ? out->slots_digest : out->slots_verify) = (uint32_t)L.be->slots();
+    out->deferred_requests += L.m_deferred;
+    out->resolver_passes += L.m_passes;
+    out->resolve_us_max = std::max(out->resolve_us_max, L.m_resolve_us_max);
+    for (int s = 0; s < COA_QSTAGES; s++) out->stage_us[s] += L.m_stage_us[s];
   }
   out->wait_us_mean = out->requests ? wsum / (double)out->requests : 0.0;
   out->wait_us_p50 = hist_percentile(hist, 0.50);

@@ -7,6 +7,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/coa_verify.h"
@@ -38,7 +39,17 @@ struct Window {
   std::vector<uint8_t> d_data;
   std::vector<uint64_t> d_offs;  // nd + 1
   std::vector<uint8_t> d_out;    // nd x 32
+  // Left open by Backend::complete (or retry) for the lane's resolver
+  // (Backend::resolve): certificates the fused kernel could not decide alone
+  // (their raw status words kept) and, with g_defer, every bare vote batch.
+  // Their requests are answered after the rest of the window.
+  std::vector<uint32_t> c_raw;    // nc raw status words (COA_CST_*), or empty
+  std::vector<uint32_t> c_defer;  // ascending certificate indices
+  bool g_defer = false;
+  int64_t intake_ns = 0;          // producers' time copying requests in (COA_QSTAGE_INTAKE)
 
+  bool deferred() const { return !c_defer.empty() || (g_defer && ng); }
+  bool is_deferred_cert(uint32_t c) const { return std::binary_search(c_defer.begin(), c_defer.end(), c); }
   size_t items() const { return nv + nd + nc + (c_voff.empty() ? 0 : c_voff.back()) + g_offs.back(); }
   // Outputs sized and set to "failed" (verdict Err, all certificate bits,
   // zero digests) before a launch or a retry.
@@ -47,12 +58,19 @@ struct Window {
     g_out.assign(ng, 1);
     c_out.assign(nc, 7);
     d_out.assign(nd * 32, 0);
+    c_raw.clear();
+    c_defer.clear();
+    g_defer = false;
   }
   // Empty again for the next intake, keeping every vector's capacity (the
   // queue recycles answered windows, so a window fills without reallocating
   // under the intake lock).
   void reset() {
     nv = ng = nc = nd = 0;
+    intake_ns = 0;
+    g_defer = false;
+    c_raw.clear();
+    c_defer.clear();
     for (auto* v : {&v_msgs, &v_pks, &v_sigs, &v_out, &g_msgs, &g_pks, &g_sigs, &g_out, &c_hdata, &c_ids, &c_origins,
                     &c_hsigs, &c_pks, &c_sigs, &c_out, &d_data, &d_out})
       v->clear();
@@ -76,6 +94,9 @@ struct Launch {
   int slot = -1;       // backend slot the launch ran on
   int attempts = 0;    // launches of this window (1 + retries)
   int64_t slot_wait_ns = 0;  // how long launch() waited for a free slot (set by the backend)
+  // time per COA_QSTAGE_* stage; the backend adds PACK, ENQUEUE, DEVICE_WAIT
+  // and SCATTER (retries included), the queue the others
+  int64_t stage_ns[COA_QSTAGES] = {};
   // COA_QUEUE_KIND_* bits of the kinds the launch holds
   uint32_t kinds() const {
     return (nv ? COA_QUEUE_KIND_SIGNATURES : 0u) | (ng ? COA_QUEUE_KIND_BATCHES : 0u) |
@@ -123,9 +144,18 @@ class Backend {
   virtual int slots() const = 0;
   // Number of device contexts retries can go to (at least 1).
   virtual int devices() const = 0;
-  // Sets the slots up (streams, staging) before the first window: called once
-  // at queue creation, so no request pays for it.
-  virtual void prepare() {}
+  // Decides what complete() / retry() left open in the windows `ws`
+  // (Window::c_defer, g_defer), writing their c_out / g_out.  Called by the
+  // lane's resolver thread -- concurrently with launch() and complete() of
+  // later windows, never with itself.  Returns the engine status.
+  virtual int resolve(const std::vector<Window*>& ws) {
+    (void)ws;
+    return COA_OK;
+  }
+  // Sets the slots up (streams, staging sized for windows of up to twice
+  // max_batch items) before the first window: called once at queue creation,
+  // so no request pays for it.
+  virtual void prepare(size_t max_batch) { (void)max_batch; }
   // Staging reallocations so far (each a page-locked or device allocation).
   virtual uint64_t grows() const { return 0; }
   // How the slots' streams were made (COA_QUEUE_STREAM_*).

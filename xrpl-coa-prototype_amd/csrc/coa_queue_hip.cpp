@@ -1,5 +1,5 @@
 // HIP launch backend of the aggregation queue (coa_queue.h), one per lane:
-// device slots (four per opened GPU context and lane by default:
+// device slots (four per opened GPU and lane by default:
 // COA_QUEUE_SLOTS for the verify lane, COA_QUEUE_DIGEST_SLOTS for the digest
 // lane), each with its own stream, event, page-locked staging and device
 // buffers.
@@ -31,16 +31,17 @@
 //                 windows of at most COA_LAT_MAX (2,048) signatures take the
 //                 latency kernel instead (one workgroup per signature)
 //   certificates  coa_certificate_verify_many_device (the fused
-//                 Certificate::verify crypto); the raw status words that need
-//                 the exact random-linear-combination check or carry a key
-//                 outside the registered committee are re-decided in
-//                 complete() through coa_certificate_verify_many, as the
-//                 host-pointer entry point does.  A window with certificates
-//                 holds its device's key-cache read gate from launch to
-//                 completion, so coa_committee_register never rewrites the
-//                 key tables under a running window
+//                 Certificate::verify crypto); the certificates whose raw
+//                 status words need the exact random-linear-combination check
+//                 or carry a key outside the registered committee are left
+//                 open by complete() (Window::c_defer) and decided by
+//                 resolve() on the lane's resolver thread with
+//                 coa_certificate_resolve_raw -- the exact path alone, not a
+//                 second fused launch -- while the rest of the window is
+//                 answered at once.  A window with certificates pins its
+//                 device's key-cache generation from launch to completion
 //   digests       coa_sha512_many_device (worker/src/processor.rs:38)
-//   vote batches  coa_ed25519_verify_batch_groups in complete() (host
+//   vote batches  coa_ed25519_verify_batch_groups in resolve() (host
 //                 pointers; bare batches are rare next to whole certificates)
 //
 // Engine-failure recovery: a failed launch drains its stream (the error code
@@ -71,6 +72,9 @@
 namespace {
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+inline int64_t ns_between(std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+}
 
 struct Grave {  // an outgrown staging buffer (see grow_pinned)
   void* p;
@@ -211,20 +215,32 @@ class HipBackend : public coa_q::Backend {
   // one small copy through each stream, which makes HIP create the stream's
   // hardware queue (a CU-masked stream's first dispatch took ~25-75 ms:
   // round-4 paced runs, one queue per rate, p99 20-75 ms from that alone).
-  void prepare() override {
+  //
+  // The verify lane is sized for the largest window the collector can close:
+  // whole shards are taken until max_batch items are in, and a shard holds up
+  // to max_batch items, so a window holds < 2 x max_batch items.  Certificate
+  // items (a certificate and its votes: 9,920 B per committee-100 certificate
+  // of 68 items) take <= 160 B each in the input block, signatures 128 B.
+  // Sized for half of that (grow_* double it), staging never regrows on the
+  // launch path (round 4's streamed C3 regrew 2-4 times per run, windows of
+  // up to 107 K items, p99 wait 8-12 ms).
+  void prepare(size_t max_batch) override {
     if (!ready()) return;
+    const size_t items = std::max<size_t>(max_batch, 1024);
+    const size_t pre_in = lane_ == coa_q::LANE_DIGEST ? (32u << 20) : items * 160 + (1u << 20);
+    const size_t pre_out = lane_ == coa_q::LANE_DIGEST ? (256u << 10) : items * 4 + (64u << 10);
+    // workspace for the widest window of each kind (each regrowth is a
+    // hipMalloc on the launch path: the round mix showed 6-9 per queue, with
+    // windows held 3-12 ms)
+    const size_t pre_ws = lane_ == coa_q::LANE_DIGEST
+                              ? 256
+                              : std::max(coa_verify_workspace_bytes(items),
+                                         coa_certificate_workspace_bytes(items / 68 + 1, items)) + 256;
     for (Slot& sl : slots_) {
-      const size_t pre_din = lane_ == coa_q::LANE_DIGEST ? (32u << 20) : (4u << 20);
-      // the verify lane's workspace for the usual windows (a committee-100
-      // round's: up to ~16K signatures, 256 certificates of 67 votes): each
-      // regrowth is a hipMalloc on the launch path (the round mix showed 6-9
-      // per queue, with windows held 3-12 ms)
-      const size_t pre_ws = lane_ == coa_q::LANE_DIGEST
-                                ? 256
-                                : std::max(coa_verify_workspace_bytes(16384),
-                                           coa_certificate_workspace_bytes(256, 256 * 67)) + 256;
-      if (hipSetDevice(sl.dev) != hipSuccess || grow_dev(sl.din, sl.cap_din, pre_din, sl.grave) != hipSuccess ||
-          grow_dev(sl.dout, sl.cap_dout, 256u << 10, sl.grave) != hipSuccess ||
+      if (hipSetDevice(sl.dev) != hipSuccess || grow_pinned(sl.hin, sl.cap_hin, pre_in, sl.grave) != hipSuccess ||
+          grow_pinned(sl.hout, sl.cap_hout, pre_out, sl.grave) != hipSuccess ||
+          grow_dev(sl.din, sl.cap_din, pre_in, sl.grave) != hipSuccess ||
+          grow_dev(sl.dout, sl.cap_dout, pre_out, sl.grave) != hipSuccess ||
           grow_dev(sl.ws, sl.cap_ws, pre_ws, sl.grave) != hipSuccess)
         continue;  // the first launch regrows and reports any failure
       (void)hipMemcpyAsync(sl.din, sl.hin, 4096, hipMemcpyHostToDevice, sl.s);
@@ -311,9 +327,15 @@ class HipBackend : public coa_q::Backend {
       return false;
     }
     const int nctx = std::min(n, 64);
-    // device slots per context: windows in flight at once (1..8;
-    // COA_QUEUE_SLOTS for the verify lane, COA_QUEUE_DIGEST_SLOTS for the
-    // digest lane; tools/queue_probe.c measures the choice)
+    for (int i = 0; i < nctx; i++)
+      if (std::find(devs_.begin(), devs_.end(), ids[i]) == devs_.end()) devs_.push_back(ids[i]);
+    // device slots per GPU (not per engine context: eight contexts open on
+    // one GPU made 32 slots per lane there, 64 CU-masked streams and so 64
+    // hardware queues on one device, more than its scheduler maps at once --
+    // the suspected cause of round 4's 84-149 ms window on a re-opened
+    // 8-context engine): windows in flight at once (1..8; COA_QUEUE_SLOTS for
+    // the verify lane, COA_QUEUE_DIGEST_SLOTS for the digest lane;
+    // tools/queue_probe.c measures the choice)
     size_t per = COA_QUEUE_SLOTS_DEFAULT;
     if (const char* e = getenv(lane_ == coa_q::LANE_DIGEST ? "COA_QUEUE_DIGEST_SLOTS" : "COA_QUEUE_SLOTS")) {
       const int v = atoi(e);
@@ -321,23 +343,19 @@ class HipBackend : public coa_q::Backend {
     }
     if (const char* e = getenv("COA_QUEUE_FAULT")) fault_every_ = strtoull(e, nullptr, 10);
     kind_ = stream_kind_env();
-    slots_.resize(per * (size_t)nctx);
-    // page-locked staging sized up front for the usual windows (a reallocation
-    // on the launch path is a hipHostFree/hipHostMalloc pair: milliseconds)
-    const size_t pre_in = lane_ == coa_q::LANE_DIGEST ? (32u << 20) : (4u << 20);  // doubled by grow_pinned
+    slots_.resize(per * devs_.size());
+    // (page-locked staging is sized by prepare(): a reallocation on the
+    // launch path is a hipHostFree/hipHostMalloc pair, milliseconds)
     for (size_t k = 0; k < slots_.size(); k++) {
       Slot& sl = slots_[k];
-      sl.dev = ids[k % (size_t)nctx];
+      sl.dev = devs_[k % devs_.size()];
       sl.kind = kind_;
       sl.lane = lane_;
-      if (make_stream(sl) != COA_OK || grow_pinned(sl.hin, sl.cap_hin, pre_in, sl.grave) != hipSuccess ||
-          grow_pinned(sl.hout, sl.cap_hout, 256u << 10, sl.grave) != hipSuccess) {
+      if (make_stream(sl) != COA_OK) {
         init_rc_ = COA_EHIP;
         return false;
       }
     }
-    for (int i = 0; i < nctx; i++)
-      if (std::find(devs_.begin(), devs_.end(), ids[i]) == devs_.end()) devs_.push_back(ids[i]);
     rescue_.resize(devs_.size());
     for (size_t i = 0; i < devs_.size(); i++) {
       rescue_[i].dev = devs_[i];
@@ -353,6 +371,7 @@ class HipBackend : public coa_q::Backend {
   // 64-byte digests.
   int enqueue(Slot& sl, coa_q::Launch& L, bool inject) {
     if (hipSetDevice(sl.dev) != hipSuccess) return COA_EHIP;
+    const auto t_pack = std::chrono::steady_clock::now();
     // a window of few signatures takes the latency kernel (one four-wave
     // workgroup per signature: ~0.1 ms however few, against ~0.8 ms for the
     // one-lane throughput kernels); its inputs are interleaved 128-byte
@@ -444,7 +463,14 @@ class HipBackend : public coa_q::Backend {
     } else {
       for (const CoaCopySeg& g : bulk) std::memcpy(g.dst, g.src, g.bytes);
     }
-    if (L.nv + L.nc + L.nd == 0) return COA_OK;  // bare vote batches only: done in complete()
+    const auto t_enq = std::chrono::steady_clock::now();
+    L.stage_ns[COA_QSTAGE_PACK] += ns_between(t_pack, t_enq);
+    if (L.nv + L.nc + L.nd == 0) return COA_OK;  // bare vote batches only: left to resolve()
+    struct EnqClock {  // ENQUEUE stage: every return below
+      coa_q::Launch& L;
+      std::chrono::steady_clock::time_point t;
+      ~EnqClock() { L.stage_ns[COA_QSTAGE_ENQUEUE] += ns_between(t, std::chrono::steady_clock::now()); }
+    } enq_clock{L, t_enq};
     uint8_t* d = static_cast<uint8_t*>(sl.din);
     uint8_t* dout = static_cast<uint8_t*>(sl.dout);
     if (hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, sl.s) != hipSuccess) return COA_EHIP;
@@ -479,8 +505,10 @@ class HipBackend : public coa_q::Backend {
   }
 
   // Waits for the slot's work (a failed enqueue drains its stream, keeping
-  // the error), then scatters the outputs to the parts.
+  // the error), then scatters the outputs to the parts; what the kernels left
+  // open (and every bare vote batch) is marked for resolve().
   void finish(Slot& sl, coa_q::Launch& L) {
+    const auto t_wait = std::chrono::steady_clock::now();
     if (sl.launched) {
       (void)hipSetDevice(sl.dev);
       if (L.rc == COA_OK) {
@@ -490,6 +518,8 @@ class HipBackend : public coa_q::Backend {
       }
       sl.launched = false;
     }
+    const auto t_scatter = std::chrono::steady_clock::now();
+    L.stage_ns[COA_QSTAGE_DEVICE_WAIT] += ns_between(t_wait, t_scatter);
     if (L.rc == COA_OK) {
       const uint8_t* h = static_cast<const uint8_t*>(sl.hout);
       size_t v = 0, c = 0, dn = 0;
@@ -501,11 +531,8 @@ class HipBackend : public coa_q::Backend {
           std::memcpy(w->v_out.data(), h + sl.o_v + v, w->nv);
         }
         for (size_t i = 0; i < w->nd; i++) std::memcpy(&w->d_out[i * 32], h + sl.o_d + (dn + i) * 64, 32);
-        if (w->nc && L.rc == COA_OK)
-          L.rc = resolve_certs(*w, reinterpret_cast<const uint32_t*>(h + sl.o_c) + c);
-        if (w->ng && L.rc == COA_OK)
-          L.rc = coa_ed25519_verify_batch_groups(w->g_msgs.data(), w->g_pks.data(), w->g_sigs.data(),
-                                                 w->g_offs.data(), w->ng, w->g_out.data(), 0);
+        if (w->nc) scatter_certs(*w, reinterpret_cast<const uint32_t*>(h + sl.o_c) + c);
+        w->g_defer = w->ng > 0;
         v += w->nv;
         c += w->nc;
         dn += w->nd;
@@ -515,39 +542,75 @@ class HipBackend : public coa_q::Backend {
       coa_keycache_unpin(sl.keys);
       sl.keys = nullptr;
     }
+    L.stage_ns[COA_QSTAGE_SCATTER] += ns_between(t_scatter, std::chrono::steady_clock::now());
   }
 
-  // Raw certificate status words -> COA_CERT_* bits; certificates the fused
-  // kernel could not decide alone are re-run through the host-pointer entry
-  // point, which decides them exactly (as coa_certificate_verify_many does).
-  static int resolve_certs(coa_q::Window& w, const uint32_t* st) {
-    std::vector<size_t> redo;
+  // Raw certificate status words -> COA_CERT_* bits; the certificates the
+  // fused kernel could not decide alone keep their raw words and are left
+  // open for resolve().
+  static void scatter_certs(coa_q::Window& w, const uint32_t* st) {
+    w.c_raw.assign(st, st + w.nc);
+    w.c_defer.clear();
     for (size_t c = 0; c < w.nc; c++) {
-      if (st[c] & (COA_CST_VOTES_INCONCLUSIVE | COA_CST_UNCACHED)) redo.push_back(c);
+      if (st[c] & (COA_CST_VOTES_INCONCLUSIVE | COA_CST_UNCACHED)) w.c_defer.push_back((uint32_t)c);
       w.c_out[c] = (uint8_t)(st[c] & 7u);
     }
-    if (redo.empty()) return COA_OK;
-    std::vector<uint8_t> hd, ids, org, hs, vp, vs, out(redo.size(), 7);
-    std::vector<uint64_t> ho{0}, rd, vo{0};
-    for (size_t c : redo) {
-      hd.insert(hd.end(), w.c_hdata.begin() + (long)w.c_hoff[c], w.c_hdata.begin() + (long)w.c_hoff[c + 1]);
-      ho.push_back(hd.size());
-      ids.insert(ids.end(), w.c_ids.begin() + (long)c * 32, w.c_ids.begin() + (long)c * 32 + 32);
-      org.insert(org.end(), w.c_origins.begin() + (long)c * 32, w.c_origins.begin() + (long)c * 32 + 32);
-      hs.insert(hs.end(), w.c_hsigs.begin() + (long)c * 64, w.c_hsigs.begin() + (long)c * 64 + 64);
-      rd.push_back(w.c_rounds[c]);
-      vp.insert(vp.end(), w.c_pks.begin() + (long)w.c_voff[c] * 32, w.c_pks.begin() + (long)w.c_voff[c + 1] * 32);
-      vs.insert(vs.end(), w.c_sigs.begin() + (long)w.c_voff[c] * 64, w.c_sigs.begin() + (long)w.c_voff[c + 1] * 64);
-      vo.push_back(vp.size() / 32);
+  }
+
+ public:
+  // The open certificates of every window in `ws` in one exact pass
+  // (coa_certificate_resolve_raw: header signature by verify_strict and votes
+  // by the RLC kernels for a key outside the committee, the RLC kernels alone
+  // for inconclusive votes -- never the fused kernel again), and every bare
+  // vote batch in one coa_ed25519_verify_batch_groups call.
+  int resolve(const std::vector<coa_q::Window*>& ws) override {
+    std::vector<uint8_t> ids, org, hs, vp, vs;
+    std::vector<uint64_t> rd, vo{0};
+    std::vector<uint32_t> raw;
+    std::vector<uint8_t> gm, gp, gs;
+    std::vector<uint64_t> go{0};
+    for (const coa_q::Window* w : ws) {
+      for (uint32_t c : w->c_defer) {
+        ids.insert(ids.end(), w->c_ids.begin() + (long)c * 32, w->c_ids.begin() + (long)c * 32 + 32);
+        org.insert(org.end(), w->c_origins.begin() + (long)c * 32, w->c_origins.begin() + (long)c * 32 + 32);
+        hs.insert(hs.end(), w->c_hsigs.begin() + (long)c * 64, w->c_hsigs.begin() + (long)c * 64 + 64);
+        rd.push_back(w->c_rounds[c]);
+        vp.insert(vp.end(), w->c_pks.begin() + (long)w->c_voff[c] * 32, w->c_pks.begin() + (long)w->c_voff[c + 1] * 32);
+        vs.insert(vs.end(), w->c_sigs.begin() + (long)w->c_voff[c] * 64,
+                  w->c_sigs.begin() + (long)w->c_voff[c + 1] * 64);
+        vo.push_back(vp.size() / 32);
+        raw.push_back(w->c_raw[c]);
+      }
+      if (w->g_defer) {
+        gm.insert(gm.end(), w->g_msgs.begin(), w->g_msgs.end());
+        gp.insert(gp.end(), w->g_pks.begin(), w->g_pks.end());
+        gs.insert(gs.end(), w->g_sigs.begin(), w->g_sigs.end());
+        for (size_t g = 1; g <= w->ng; g++) go.push_back(go.back() + (w->g_offs[g] - w->g_offs[g - 1]));
+      }
     }
-    hd.push_back(0);
-    const int rc = coa_certificate_verify_many(hd.data(), ho.data(), ids.data(), org.data(), hs.data(), rd.data(),
-                                               vp.data(), vs.data(), vo.data(), redo.size(), 0, out.data());
-    if (rc != COA_OK) return rc;
-    for (size_t j = 0; j < redo.size(); j++) w.c_out[redo[j]] = out[j];
+    if (!raw.empty()) {
+      std::vector<uint8_t> out(raw.size(), 7);
+      const int rc = coa_certificate_resolve_raw(ids.data(), org.data(), hs.data(), rd.data(), vp.data(), vs.data(),
+                                                 vo.data(), raw.size(), raw.data(), out.data());
+      if (rc != COA_OK) return rc;
+      size_t j = 0;
+      for (coa_q::Window* w : ws)
+        for (uint32_t c : w->c_defer) w->c_out[c] = out[j++];
+    }
+    if (go.size() > 1) {
+      std::vector<uint8_t> out(go.size() - 1, 1);
+      const int rc = coa_ed25519_verify_batch_groups(gm.data(), gp.data(), gs.data(), go.data(), go.size() - 1,
+                                                     out.data(), 0);
+      if (rc != COA_OK) return rc;
+      size_t j = 0;
+      for (coa_q::Window* w : ws)
+        if (w->g_defer)
+          for (size_t g = 0; g < w->ng; g++) w->g_out[g] = out[j++];
+    }
     return COA_OK;
   }
 
+ private:
   std::vector<Slot> slots_;
   std::vector<Slot> rescue_;  // one recovery context per device, used only by retry()
   std::vector<int> devs_;     // distinct device ids

@@ -216,6 +216,15 @@ class CopyPool {
   }
   // Copies every segment, pieces of at most kPiece bytes spread over the pool.
   void copy(const std::vector<Seg>& segs) {
+    // Below kInline bytes the caller copies alone: waking the pool
+    // (notify_all of 7 threads + a done_cv wait) cost one C3 certificate
+    // (~10 KB in 7 segments) ~27 us of its 0.12 ms p50 in round 4.
+    size_t total = 0;
+    for (const Seg& g : segs) total += g.bytes;
+    if (total < kInline) {
+      for (const Seg& g : segs) std::memcpy(g.dst, g.src, g.bytes);
+      return;
+    }
     std::vector<Seg> pieces;
     for (const Seg& g : segs)
       for (size_t o = 0; o < g.bytes; o += kPiece)
@@ -252,6 +261,7 @@ class CopyPool {
 
  private:
   static constexpr size_t kPiece = 1 << 20;
+  static constexpr size_t kInline = 512 << 10;  // ~50 us of one core's memcpy
   CopyPool() {
     const char* e = getenv("COA_PACK_THREADS");
     const int n = std::max(1, std::min(16, e ? atoi(e) : 8));
@@ -346,6 +356,18 @@ double key_wcomb_budget() {
 double key_wcomb20_budget() {
   const char* v = getenv("COA_KEY_WCOMB20_MB");
   return (v ? atof(v) : 131072.0) * 1048576.0;
+}
+// Bytes of HBM the wide key combs of ALL key-cache generations resident on
+// one device at once may take (COA_KEY_RESIDENT_MB, default 224 GiB of the
+// MI355X's 288 GB, beside B's 8.9 GB comb and the contexts' workspaces): the
+// current generation, the one a registration builds beside it, and the
+// spare kept for the next registration.  A new generation takes wide combs
+// only when they fit beside the current one; a spare is kept only when it
+// fits beside the current generation (the per-generation budget
+// alone let two 65 GB generations plus a spare approach the HBM size).
+double key_resident_budget() {
+  const char* v = getenv("COA_KEY_RESIDENT_MB");
+  return (v ? atof(v) : 229376.0) * 1048576.0;
 }
 // COA_VERIFY_WAVES=3 selects the 168-VGPR instance of k_verify_halved.
 int verify_waves() {
@@ -1442,6 +1464,32 @@ int cert_resolve(const CertIn& in, const std::vector<size_t>& idx, bool hdr_too,
   return COA_OK;
 }
 
+// Raw status words of the fused kernel -> exact verdicts: a certificate with
+// a key outside the registered committee is re-decided entirely (header
+// signature by verify_strict, votes by the RLC kernels; its digest check does
+// not use the cache and stands), one whose votes were inconclusive (a vote
+// failed its own equation, or a key has torsion) by the RLC kernels alone.
+// Shared by certificates_impl and the queue's resolver
+// (coa_certificate_resolve_raw), which hands over the words of the
+// certificates its window could not answer at once.
+int resolve_raw(const CertIn& in, size_t n, uint32_t* st, uint64_t rng_seed) {
+  std::vector<size_t> uncached, rlc;
+  for (size_t i = 0; i < n; i++) {
+    if (st[i] & COA_CST_UNCACHED) {
+      st[i] &= COA_CST_BAD_HEADER_ID;  // the digest check does not use the cache
+      uncached.push_back(i);
+    } else if ((st[i] & COA_CST_VOTES_INCONCLUSIVE) && !(st[i] & COA_CST_BAD_VOTES)) {
+      rlc.push_back(i);
+    }
+  }
+  // weights for the exact re-decision only: OS entropy is a syscall, and the
+  // common call (every certificate decided by the cached kernel) needs none
+  const uint64_t seed = rng_seed || (uncached.empty() && rlc.empty()) ? rng_seed : os_entropy_seed();
+  int rc = cert_resolve(in, uncached, true, seed, st);
+  if (rc != COA_OK) return rc;
+  return cert_resolve(in, rlc, false, seed, st);
+}
+
 int certificates_impl(const CertIn& in, size_t n, uint64_t rng_seed, uint8_t* status_out) {
   if (n == 0) return COA_OK;
   if (!in.hdr_off || !in.ids || !in.origins || !in.hsigs || !in.rounds || !in.voff || !status_out)
@@ -1466,21 +1514,7 @@ int certificates_impl(const CertIn& in, size_t n, uint64_t rng_seed, uint8_t* st
         n + in.voff[n]);
   }
   if (rc != COA_OK) return rc;
-  std::vector<size_t> uncached, rlc;
-  for (size_t i = 0; i < n; i++) {
-    if (st[i] & COA_CST_UNCACHED) {
-      st[i] &= COA_CST_BAD_HEADER_ID;  // the digest check does not use the cache
-      uncached.push_back(i);
-    } else if ((st[i] & COA_CST_VOTES_INCONCLUSIVE) && !(st[i] & COA_CST_BAD_VOTES)) {
-      rlc.push_back(i);
-    }
-  }
-  // weights for the exact re-decision only: OS entropy is a syscall, and the
-  // common call (every certificate decided by the cached kernel) needs none
-  const uint64_t seed = rng_seed || (uncached.empty() && rlc.empty()) ? rng_seed : os_entropy_seed();
-  rc = cert_resolve(in, uncached, true, seed, st.data());
-  if (rc != COA_OK) return rc;
-  rc = cert_resolve(in, rlc, false, seed, st.data());
+  rc = resolve_raw(in, n, st.data(), rng_seed);
   if (rc != COA_OK) return rc;
   for (size_t i = 0; i < n; i++) status_out[i] = (uint8_t)(st[i] & 7u);
   return COA_OK;
@@ -1540,6 +1574,14 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
   const bool keep_spare = !env_is("COA_KEY_SPARE", "0");
   std::shared_ptr<KeySet> ks = keep_spare && sh.spare ? std::move(sh.spare) : std::make_shared<KeySet>();
   sh.spare.reset();
+  // wide-comb bytes the current generation keeps resident while this one is
+  // built (charged against COA_KEY_RESIDENT_MB)
+  double cur_wide = 0.0;
+  {
+    std::lock_guard<std::mutex> l(sh.mu);
+    if (sh.keys) cur_wide = (double)sh.keys->kwtabs.cap;
+  }
+  const double resident_room = key_resident_budget() - cur_wide;
   ks->dev = sh.id;
   ks->nkeys = 0;
   ks->kwide = ks->kw20 = false;
@@ -1566,7 +1608,8 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
       if (b.cap != bytes) b.release();
       return b.ensure(bytes, true);
     };
-    if ((double)nk * COA_KWCOMB20_DWORDS * 4 <= key_wcomb20_budget()) {
+    const double w20 = (double)nk * COA_KWCOMB20_DWORDS * 4, w16 = (double)nk * COA_KWCOMB_DWORDS * 4;
+    if (w20 <= key_wcomb20_budget() && w20 <= resident_room) {
       if (fit(k.kwtabs, nk * (size_t)COA_KWCOMB20_DWORDS * 4) == hipSuccess) {
         t_alloc = clk::now();
         HIP_TRY(coa_launch_key_wcombs20(k.ktabs.as<uint32_t>(), (uint32_t)nk, k.kwtabs.as<uint32_t>(), s));
@@ -1576,7 +1619,7 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
         (void)hipGetLastError();
       }
     }
-    if (!k.kw20 && (double)nk * COA_KWCOMB_DWORDS * 4 <= key_wcomb_budget()) {
+    if (!k.kw20 && w16 <= key_wcomb_budget() && w16 <= resident_room) {
       if (fit(k.kwtabs, nk * (size_t)COA_KWCOMB_DWORDS * 4) == hipSuccess) {
         HIP_TRY(coa_launch_key_wcombs(k.ktabs.as<uint32_t>(), (uint32_t)nk, k.kwtabs.as<uint32_t>(), s));
         k.kwide = true;
@@ -1585,6 +1628,7 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
         (void)hipGetLastError();
       }
     }
+    if (!k.kwide) k.kwtabs.release();  // a reused spare's wide combs no budget admits
     HIP_TRY(hipStreamSynchronize(s));
     k.nkeys = (uint32_t)nk;
     t_built = clk::now();
@@ -1615,7 +1659,13 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
       return k.ckeys.cap >= nk * 32 && k.kflags.cap >= nk * 4 && k.ktabs.cap >= nk * (size_t)COA_KEY_TAB_DWORDS * 4 &&
              k.kwtabs.cap == cur.kwtabs.cap;
     };
-    if (old && fits(*old)) {
+    // a spare only beside the current generation within COA_KEY_RESIDENT_MB
+    // (without one, the next registration allocates its wide combs while
+    // windows run: 2.4-7.6 ms held back, profiles/r04_register_ab.txt)
+    const bool room = 2.0 * (double)cur.kwtabs.cap <= key_resident_budget();
+    if (!room) {
+      old.reset();
+    } else if (old && fits(*old)) {
       sh.spare = std::const_pointer_cast<KeySet>(old);
     } else {
       old.reset();  // another size: freed now, and a spare of this size made
@@ -2135,6 +2185,24 @@ int coa_certificate_verify(const uint8_t* header_data, size_t header_len, const 
   const int rc = coa_certificate_verify_many(header_data, hoff, id, origin, header_sig, &round, vote_pks, vote_sigs,
                                              voff, 1, rng_seed, &st);
   return rc != COA_OK ? rc : (int)st;
+}
+
+int coa_certificate_resolve_raw(const uint8_t* ids, const uint8_t* origins, const uint8_t* header_sigs,
+                                const uint64_t* rounds, const uint8_t* vote_pks, const uint8_t* vote_sigs,
+                                const uint64_t* vote_offsets, size_t n, uint32_t* raw, uint8_t* status_out) {
+  int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  if (n == 0) return COA_OK;
+  if (!ids || !origins || !header_sigs || !rounds || !vote_offsets || !raw || !status_out ||
+      (vote_offsets[n] && (!vote_pks || !vote_sigs)))
+    return fail(COA_EINVAL, "null argument");
+  // the exact path never reads the header bytes (Header::digest was checked
+  // by the fused kernel and its bit stands)
+  const CertIn in{nullptr, nullptr, ids, origins, header_sigs, rounds, vote_pks, vote_sigs, vote_offsets};
+  rc = resolve_raw(in, n, raw, 0);
+  if (rc != COA_OK) return rc;
+  for (size_t i = 0; i < n; i++) status_out[i] = (uint8_t)(raw[i] & 7u);
+  return COA_OK;
 }
 
 size_t coa_certificate_workspace_bytes(size_t n, size_t n_votes) { return coa_cert_scratch_bytes(n + n_votes); }

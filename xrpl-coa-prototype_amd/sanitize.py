@@ -197,8 +197,12 @@ def _certificate_from(d, j):
 
 # ---------------------------------------------------------------------------
 def message_author(message):
-    """The authority whose connection delivered the message: the order the
-    pre-verification stage keeps (rust/primary/src/pre_verify.rs author_of)."""
+    """The message's claimed author (a certificate's: its header author):
+    the order the pre-verification stage keeps (rust/primary/src/pre_verify.rs
+    author_of).  Not the delivering connection -- a certificate forwarded by
+    another peer's Helper is ordered behind its header author's messages --
+    and unauthenticated until verified; Core depends on no cross-author
+    order (see pre_verify.rs's module doc)."""
     if isinstance(message, C.Certificate):
         return message.origin()
     return message.author
