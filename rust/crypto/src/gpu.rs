@@ -23,18 +23,23 @@
 //! it computed ahead of these synchronous calls (`verified`), which
 //! `verify` consults first.
 use crate::coa_ffi as ffi;
+use crate::degrade;
 use crate::{CryptoError, Digest, PublicKey};
 
-/// Ok / Err as the engine returned it; a negative code is an engine failure
-/// (no GPU, bad arguments, or a HIP error that persisted after the engine
-/// rebuilt the failing context and re-ran the work on every other context,
-/// coa_engine_recoveries), which must never turn into a verdict: there is no
-/// CPU fallback, so it panics with the engine's message.
-fn verdict(rc: i32) -> Result<(), CryptoError> {
+/// Ok / Err as the engine returned it, or None for an engine failure (no
+/// GPU, bad arguments, or a HIP error that persisted after the engine rebuilt
+/// the failing context and re-ran the work on every other context,
+/// coa_engine_recoveries).  A failure never turns into a verdict: the caller
+/// answers with the reference's own code (degrade.rs), or panics under
+/// COA_ON_ENGINE_FAILURE=panic.
+fn verdict(rc: i32, what: &str) -> Option<Result<(), CryptoError>> {
     match rc {
-        ffi::COA_OK => Ok(()),
-        ffi::COA_REJECT => Err(CryptoError::new()), // opaque, as ed25519::Error always is
-        _ => panic!("MI355X verification engine failure {}: {}", rc, ffi::last_error()),
+        ffi::COA_OK => Some(Ok(())),
+        ffi::COA_REJECT => Some(Err(CryptoError::new())), // opaque, as ed25519::Error always is
+        _ => {
+            degrade::engine_failed(rc, &ffi::last_error(), what);
+            None
+        }
     }
 }
 
@@ -45,9 +50,14 @@ pub fn signature_bytes(signature: &crate::Signature) -> [u8; 64] {
     signature.flatten()
 }
 
-fn engine_ok(rc: i32) -> i32 {
-    assert!(rc >= 0, "MI355X verification engine failure {}: {}", rc, ffi::last_error());
-    rc
+/// true when the engine answered; false after reporting its failure (the
+/// caller then answers with the reference's own code, degrade.rs)
+fn engine_ok(rc: i32, what: &str) -> bool {
+    if rc >= 0 {
+        return true;
+    }
+    degrade::engine_failed(rc, &ffi::last_error(), what);
+    false
 }
 
 /// Signature::verify (crypto/src/lib.rs:200-204): dalek 1.0.1 verify_strict
@@ -59,7 +69,8 @@ pub fn verify(signature: &[u8; 64], digest: &Digest, public_key: &PublicKey) -> 
     if let Some(ok) = crate::verified::take_signature(digest, public_key, signature) {
         return if ok { Ok(()) } else { Err(CryptoError::new()) };
     }
-    verdict(unsafe { ffi::coa_ed25519_verify_strict(digest.0.as_ptr(), public_key.0.as_ptr(), signature.as_ptr()) })
+    let rc = unsafe { ffi::coa_ed25519_verify_strict(digest.0.as_ptr(), public_key.0.as_ptr(), signature.as_ptr()) };
+    verdict(rc, "Signature::verify").unwrap_or_else(|| degrade::verify_strict(signature, digest, public_key))
 }
 
 /// Signature::verify_batch (crypto/src/lib.rs:206-219): dalek 1.0.1
@@ -69,14 +80,14 @@ pub fn verify_batch<'a, I>(digest: &Digest, votes: I) -> Result<(), CryptoError>
 where
     I: IntoIterator<Item = (&'a PublicKey, [u8; 64])>,
 {
-    let (mut pks, mut sigs) = (Vec::new(), Vec::new());
-    for (key, sig) in votes {
+    let votes: Vec<(PublicKey, [u8; 64])> = votes.into_iter().map(|(k, s)| (*k, s)).collect();
+    let (mut pks, mut sigs) = (Vec::with_capacity(32 * votes.len()), Vec::with_capacity(64 * votes.len()));
+    for (key, sig) in &votes {
         pks.extend_from_slice(&key.0);
-        sigs.extend_from_slice(&sig);
+        sigs.extend_from_slice(sig);
     }
-    verdict(unsafe {
-        ffi::coa_ed25519_verify_batch(digest.0.as_ptr(), pks.as_ptr(), sigs.as_ptr(), pks.len() / 32, 0)
-    })
+    let rc = unsafe { ffi::coa_ed25519_verify_batch(digest.0.as_ptr(), pks.as_ptr(), sigs.as_ptr(), votes.len(), 0) };
+    verdict(rc, "Signature::verify_batch").unwrap_or_else(|| degrade::verify_batch(digest, &votes))
 }
 
 /// Digest(Sha512(bytes)[..32]) of ONE message on the device.  One 508 KB
@@ -88,7 +99,10 @@ where
 pub fn sha512_digest(bytes: &[u8]) -> Digest {
     let offsets = [0u64, bytes.len() as u64];
     let mut out = [0u8; 32];
-    engine_ok(unsafe { ffi::coa_sha512_trunc32_many(bytes.as_ptr(), offsets.as_ptr(), 1, out.as_mut_ptr()) });
+    if !engine_ok(unsafe { ffi::coa_sha512_trunc32_many(bytes.as_ptr(), offsets.as_ptr(), 1, out.as_mut_ptr()) },
+                  "Sha512 digest") {
+        return degrade::sha512_digest(bytes);
+    }
     Digest(out)
 }
 
@@ -102,9 +116,11 @@ pub fn sha512_digests(messages: &[&[u8]]) -> Vec<Digest> {
         offsets.push(data.len() as u64);
     }
     let mut out = vec![0u8; 32 * messages.len()];
-    engine_ok(unsafe {
+    if !engine_ok(unsafe {
         ffi::coa_sha512_trunc32_many(data.as_ptr(), offsets.as_ptr(), messages.len(), out.as_mut_ptr())
-    });
+    }, "Sha512 digests") {
+        return messages.iter().map(|m| degrade::sha512_digest(m)).collect();
+    }
     out.chunks_exact(32)
         .map(|c| {
             let mut d = [0u8; 32];
@@ -122,7 +138,9 @@ where
     I: IntoIterator<Item = &'a PublicKey>,
 {
     let flat: Vec<u8> = keys.into_iter().flat_map(|k| k.0.iter().copied()).collect();
-    engine_ok(unsafe { ffi::coa_committee_register(flat.as_ptr(), flat.len() / 32) }) as usize
+    let rc = unsafe { ffi::coa_committee_register(flat.as_ptr(), flat.len() / 32) };
+    // speed only: without a key cache every call still answers exactly
+    if engine_ok(rc, "coa_committee_register") { rc as usize } else { 0 }
 }
 
 /// Many independent (digest, key, signature) triples in one launch (the
@@ -136,9 +154,11 @@ pub fn verify_many(items: &[(Digest, PublicKey, [u8; 64])]) -> Vec<Result<(), Cr
         sigs.extend_from_slice(s);
     }
     let mut out = vec![1u8; n];
-    engine_ok(unsafe {
+    if !engine_ok(unsafe {
         ffi::coa_ed25519_verify_strict_many(msgs.as_ptr(), 32, pks.as_ptr(), sigs.as_ptr(), n, out.as_mut_ptr())
-    });
+    }, "Signature::verify (many)") {
+        return items.iter().map(|(d, k, s)| degrade::verify_strict(s, d, k)).collect();
+    }
     out.into_iter().map(|v| if v == 0 { Ok(()) } else { Err(CryptoError::new()) }).collect()
 }
 
@@ -160,9 +180,11 @@ pub fn verify_batch_groups(digests: &[Digest], groups: &[Vec<(PublicKey, [u8; 64
         offsets.push((pks.len() / 32) as u64);
     }
     let mut out = vec![1u8; groups.len()];
-    engine_ok(unsafe {
+    if !engine_ok(unsafe {
         ffi::coa_ed25519_verify_batch_groups(msgs.as_ptr(), pks.as_ptr(), sigs.as_ptr(), offsets.as_ptr(),
                                              groups.len(), out.as_mut_ptr(), 0)
-    });
+    }, "Signature::verify_batch (groups)") {
+        return digests.iter().zip(groups).map(|(d, g)| degrade::verify_batch(d, g)).collect();
+    }
     out.into_iter().map(|v| if v == 0 { Ok(()) } else { Err(CryptoError::new()) }).collect()
 }

@@ -22,14 +22,17 @@
 //! panics (that would unwind across the FFI boundary): an engine failure --
 //! reported only after the queue re-ran the window on every device context
 //! (coa_queue_metrics' retried/recovered/failed counters) -- travels to the
-//! awaiting task as `Err(status)`, and the task panics there with the
-//! engine's message, as the synchronous calls in `gpu.rs` do.  There is no
-//! CPU fallback.
+//! awaiting task as `Err(status)` with the request's inputs handed back, and
+//! the task answers it there with the reference's own code (degrade.rs:
+//! ed25519-dalek's verify_strict / verify_batch and its Sha512, so the
+//! verdict is the reference's), or panics under COA_ON_ENGINE_FAILURE=panic,
+//! as the synchronous calls in `gpu.rs` do.
 //!
 //! Wiring (crypto/src/lib.rs): `pub mod service;`.  One service per process,
 //! created once the committee is registered (node/src/main.rs):
 //!     let verifier = crypto::service::VerifyService::new(65_536, 500);
 use crate::coa_ffi as ffi;
+use crate::degrade;
 use crate::{CryptoError, Digest, PublicKey};
 use std::os::raw::{c_int, c_void};
 use tokio::sync::mpsc::{channel, Receiver, Sender};
@@ -127,12 +130,13 @@ impl CertificateCrypto {
 }
 
 /// A worker batch on its way through the engine, handed back with its digest
-/// (the batch is then stored, worker/src/processor.rs:41).
-type DigestReply = Result<(Digest, Vec<u8>), c_int>;
+/// (the batch is then stored, worker/src/processor.rs:41) -- or with the
+/// engine's failure status, for the CPU answer (degrade.rs).
+type DigestReply = Result<(Digest, Vec<u8>), (c_int, Vec<u8>)>;
 
 /// A certificate's COA_CERT_* bits, with its crypto handed back (it becomes
-/// the `verified` key without a copy).
-type CertificateReply = Result<(u8, CertificateCrypto), c_int>;
+/// the `verified` key without a copy) -- or with the engine's failure status.
+type CertificateReply = Result<(u8, CertificateCrypto), (c_int, CertificateCrypto)>;
 
 enum Request {
     Verify(Digest, PublicKey, [u8; 64], oneshot::Sender<Verdict>),
@@ -215,17 +219,26 @@ impl VerifyService {
         self.send(Request::Verify(digest.clone(), *key, signature, sender)).await;
         match receiver.await.expect("Failed to receive verdict from Verify Service") {
             Ok(verdict) => verdict,
-            Err(status) => panic!("MI355X verification engine failure {} (every context failed)", status),
+            Err(status) => {
+                degrade::engine_failed(status, "every context failed", "VerifyService::verify");
+                degrade::verify_strict(&signature, digest, key)
+            }
         }
     }
 
     /// `Signature::verify_batch(digest, votes)` (crypto/src/lib.rs:206-219).
     pub async fn verify_batch(&self, digest: &Digest, votes: Vec<(PublicKey, [u8; 64])>) -> Result<(), CryptoError> {
         let (sender, receiver) = oneshot::channel();
+        // kept for the CPU answer of an engine failure (bare vote batches are
+        // rare next to whole certificates: the copy is a few KB)
+        let kept = votes.clone();
         self.send(Request::Batch(digest.clone(), votes, sender)).await;
         match receiver.await.expect("Failed to receive verdict from Verify Service") {
             Ok(verdict) => verdict,
-            Err(status) => panic!("MI355X verification engine failure {} (every context failed)", status),
+            Err(status) => {
+                degrade::engine_failed(status, "every context failed", "VerifyService::verify_batch");
+                degrade::verify_batch(digest, &kept)
+            }
         }
     }
 
@@ -237,7 +250,12 @@ impl VerifyService {
         self.send(Request::Certificate(crypto, sender)).await;
         match receiver.await.expect("Failed to receive status from Verify Service") {
             Ok(reply) => reply,
-            Err(status) => panic!("MI355X verification engine failure {} (every context failed)", status),
+            Err((status, c)) => {
+                degrade::engine_failed(status, "every context failed", "VerifyService::certificate");
+                let bits = degrade::certificate_bits(c.header_input(), c.id(), c.origin(), c.header_signature(),
+                                                     c.round(), c.vote_keys(), c.vote_signatures());
+                (bits, c)
+            }
         }
     }
 
@@ -248,7 +266,10 @@ impl VerifyService {
         self.send(Request::Digest(bytes, sender)).await;
         match receiver.await.expect("Failed to receive digest from Verify Service") {
             Ok(reply) => reply,
-            Err(status) => panic!("MI355X verification engine failure {} (every context failed)", status),
+            Err((status, bytes)) => {
+                degrade::engine_failed(status, "every context failed", "VerifyService::digest");
+                (degrade::sha512_digest(&bytes), bytes)
+            }
         }
     }
 }
@@ -326,8 +347,8 @@ fn submit_certificate(queue: &Queue, crypto: CertificateCrypto, sender: oneshot:
     };
     if rc != ffi::COA_OK {
         let pair = unsafe { Box::from_raw(user as *mut (oneshot::Sender<CertificateReply>, CertificateCrypto)) };
-        let (sender, _) = *pair;
-        let _ = sender.send(Err(rc));
+        let (sender, crypto) = *pair;
+        let _ = sender.send(Err((rc, crypto)));
     }
 }
 
@@ -341,8 +362,8 @@ fn submit_digest(queue: &Queue, bytes: Vec<u8>, sender: oneshot::Sender<DigestRe
     let rc = unsafe { ffi::coa_queue_submit_digest(queue.0, ptr, len, Some(on_digest), user) };
     if rc != ffi::COA_OK {
         let pair = unsafe { Box::from_raw(user as *mut (oneshot::Sender<DigestReply>, Vec<u8>)) };
-        let (sender, _) = *pair;
-        let _ = sender.send(Err(rc));
+        let (sender, bytes) = *pair;
+        let _ = sender.send(Err((rc, bytes)));
     }
 }
 
@@ -387,9 +408,9 @@ unsafe extern "C" fn on_status(user: *mut c_void, status: c_int, verdicts: *cons
     let pair = Box::from_raw(user as *mut (oneshot::Sender<CertificateReply>, CertificateCrypto));
     let (sender, crypto) = *pair;
     let reply = if status != ffi::COA_OK {
-        Err(status)
+        Err((status, crypto))
     } else if verdicts.is_null() || n != 1 {
-        Err(ffi::COA_EINVAL)
+        Err((ffi::COA_EINVAL, crypto))
     } else {
         Ok((*verdicts, crypto))
     };
@@ -401,9 +422,9 @@ unsafe extern "C" fn on_digest(user: *mut c_void, status: c_int, verdicts: *cons
     let pair = Box::from_raw(user as *mut (oneshot::Sender<DigestReply>, Vec<u8>));
     let (sender, bytes) = *pair;
     let reply = if status != ffi::COA_OK {
-        Err(status)
+        Err((status, bytes))
     } else if verdicts.is_null() || n != 32 {
-        Err(ffi::COA_EINVAL)
+        Err((ffi::COA_EINVAL, bytes))
     } else {
         let mut digest = [0u8; 32];
         digest.copy_from_slice(std::slice::from_raw_parts(verdicts, 32));

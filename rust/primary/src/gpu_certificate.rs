@@ -49,9 +49,15 @@ const BAD_HEADER_ID: c_int = 1;
 const BAD_HEADER_SIG: c_int = 2;
 const BAD_VOTES: c_int = 4;
 
-fn engine_failure(rc: c_int) -> ! {
+/// An engine failure (every context failed, or no GPU): reported (or a
+/// panic under COA_ON_ENGINE_FAILURE=panic), then the certificate's crypto
+/// bits come from the reference's own ed25519-dalek / Sha512 code
+/// (crypto/src/degrade.rs), so the DagError is still the reference's.
+fn engine_failure(rc: c_int, c: &CertificateCrypto) -> c_int {
     let msg = unsafe { std::ffi::CStr::from_ptr(coa_last_error()) }.to_string_lossy().into_owned();
-    panic!("MI355X verification engine failure {}: {}", rc, msg)
+    crypto::degrade::engine_failed(rc, &msg, "Certificate::verify");
+    crypto::degrade::certificate_bits(c.header_input(), c.id(), c.origin(), c.header_signature(), c.round(),
+                                      c.vote_keys(), c.vote_signatures()) as c_int
 }
 
 /// Length of the bytes Header::digest hashes (primary/src/messages.rs:70-84).
@@ -131,9 +137,7 @@ pub fn verify(cert: &Certificate, committee: &Committee) -> DagResult<()> {
                                c.origin().as_ptr(), c.header_signature().as_ptr(), c.round(),
                                c.vote_keys().as_ptr(), c.vote_signatures().as_ptr(), c.n_votes(), 0)
     };
-    if st < 0 {
-        engine_failure(st);
-    }
+    let st = if st < 0 { engine_failure(st, &c) } else { st };
     checks_in_order(cert, committee, st)
 }
 
@@ -172,7 +176,10 @@ pub fn verify_many(certs: &[&Certificate], committee: &Committee) -> Vec<DagResu
                                         voff.as_ptr(), n, 0, status.as_mut_ptr())
         };
         if rc < 0 {
-            engine_failure(rc);
+            // every certificate of the window answered by the reference's code
+            for (j, &i) in todo.iter().enumerate() {
+                status[j] = engine_failure(rc, &certificate_crypto(certs[i])) as u8;
+            }
         }
     }
     let mut out: Vec<DagResult<()>> = (0..certs.len()).map(|_| Ok(())).collect();

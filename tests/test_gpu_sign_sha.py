@@ -85,3 +85,26 @@ def test_sha512_lanes_per_message_ragged(engine, lanes, monkeypatch):
     got = engine.sha512_many(msgs)
     for m, g in zip(msgs, got):
         assert bytes(g) == hashlib.sha512(m).digest(), len(m)
+
+
+@pytest.mark.parametrize("lanes", ["2", "4", "8", "64"])
+@pytest.mark.parametrize("prefetch", ["0", "1"])
+def test_sha512_prefetched_whole_blocks(engine, lanes, prefetch, monkeypatch):
+    """k_sha512_ml's prefetched loop over the groups of blocks that are whole
+    for every message of a wave, then the padded tail groups: 16-byte-aligned
+    messages (lengths multiples of 16, so each starts aligned in the packed
+    buffer) of different block counts in one wave -- the wave-uniform end of
+    the whole groups falls inside some messages and after others -- plus a
+    wave whose last groups have dead lanes; with and without the prefetch
+    (COA_SHA_PREFETCH), vs hashlib."""
+    import hashlib
+    import random
+
+    monkeypatch.setenv("COA_SHA_LANES", lanes)
+    monkeypatch.setenv("COA_SHA_PREFETCH", prefetch)
+    rng = random.Random(7 + int(lanes))
+    lens = [16 * rng.randrange(0, 200) for _ in range(45)] + [128 * 40, 128 * 40 + 112, 16 * 513]
+    msgs = [bytes(rng.getrandbits(8) for _ in range(n)) for n in lens]
+    got = engine.sha512_many(msgs)
+    for m, g in zip(msgs, got):
+        assert bytes(g) == hashlib.sha512(m).digest(), len(m)

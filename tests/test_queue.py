@@ -232,7 +232,7 @@ def test_open_certificate_does_not_hold_its_window_gpu(engine):
     lo = int(b.offsets[6])
     p_out, s_out = engine.sign_many(workloads.key_seeds(1, 77_777), b.cert_digests[6:7])
     b.vote_pks[lo], b.vote_sigs[lo] = p_out[0], s_out[0]   # certificate 6: open, Ok
-    b.vote_sigs[int(b.offsets[11]) + 2, 45] ^= 1             # certificate 11: bad vote (decided by the kernel)
+    b.vote_sigs[int(b.offsets[11]) + 2, 45] ^= 1             # certificate 11: bad vote (open, then Err)
     zs = np.random.default_rng(3).integers(0, 256, (int(b.offsets[-1]), 16), dtype=np.uint8)
     exp = co.certificate_verify_many(list(b.header_inputs), b.ids, b.authors, b.header_sigs, b.round, b.vote_pks,
                                      b.vote_sigs, b.offsets, zs, min(8, os.cpu_count() or 1))
@@ -266,7 +266,10 @@ def test_open_certificate_does_not_hold_its_window_gpu(engine):
             assert f.result(timeout=60) == want
         m = q.metrics()
     assert exp[6] == 0 and exp[11] == engine.CERT_BAD_VOTES
-    assert m["windows"] == 1 and m["deferred_requests"] == 1 and m["resolver_passes"] == 1
-    # the open certificate is the last answer of its window
-    assert order[-1] == ("cert", 6), order[-5:]
+    # two open certificates: 6 (a key outside the committee) and 11 (its
+    # corrupted vote fails its own equation: inconclusive until the exact
+    # random-linear-combination check, which may not assume R torsion-free)
+    assert m["windows"] == 1 and m["deferred_requests"] == 2 and m["resolver_passes"] == 1
+    # they are the last answers of their window, decided in one resolver pass
+    assert set(order[-2:]) == {("cert", 6), ("cert", 11)}, order[-5:]
     assert len(order) == len(futs)

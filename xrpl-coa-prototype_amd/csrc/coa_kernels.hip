@@ -286,7 +286,13 @@ __global__ void __launch_bounds__(256) k_sha512_many(const uint8_t* __restrict__
 // rounds of those L blocks from LDS (28 instructions per round).  One
 // 64-thread workgroup per wave; G = 64 / L messages per wave.
 // ---------------------------------------------------------------------------
-template <int L>
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int L, bool PF>
 __global__ void __launch_bounds__(64) k_sha512_ml(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
                                                   uint32_t n, uint32_t* __restrict__ out) {
   constexpr int G = 64 / L;
@@ -310,8 +316,61 @@ __global__ void __launch_bounds__(64) k_sha512_ml(const uint8_t* __restrict__ da
   const coa_sha::Lane2 L2 = coa_sha::lane2(q);
   uint64_t hs[4];
   coa_sha::init2(hs, L2);
+  // PF: the groups of blocks that are whole for every live message of the
+  // wave run first, each lane's next block (b0 + L + q) loaded into
+  // registers before the group's rounds run, so its global-memory latency
+  // hides behind L compressions instead of sitting on the message's serial
+  // chain (a lone wave per SIMD has no other wave to cover it); the padded
+  // tail groups follow, loading on demand.  Kept as two loops: with the
+  // padded loads in the same loop body the compiler's wait-count merge made
+  // the wave wait for the prefetch (s_waitcnt vmcnt(0)) before its first
+  // compression.
+  const uint64_t nwhole = (reinterpret_cast<uintptr_t>(p) & 15) == 0 ? len / 128 : 0;
+  uint64_t fe = PF ? (live ? nwhole / L * L : ~0ull) : 0;  // wave-uniform end of the whole groups
+#pragma unroll
+  for (int o = 32; PF && o > 0; o >>= 1) {
+    const uint64_t other = ((uint64_t)__shfl_xor((int)(fe >> 32), o, 64) << 32) |
+                           (uint32_t)__shfl_xor((int)(uint32_t)fe, o, 64);
+    fe = other < fe ? other : fe;
+  }
+  if (fe == ~0ull) fe = 0;
+  uint64_t b0 = 0;
+  if (PF && fe > 0) {
+    // every lane loads and expands unconditionally (one straight-line body,
+    // so the prefetch registers are not copied behind a wait): a live lane
+    // its next whole block, clamped to its last one; a dead lane (no
+    // message) re-reads the first block of `data`, which exists because a
+    // live message of the wave has >= L whole blocks, and its state is never
+    // written out
+    const uint8_t* base = live ? p : data;
+    const uint64_t last = live ? nwhole - 1 : 0;
+    uint4 nxt[8];
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(base + (live ? (uint64_t)q : 0) * 128);
+#pragma unroll
+      for (int i = 0; i < 8; i++) nxt[i] = src[i];
+    }
 #pragma unroll 1
-  for (uint64_t b0 = 0; b0 < maxblk; b0 += L) {
+    for (; b0 < fe; b0 += L) {
+      uint64_t W[16];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        W[2 * i] = coa_sha::be64(nxt[i].x, nxt[i].y);
+        W[2 * i + 1] = coa_sha::be64(nxt[i].z, nxt[i].w);
+      }
+      const uint64_t nb = b0 + L + q < last ? b0 + L + q : last;
+      const uint4* src = reinterpret_cast<const uint4*>(base + (live ? nb : 0) * 128);
+#pragma unroll
+      for (int i = 0; i < 8; i++) nxt[i] = src[i];
+      coa_sha::expand_kws<64>(kw + q * G + grp, W);
+      lds_sync();
+#pragma unroll 1
+      for (int j = 0; j < L; j++) coa_sha::compress_kw2<64>(hs, kw + j * G + grp, L2);
+      lds_sync();
+    }
+  }
+#pragma unroll 1
+  for (; b0 < maxblk; b0 += L) {
     if (b0 + q < nblk) {
       uint64_t W[16];
       coa_sha::padded_block(W, p, len, b0 + q, nblk);
@@ -478,21 +537,35 @@ hipError_t coa_launch_verify_strict(const uint8_t* pks, const uint8_t* sigs, con
 hipError_t coa_launch_sha512_many(const uint8_t* data, const uint64_t* off, uint32_t n, uint32_t* out,
                                   hipStream_t s) {
   if (n == 0) return hipSuccess;
-  // lanes per message: enough messages fill 1024 waves (one per SIMD) with
-  // one lane each; fewer share the schedule work (COA_SHA_LANES overrides)
+  // lanes per message: at least 1024 waves (one per SIMD; a message's
+  // compressions are one serial chain, so a SIMD left without a wave is lost
+  // time, and more lanes per message split its schedule work further) --
+  // 16,384 worker batches take 4 lanes each (round 4 gave them 2: 512 waves,
+  // half the SIMDs idle); COA_SHA_LANES overrides, COA_SHA_PREFETCH=0 turns
+  // the next-block prefetch off (A/B; both read per call)
   uint32_t L = 1;
-  while (L < 64 && (uint64_t)n * L * 2 <= 65536) L *= 2;
+  while (L < 64 && (uint64_t)n * L < 65536) L *= 2;
   if (const char* e = getenv("COA_SHA_LANES")) L = (uint32_t)atoi(e);
+  const char* pf_env = getenv("COA_SHA_PREFETCH");
+  const bool pf = !(pf_env && pf_env[0] == '0');
   const uint32_t waves = (uint32_t)(((uint64_t)n * L + 63) / 64);
+#define COA_SHA_ML(LL)                                                                                  \
+  case LL:                                                                                              \
+    if (pf)                                                                                             \
+      hipLaunchKernelGGL((k_sha512_ml<LL, true>), dim3(waves), dim3(64), 0, s, data, off, n, out);   \
+    else                                                                                                \
+      hipLaunchKernelGGL((k_sha512_ml<LL, false>), dim3(waves), dim3(64), 0, s, data, off, n, out);  \
+    break;
   switch (L) {
-    case 2: hipLaunchKernelGGL(k_sha512_ml<2>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
-    case 4: hipLaunchKernelGGL(k_sha512_ml<4>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
-    case 8: hipLaunchKernelGGL(k_sha512_ml<8>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
-    case 16: hipLaunchKernelGGL(k_sha512_ml<16>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
-    case 32: hipLaunchKernelGGL(k_sha512_ml<32>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
-    case 64: hipLaunchKernelGGL(k_sha512_ml<64>, dim3(waves), dim3(64), 0, s, data, off, n, out); break;
+    COA_SHA_ML(2)
+    COA_SHA_ML(4)
+    COA_SHA_ML(8)
+    COA_SHA_ML(16)
+    COA_SHA_ML(32)
+    COA_SHA_ML(64)
     default: hipLaunchKernelGGL(k_sha512_many, dim3(grid_for(n, 64, 65536)), dim3(64), 0, s, data, off, n, out);
   }
+#undef COA_SHA_ML
   return hipGetLastError();
 }
 

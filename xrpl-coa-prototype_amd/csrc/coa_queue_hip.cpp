@@ -552,7 +552,11 @@ class HipBackend : public coa_q::Backend {
     w.c_raw.assign(st, st + w.nc);
     w.c_defer.clear();
     for (size_t c = 0; c < w.nc; c++) {
-      if (st[c] & (COA_CST_VOTES_INCONCLUSIVE | COA_CST_UNCACHED)) w.c_defer.push_back((uint32_t)c);
+      // exactly the words coa_certificate_resolve_raw re-decides: a key
+      // outside the committee, or inconclusive votes not already bad
+      const bool open = (st[c] & COA_CST_UNCACHED) ||
+                        ((st[c] & COA_CST_VOTES_INCONCLUSIVE) && !(st[c] & COA_CST_BAD_VOTES));
+      if (open) w.c_defer.push_back((uint32_t)c);
       w.c_out[c] = (uint8_t)(st[c] & 7u);
     }
   }
