@@ -47,3 +47,53 @@ def engine():
 
     coa_crypto.init(0)
     return coa_crypto
+
+
+@pytest.fixture(autouse=True)
+def _kfd_queue_trace(request):
+    """COA_TRACE_KFD_QUEUES=1 (diagnostics only): print how many hardware
+    queues the kernel driver holds for this process before and after each
+    test (/sys/class/kfd/kfd/proc/<pid>/queues) -- a process whose queues
+    outnumber what the GPU's scheduler maps at once is time-sliced."""
+    if os.environ.get("COA_TRACE_KFD_QUEUES") != "1":
+        yield
+        return
+    path = f"/sys/class/kfd/kfd/proc/{os.getpid()}/queues"
+
+    def count():
+        try:
+            return len(os.listdir(path))
+        except OSError as e:
+            return f"n/a ({e.__class__.__name__})"
+
+    before = count()
+    yield
+    print(f"\n[kfd queues] {request.node.name}: {before} -> {count()}", file=sys.stderr, flush=True)
+
+
+@pytest.fixture(autouse=True, scope="session")
+def _gc_pause_trace():
+    """COA_TRACE_GC=1 (diagnostics only): print every Python garbage
+    collection that held the interpreter for more than 5 ms, with its
+    CLOCK_MONOTONIC time (the clock of the queue's COA_QUEUE_TRACE_SLOW_US
+    lines): a queue callback into Python waits for the GIL that long."""
+    if os.environ.get("COA_TRACE_GC") != "1":
+        yield
+        return
+    import gc
+    import time
+
+    t0 = {}
+
+    def cb(phase, info):
+        if phase == "start":
+            t0["t"] = time.monotonic()
+        else:
+            dt = time.monotonic() - t0.get("t", time.monotonic())
+            if dt > 0.005:
+                print(f"\n[gc] generation {info['generation']} pause {dt * 1e3:.1f} ms at t={t0['t']:.6f} s "
+                      f"({info['collected']} collected)", file=sys.stderr, flush=True)
+
+    gc.callbacks.append(cb)
+    yield
+    gc.callbacks.remove(cb)

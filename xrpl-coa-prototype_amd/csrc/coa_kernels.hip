@@ -325,7 +325,9 @@ __global__ void __launch_bounds__(64) k_sha512_ml(const uint8_t* __restrict__ da
   // padded loads in the same loop body the compiler's wait-count merge made
   // the wave wait for the prefetch (s_waitcnt vmcnt(0)) before its first
   // compression.
-  const uint64_t nwhole = (reinterpret_cast<uintptr_t>(p) & 15) == 0 ? len / 128 : 0;
+  // (dword loads: a message needs only 4-byte alignment -- C4's 508,052-byte
+  // batches sit at 4-byte but not 16-byte offsets of the packed buffer)
+  const uint64_t nwhole = (reinterpret_cast<uintptr_t>(p) & 3) == 0 ? len / 128 : 0;
   uint64_t fe = PF ? (live ? nwhole / L * L : ~0ull) : 0;  // wave-uniform end of the whole groups
 #pragma unroll
   for (int o = 32; PF && o > 0; o >>= 1) {
@@ -344,24 +346,21 @@ __global__ void __launch_bounds__(64) k_sha512_ml(const uint8_t* __restrict__ da
     // written out
     const uint8_t* base = live ? p : data;
     const uint64_t last = live ? nwhole - 1 : 0;
-    uint4 nxt[8];
+    uint32_t nxt[32];
     {
-      const uint4* src = reinterpret_cast<const uint4*>(base + (live ? (uint64_t)q : 0) * 128);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(base + (live ? (uint64_t)q : 0) * 128);
 #pragma unroll
-      for (int i = 0; i < 8; i++) nxt[i] = src[i];
+      for (int i = 0; i < 32; i++) nxt[i] = src[i];
     }
 #pragma unroll 1
     for (; b0 < fe; b0 += L) {
       uint64_t W[16];
 #pragma unroll
-      for (int i = 0; i < 8; i++) {
-        W[2 * i] = coa_sha::be64(nxt[i].x, nxt[i].y);
-        W[2 * i + 1] = coa_sha::be64(nxt[i].z, nxt[i].w);
-      }
+      for (int i = 0; i < 16; i++) W[i] = coa_sha::be64(nxt[2 * i], nxt[2 * i + 1]);
       const uint64_t nb = b0 + L + q < last ? b0 + L + q : last;
-      const uint4* src = reinterpret_cast<const uint4*>(base + (live ? nb : 0) * 128);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(base + (live ? nb : 0) * 128);
 #pragma unroll
-      for (int i = 0; i < 8; i++) nxt[i] = src[i];
+      for (int i = 0; i < 32; i++) nxt[i] = src[i];
       coa_sha::expand_kws<64>(kw + q * G + grp, W);
       lds_sync();
 #pragma unroll 1

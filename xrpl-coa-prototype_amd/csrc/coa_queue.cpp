@@ -58,6 +58,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -91,6 +92,7 @@ struct Req {
 
 constexpr size_t kShards = 64;  // intake shards per queue
 constexpr size_t kReport = 64;  // a shard tells the pending count every kReport items
+constexpr size_t kSpares = 4;   // recycled windows kept per shard
 
 // One intake shard.  `reported` is the part of `items` already added to the
 // queue's pending count.
@@ -99,9 +101,13 @@ struct alignas(64) Shard {
   std::unique_ptr<Window> w;
   std::vector<Req> reqs;
   size_t items = 0, reported = 0;
-  // a recycled window and request vector for the next take (capacity kept)
-  std::unique_ptr<Window> spare;
-  std::vector<Req> spare_reqs;
+  // recycled windows and request vectors for the next takes (capacity kept):
+  // up to kSpares each, because with several windows in flight a shard's
+  // windows come back later than it needs the next one -- a fresh Window
+  // grows its vectors from nothing, on new pages (round 4's streamed C3:
+  // producers copied at ~3 GB/s, the collector's take cost 60-190 us)
+  std::vector<std::unique_ptr<Window>> spares;
+  std::vector<std::vector<Req>> spare_reqs;
 };
 
 // One shard's requests inside a launch.
@@ -277,6 +283,7 @@ struct Lane {
   // COA_QUEUE_IDLE_LAUNCH (read at creation; 0 = off, the default): a window
   // closes at once while fewer than this many windows are in flight
   size_t idle_launch = 0;
+  double trace_slow_us = 0;  // COA_QUEUE_TRACE_SLOW_US (read at creation): report slower windows on stderr
 
   Lane() {
     for (size_t i = 0; i < kShards; i++) {
@@ -341,13 +348,17 @@ struct Lane {
         if (sh.items == 0) continue;
         p.w = std::move(sh.w);
         p.reqs.swap(sh.reqs);
-        if (sh.spare) {
-          sh.w = std::move(sh.spare);
+        if (!sh.spares.empty()) {
+          sh.w = std::move(sh.spares.back());
+          sh.spares.pop_back();
         } else {
           sh.w.reset(new Window());
           sh.w->reset();
         }
-        sh.reqs.swap(sh.spare_reqs);
+        if (!sh.spare_reqs.empty()) {
+          sh.reqs.swap(sh.spare_reqs.back());
+          sh.spare_reqs.pop_back();
+        }
         items = sh.items;
         rep = sh.reported;
         sh.items = sh.reported = 0;
@@ -430,6 +441,15 @@ struct Lane {
       l.unlock();
       be->complete(f.L);
       const double window_us = (double)(now_ns() - f.t_launch) * 1e-3;
+      if (trace_slow_us > 0 && window_us > trace_slow_us) {  // COA_QUEUE_TRACE_SLOW_US (diagnostics)
+        fprintf(stderr,
+                "[coa queue] slow window %.0f us at t=%.6f s: %zu items kinds %u slot %d; slot_wait %.0f pack %.0f "
+                "enqueue %.0f device_wait %.0f scatter %.0f us\n",
+                window_us, (double)f.t_launch * 1e-9, f.L.items(), f.L.kinds(), f.L.slot,
+                f.L.stage_ns[COA_QSTAGE_SLOT_WAIT] * 1e-3, f.L.stage_ns[COA_QSTAGE_PACK] * 1e-3,
+                f.L.stage_ns[COA_QSTAGE_ENQUEUE] * 1e-3, f.L.stage_ns[COA_QSTAGE_DEVICE_WAIT] * 1e-3,
+                f.L.stage_ns[COA_QSTAGE_SCATTER] * 1e-3);
+      }
       const bool retried = recoverable(f.L.rc);
       if (retried) recover(f.L);
       const int rc = f.L.rc;
@@ -521,8 +541,8 @@ struct Lane {
         p.reqs.clear();
         Shard& sh = shards[p.shard];
         std::lock_guard<std::mutex> g(sh.mu);
-        if (!sh.spare && p.w) sh.spare = std::move(p.w);
-        if (sh.spare_reqs.capacity() < p.reqs.capacity()) sh.spare_reqs.swap(p.reqs);
+        if (p.w && sh.spares.size() < kSpares) sh.spares.push_back(std::move(p.w));
+        if (sh.spare_reqs.size() < kSpares) sh.spare_reqs.push_back(std::move(p.reqs));
       }
       l.lock();
       for (int b = 0; b < HB; b++) m_hist[b] += hist[b];
@@ -681,9 +701,7 @@ void submitted(Lane* q, Shard& sh, std::unique_lock<std::mutex>& sl, Kind kind, 
 
 template <size_t N>
 inline void put(std::vector<uint8_t>& v, const uint8_t* src) {
-  const size_t at = v.size();
-  v.resize(at + N);
-  std::memcpy(v.data() + at, src, N);
+  v.insert(v.end(), src, src + N);  // one copy (resize would zero the bytes first)
 }
 }  // namespace
 
@@ -708,6 +726,7 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
     L.max_delay = std::chrono::microseconds(max_delay_us);
     if (const char* e = getenv("COA_QUEUE_HELPERS")) L.n_helpers = std::max(0, std::min(15, atoi(e)));
     if (const char* e = getenv("COA_QUEUE_IDLE_LAUNCH")) L.idle_launch = (size_t)std::max(0, std::min(64, atoi(e)));
+    if (const char* e = getenv("COA_QUEUE_TRACE_SLOW_US")) L.trace_slow_us = atof(e);
     L.be.reset(coa_q::make_backend(k));
     L.be->prepare(L.max_batch);
     L.start();

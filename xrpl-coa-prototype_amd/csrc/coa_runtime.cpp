@@ -1682,9 +1682,10 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
   old.reset();
   if (env_is("COA_REGISTER_TRACE", "1"))
     fprintf(stderr,
-            "coa_committee_register dev %d keys %zu: alloc %.1f build %.1f swap %.1f unpinned %.1f sync %.1f free "
-            "%.1f ms\n",
-            sh.id, nk, ms(t0, t_alloc), ms(t_alloc, t_built), ms(t_built, t_swap), ms(t_swap, t_unpinned),
+            "coa_committee_register dev %d keys %zu at t=%.6f s: alloc %.1f build %.1f swap %.1f unpinned %.1f sync "
+            "%.1f free %.1f ms\n",
+            sh.id, nk, std::chrono::duration<double>(t0.time_since_epoch()).count(), ms(t0, t_alloc),
+            ms(t_alloc, t_built), ms(t_built, t_swap), ms(t_swap, t_unpinned),
             ms(t_unpinned, t_synced), ms(t_synced, clk::now()));
   return COA_OK;
 }
