@@ -354,6 +354,7 @@ struct Lane {
         } else {
           sh.w.reset(new Window());
           sh.w->reset();
+          sh.w->reserve_like(*p.w);
         }
         if (!sh.spare_reqs.empty()) {
           sh.reqs.swap(sh.spare_reqs.back());

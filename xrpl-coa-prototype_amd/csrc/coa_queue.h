@@ -62,6 +62,20 @@ struct Window {
     c_defer.clear();
     g_defer = false;
   }
+  // Capacity of every vector at least `o`'s sizes: a fresh window made while
+  // the shard's recycled ones are still in flight starts at the size its
+  // predecessor reached, so producers never grow (reallocate and copy) a
+  // multi-MB vector under the shard lock, which the collector's take then
+  // waits for.
+  void reserve_like(const Window& o) {
+    auto r8 = [](std::vector<uint8_t>& v, const std::vector<uint8_t>& w) { v.reserve(w.size()); };
+    auto r64 = [](std::vector<uint64_t>& v, const std::vector<uint64_t>& w) { v.reserve(w.size()); };
+    r8(v_msgs, o.v_msgs), r8(v_pks, o.v_pks), r8(v_sigs, o.v_sigs);
+    r8(g_msgs, o.g_msgs), r8(g_pks, o.g_pks), r8(g_sigs, o.g_sigs), r64(g_offs, o.g_offs);
+    r8(c_hdata, o.c_hdata), r8(c_ids, o.c_ids), r8(c_origins, o.c_origins), r8(c_hsigs, o.c_hsigs);
+    r8(c_pks, o.c_pks), r8(c_sigs, o.c_sigs), r64(c_hoff, o.c_hoff), r64(c_rounds, o.c_rounds);
+    r64(c_voff, o.c_voff), r8(d_data, o.d_data), r64(d_offs, o.d_offs);
+  }
   // Empty again for the next intake, keeping every vector's capacity (the
   // queue recycles answered windows, so a window fills without reallocating
   // under the intake lock).
