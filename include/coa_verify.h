@@ -420,6 +420,10 @@ typedef struct {
 #define COA_QUEUE_STREAM_CUMASK 1
 #define COA_QUEUE_STREAM_PRIORITY 2
 int coa_queue_metrics(coa_queue* q, coa_queue_metrics_t* out);
+/* Zeroes the counters, maxima, stage times and the wait histogram (not the
+ * slot counts): the next coa_queue_metrics covers only what happens after,
+ * e.g. a steady-state interval after a warm-up.  No reference counterpart. */
+int coa_queue_metrics_reset(coa_queue* q);
 int coa_queue_destroy(coa_queue* q);
 
 #ifdef __cplusplus

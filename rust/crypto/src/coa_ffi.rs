@@ -188,6 +188,7 @@ extern "C" {
     pub fn coa_queue_stats(q: *mut CoaQueue, launches: *mut u64, items: *mut u64, groups: *mut u64) -> c_int;
     pub fn coa_queue_digest_count(q: *mut CoaQueue, digests: *mut u64) -> c_int;
     pub fn coa_queue_metrics(q: *mut CoaQueue, out: *mut CoaQueueMetrics) -> c_int;
+    pub fn coa_queue_metrics_reset(q: *mut CoaQueue) -> c_int;
     pub fn coa_queue_destroy(q: *mut CoaQueue) -> c_int;
 }
 

@@ -190,6 +190,10 @@ int main(int argc, char** argv) {
             qm.certificates == 1 && qm.digests == 1 && qm.wait_us_max >= qm.wait_us_mean &&
             qm.retried_windows == qm.recovered_windows && qm.failed_windows == (gpu ? 0u : qm.windows),
         "queue_metrics");
+  CHECK(coa_queue_metrics_reset(q) == COA_OK && coa_queue_metrics(q, &qm) == COA_OK && qm.requests == 0 &&
+            qm.windows == 0 && qm.wait_us_p99 == 0.0 && qm.stage_us[COA_QSTAGE_CALLBACKS] == 0.0 &&
+            (!gpu || qm.slots_verify > 0) && coa_queue_metrics_reset(NULL) == COA_EINVAL,
+        "queue_metrics_reset");
   CHECK(coa_queue_destroy(q) == COA_OK, "queue_destroy");
 
   CHECK(coa_shutdown() == COA_OK, "coa_shutdown");

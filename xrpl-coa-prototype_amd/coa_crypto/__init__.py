@@ -154,6 +154,7 @@ def lib():
         "coa_queue_set_idle_launch": ([vp, ctypes.c_uint32], ctypes.c_int),
         "coa_queue_stats": ([vp, P64, P64, P64], ctypes.c_int),
         "coa_queue_metrics": ([vp, ctypes.POINTER(QueueMetrics)], ctypes.c_int),
+        "coa_queue_metrics_reset": ([vp], ctypes.c_int),
         "coa_queue_destroy": ([vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
@@ -799,6 +800,10 @@ class AggregationQueue:
         m = QueueMetrics()
         _check(lib().coa_queue_metrics(self._q, ctypes.byref(m)))
         return metrics_dict(m)
+
+    def metrics_reset(self):
+        """coa_queue_metrics_reset: start a new measurement interval."""
+        _check(lib().coa_queue_metrics_reset(self._q))
 
     def close(self):
         if self._q:

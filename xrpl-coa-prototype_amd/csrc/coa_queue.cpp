@@ -76,6 +76,14 @@ using coa_q::Window;
 
 enum Kind : uint8_t { K_VERIFY, K_BATCH, K_CERT, K_DIGEST };
 
+inline void cpu_relax() {
+#if defined(__x86_64__)
+  __builtin_ia32_pause();
+#else
+  std::this_thread::yield();
+#endif
+}
+
 inline int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
@@ -98,6 +106,11 @@ constexpr size_t kSpares = 4;   // recycled windows kept per shard
 // queue's pending count.
 struct alignas(64) Shard {
   std::mutex mu;
+  // set while the collector waits to take the shard: a producer submitting
+  // in a tight loop re-takes the (unfair) mutex within nanoseconds of
+  // releasing it, and a round-4 take waited 60-310 us per window for a gap;
+  // producers hold off while it is set, so a take waits for one copy at most
+  std::atomic<bool> taking{false};
   std::unique_ptr<Window> w;
   std::vector<Req> reqs;
   size_t items = 0, reported = 0;
@@ -240,6 +253,7 @@ struct AnswerPool {
 // One lane of a queue: intake shards, collector, backend slots, completer.
 struct Lane {
   size_t max_batch = 65536;
+  bool digest_lane = false;
   std::chrono::microseconds max_delay{500};
   std::unique_ptr<coa_q::Backend> be;
   std::unique_ptr<Shard[]> shards{new Shard[kShards]};
@@ -308,6 +322,7 @@ struct Lane {
     const size_t home = thread_ordinal() % kShards;
     for (size_t k = 0;; k++) {
       Shard& sh = shards[(home + k) % kShards];
+      while (sh.taking.load(std::memory_order_acquire)) std::this_thread::yield();
       sl = std::unique_lock<std::mutex>(sh.mu);
       if (sh.items < max_batch || k + 1 == kShards) return sh;
     }
@@ -344,7 +359,13 @@ struct Lane {
       Part p;
       size_t items, rep;
       {
-        std::lock_guard<std::mutex> l(sh.mu);
+        // spin, not sleep: the holder is inside one copy and will not re-take
+        // the lock while `taking` is set (a futex sleep here cost a scheduling
+        // round trip per shard under load)
+        sh.taking.store(true, std::memory_order_release);
+        while (!sh.mu.try_lock()) cpu_relax();
+        std::lock_guard<std::mutex> l(sh.mu, std::adopt_lock);
+        sh.taking.store(false, std::memory_order_release);
         if (sh.items == 0) continue;
         p.w = std::move(sh.w);
         p.reqs.swap(sh.reqs);
@@ -354,7 +375,7 @@ struct Lane {
         } else {
           sh.w.reset(new Window());
           sh.w->reset();
-          sh.w->reserve_like(*p.w);
+          sh.w->reserve_for(2 * max_batch, digest_lane);
         }
         if (!sh.spare_reqs.empty()) {
           sh.reqs.swap(sh.spare_reqs.back());
@@ -636,6 +657,23 @@ struct Lane {
     }
   }
 
+  void reset_metrics() {
+    std::lock_guard<std::mutex> l(mu);
+    m_requests = m_windows = m_sig = m_batch = m_cert = m_dig = 0;
+    m_max_window = m_max_in_flight = 0;
+    m_retried = m_recovered = m_failed = 0;
+    m_max_pending.store(0);
+    m_wait_sum = m_wait_max = 0.0;
+    std::fill(m_hist, m_hist + HB, 0);
+    m_window_us_max = m_slot_wait_us_max = 0.0;
+    m_window_max_items = 0;
+    m_window_max_kinds = 0;
+    m_deferred = m_passes = 0;
+    m_resolve_us_max = 0.0;
+    std::fill(m_stage_us, m_stage_us + COA_QSTAGES, 0.0);
+    be->reset_grows();
+  }
+
   void shutdown() {
     {
       std::lock_guard<std::mutex> l(mu);
@@ -725,6 +763,8 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
       L.max_batch = std::min(L.max_batch, cap);
     }
     L.max_delay = std::chrono::microseconds(max_delay_us);
+    L.digest_lane = k == coa_q::LANE_DIGEST;
+    for (size_t i = 0; i < kShards; i++) L.shards[i].w->reserve_for(2 * L.max_batch, L.digest_lane);
     if (const char* e = getenv("COA_QUEUE_HELPERS")) L.n_helpers = std::max(0, std::min(15, atoi(e)));
     if (const char* e = getenv("COA_QUEUE_IDLE_LAUNCH")) L.idle_launch = (size_t)std::max(0, std::min(64, atoi(e)));
     if (const char* e = getenv("COA_QUEUE_TRACE_SLOW_US")) L.trace_slow_us = atof(e);
@@ -896,6 +936,12 @@ int coa_queue_metrics(coa_queue* q, coa_queue_metrics_t* out) {
   out->wait_us_mean = out->requests ? wsum / (double)out->requests : 0.0;
   out->wait_us_p50 = hist_percentile(hist, 0.50);
   out->wait_us_p99 = hist_percentile(hist, 0.99);
+  return COA_OK;
+}
+
+int coa_queue_metrics_reset(coa_queue* q) {
+  if (!q) return COA_EINVAL;
+  for (Lane& L : q->lanes) L.reset_metrics();
   return COA_OK;
 }
 

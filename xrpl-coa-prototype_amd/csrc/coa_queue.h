@@ -62,19 +62,24 @@ struct Window {
     c_defer.clear();
     g_defer = false;
   }
-  // Capacity of every vector at least `o`'s sizes: a fresh window made while
-  // the shard's recycled ones are still in flight starts at the size its
-  // predecessor reached, so producers never grow (reallocate and copy) a
-  // multi-MB vector under the shard lock, which the collector's take then
-  // waits for.
-  void reserve_like(const Window& o) {
-    auto r8 = [](std::vector<uint8_t>& v, const std::vector<uint8_t>& w) { v.reserve(w.size()); };
-    auto r64 = [](std::vector<uint64_t>& v, const std::vector<uint64_t>& w) { v.reserve(w.size()); };
-    r8(v_msgs, o.v_msgs), r8(v_pks, o.v_pks), r8(v_sigs, o.v_sigs);
-    r8(g_msgs, o.g_msgs), r8(g_pks, o.g_pks), r8(g_sigs, o.g_sigs), r64(g_offs, o.g_offs);
-    r8(c_hdata, o.c_hdata), r8(c_ids, o.c_ids), r8(c_origins, o.c_origins), r8(c_hsigs, o.c_hsigs);
-    r8(c_pks, o.c_pks), r8(c_sigs, o.c_sigs), r64(c_hoff, o.c_hoff), r64(c_rounds, o.c_rounds);
-    r64(c_voff, o.c_voff), r8(d_data, o.d_data), r64(d_offs, o.d_offs);
+  // Capacity for the largest window the lane's collector closes (`items` =
+  // twice max_batch: whole shards are taken until max_batch items are in),
+  // reserved when the window is made: a producer then never grows (reallocates
+  // and copies) a multi-MB vector while it holds the shard lock, which the
+  // collector's take waits for (round 4's streamed C3: 60-310 us per take).
+  // Only address space until written (the pages of a large allocation are
+  // faulted in on first touch); bare vote batches (rare) grow on demand.
+  void reserve_for(size_t items, bool digest_lane) {
+    if (digest_lane) {
+      d_data.reserve(items * (512u << 10));  // ~500 KB worker batches
+      d_offs.reserve(items + 1);
+      return;
+    }
+    v_msgs.reserve(items * 32), v_pks.reserve(items * 32), v_sigs.reserve(items * 64);
+    c_pks.reserve(items * 32), c_sigs.reserve(items * 64);
+    const size_t nc = items / 16 + 1;  // certificates of >= 15 votes (C1's committee of 4 has 3: they regrow)
+    c_hdata.reserve(nc * 4096), c_ids.reserve(nc * 32), c_origins.reserve(nc * 32), c_hsigs.reserve(nc * 64);
+    c_hoff.reserve(nc + 1), c_rounds.reserve(nc), c_voff.reserve(nc + 1);
   }
   // Empty again for the next intake, keeping every vector's capacity (the
   // queue recycles answered windows, so a window fills without reallocating
@@ -172,6 +177,7 @@ class Backend {
   virtual void prepare(size_t max_batch) { (void)max_batch; }
   // Staging reallocations so far (each a page-locked or device allocation).
   virtual uint64_t grows() const { return 0; }
+  virtual void reset_grows() {}
   // How the slots' streams were made (COA_QUEUE_STREAM_*).
   virtual int stream_kind() const { return 0; }
 };

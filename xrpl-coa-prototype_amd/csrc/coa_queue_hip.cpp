@@ -209,6 +209,7 @@ class HipBackend : public coa_q::Backend {
   // windows of this queue lane that had to enlarge a slot's staging or
   // workspace (the warm-up at creation not counted)
   uint64_t grows() const override { return grows_.load(); }
+  void reset_grows() override { grows_.store(0); }
 
   // Everything a first window would otherwise pay for, done at queue
   // creation: the slots' streams, their page-locked and device staging, and
