@@ -1209,7 +1209,7 @@ def host_e2e(local, dev, msgs_h, pks_h, sigs_h, n_certs=10000):
     vp, sz, ci, dp = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double)
     lib.latc_verify_many.argtypes = [vp, vp, vp, sz, ci, ci, dp]
     lib.latc_certificates_many.argtypes = [vp] * 9 + [sz, vp, ci, ci, dp]
-    lib.latc_stream_certificates.argtypes = [sz, ctypes.c_uint, ci, ci] + [vp] * 9 + [sz, vp, dp, vp]
+    lib.latc_stream_certificates.argtypes = [sz, ctypes.c_uint, ci, ci, ci] + [vp] * 9 + [sz, vp, dp, vp]
     for f in (lib.latc_verify_many, lib.latc_certificates_many, lib.latc_stream_certificates):
         f.restype = ci
     out = {"pcie_h2d_GBps": round(pcie_h2d_gbps(dev), 1)}
@@ -1249,19 +1249,24 @@ def host_e2e(local, dev, msgs_h, pks_h, sigs_h, n_certs=10000):
     out["c3_host"] = {"certificates_per_call": n_certs, "bytes_in_per_certificate": round(bytes_per_cert),
                       "certs_per_s": round(n_certs * calls / el.value, 1),
                       "ms_per_round": round(el.value / calls * 1e3, 3)}
-    c3s = {}
-    for producers in (1, 4, 8):
-        met = coa_crypto.QueueMetrics()
-        rounds = 3
-        rc = lib.latc_stream_certificates(65536, 500, producers, rounds, *ptrs, n_certs, expect.ctypes.data,
-                                          ctypes.byref(el), ctypes.addressof(met))
-        assert rc == 0, f"streamed certificates: {rc} wrong"
-        md = coa_crypto.metrics_dict(met)
-        c3s[f"producers_{producers}"] = {"certificates": n_certs * rounds,
-                                         "certs_per_s": round(n_certs * rounds / el.value, 1),
-                                         "windows": int(md["windows"]),
-                                         "wait_ms_p50": round(md["wait_us_p50"] * 1e-3, 3),
-                                         "wait_ms_p99": round(md["wait_us_p99"] * 1e-3, 3), "diag": queue_diag(md)}
+    # each producer submits its share of the round as fast as it can, after
+    # one untimed round (steady state: tools/latc.c); "borrowed" requests
+    # (coa_queue_submit_certificate_borrowed, what rust/crypto/src/service.rs
+    # submits) are packed from the producer's arrays, "copied" ones are first
+    # copied into the queue's intake shard
+    c3s = {"mode": "borrowed (the Rust service's submission); copied in copied_producers_*"}
+    for borrowed in (1, 0):
+        for producers in (1, 4, 8):
+            met = coa_crypto.QueueMetrics()
+            rounds = 3
+            rc = lib.latc_stream_certificates(65536, 500, producers, rounds, borrowed, *ptrs, n_certs,
+                                              expect.ctypes.data, ctypes.byref(el), ctypes.addressof(met))
+            assert rc == 0, f"streamed certificates: {rc} wrong"
+            md = coa_crypto.metrics_dict(met)
+            key = f"producers_{producers}" if borrowed else f"copied_producers_{producers}"
+            c3s[key] = {"certificates": n_certs * rounds, "certs_per_s": round(n_certs * rounds / el.value, 1),
+                        "windows": int(md["windows"]), "wait_ms_p50": round(md["wait_us_p50"] * 1e-3, 3),
+                        "wait_ms_p99": round(md["wait_us_p99"] * 1e-3, 3), "diag": queue_diag(md)}
     out["c3_stream"] = c3s
     coa_crypto.committee_register(np.zeros((0, 32), np.uint8))
     return out
@@ -1480,6 +1485,8 @@ def summarize(value, sec, cpu):
     out["host_c2_verify_per_s"] = {t: get("host_e2e", "c2_host", f"threads_{t}", "verify_per_s") for t in "124"}
     out["host_c3_certs_per_s"] = get("host_e2e", "c3_host", "certs_per_s")
     out["c3_stream_certs_per_s"] = {p: get("host_e2e", "c3_stream", f"producers_{p}", "certs_per_s") for p in "148"}
+    out["c3_stream_copied_certs_per_s"] = {p: get("host_e2e", "c3_stream", f"copied_producers_{p}", "certs_per_s")
+                                           for p in "148"}
     out["c3_stream_wait_p99_ms"] = {p: get("host_e2e", "c3_stream", f"producers_{p}", "wait_ms_p99") for p in "148"}
     if cpu:
         out["cpu_c2_verify_per_s"] = cpu.get("value")

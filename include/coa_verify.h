@@ -333,6 +333,17 @@ int coa_queue_submit_certificate(coa_queue* q, const uint8_t* header_data, size_
                                  const uint8_t origin[32], const uint8_t header_sig[64], uint64_t round,
                                  const uint8_t* vote_pks, const uint8_t* vote_sigs, size_t n_votes, coa_verdict_cb cb,
                                  void* user);
+/* The same without the copy: the arrays are read in place -- packed by the
+ * launch that takes the request straight into the device staging, and read
+ * again by the resolver if the certificate needs the exact re-decision -- so
+ * they must stay valid and unchanged until the callback has run.  For callers
+ * that hold each request's bytes until its answer anyway
+ * (rust/crypto/src/service.rs boxes them with the reply sender): the
+ * producer's copy, one of the streamed path's two host copies, is gone. */
+int coa_queue_submit_certificate_borrowed(coa_queue* q, const uint8_t* header_data, size_t header_len,
+                                          const uint8_t id[32], const uint8_t origin[32], const uint8_t header_sig[64],
+                                          uint64_t round, const uint8_t* vote_pks, const uint8_t* vote_sigs,
+                                          size_t n_votes, coa_verdict_cb cb, void* user);
 /* Worker batch digests (worker/src/processor.rs:38, Processor::spawn): the
  * callback receives the 32-byte Digest (n = 32). */
 int coa_queue_submit_digest(coa_queue* q, const uint8_t* data, size_t len, coa_verdict_cb cb, void* user);

@@ -181,6 +181,10 @@ extern "C" {
                                         id: *const u8, origin: *const u8, header_sig: *const u8, round: u64,
                                         vote_pks: *const u8, vote_sigs: *const u8, n_votes: usize,
                                         cb: CoaVerdictCb, user: *mut c_void) -> c_int;
+    pub fn coa_queue_submit_certificate_borrowed(q: *mut CoaQueue, header_data: *const u8, header_len: usize,
+                                        id: *const u8, origin: *const u8, header_sig: *const u8, round: u64,
+                                        vote_pks: *const u8, vote_sigs: *const u8, n_votes: usize,
+                                        cb: CoaVerdictCb, user: *mut c_void) -> c_int;
     pub fn coa_queue_submit_digest(q: *mut CoaQueue, data: *const u8, len: usize, cb: CoaVerdictCb,
                                    user: *mut c_void) -> c_int;
     pub fn coa_queue_flush(q: *mut CoaQueue) -> c_int;

@@ -335,12 +335,15 @@ fn submit_batch(queue: &Queue, digest: &Digest, votes: &[(PublicKey, [u8; 64])],
 }
 
 fn submit_certificate(queue: &Queue, crypto: CertificateCrypto, sender: oneshot::Sender<CertificateReply>) {
-    // the request rides along with the sender (the queue copies its fields
-    // at submission) and comes back with the bits
+    // the request rides along with the sender and comes back with the bits:
+    // its buffer lives (boxed, never moved: the Vec's heap block stays put)
+    // until the callback has run, so the queue reads it in place
+    // (coa_queue_submit_certificate_borrowed: no intake copy; the window's
+    // launch packs it straight into the device staging)
     let user = Box::into_raw(Box::new((sender, crypto))) as *mut c_void;
     let c = unsafe { &(*(user as *const (oneshot::Sender<CertificateReply>, CertificateCrypto))).1 };
     let rc = unsafe {
-        ffi::coa_queue_submit_certificate(queue.0, c.header_input().as_ptr(), c.header_input().len(),
+        ffi::coa_queue_submit_certificate_borrowed(queue.0, c.header_input().as_ptr(), c.header_input().len(),
                                           c.id().as_ptr(), c.origin().as_ptr(), c.header_signature().as_ptr(),
                                           c.round(), c.vote_keys().as_ptr(), c.vote_signatures().as_ptr(),
                                           c.n_votes(), Some(on_status), user)

@@ -49,10 +49,10 @@ void run_launch(coa_q::Launch& L) {
     // "kernel" cannot decide alone (here: id[3] odd), are left to resolve()
     w.g_defer = w.ng > 0;
     for (size_t c = 0; c < w.nc; c++) {
-      if (w.c_ids[c * 32 + 3] & 1u)
+      if (w.c_refs[c].id[3] & 1u)
         w.c_defer.push_back((uint32_t)c);
       else
-        w.c_out[c] = v_cert(&w.c_ids[c * 32], w.c_voff[c + 1] - w.c_voff[c]);
+        w.c_out[c] = v_cert(w.c_refs[c].id, w.c_refs[c].nv);
     }
     for (size_t i = 0; i < w.nd; i++)
       for (int j = 0; j < 32; j++)
@@ -104,7 +104,7 @@ class StubBackend : public coa_q::Backend {
     std::this_thread::sleep_for(std::chrono::microseconds(200));  // slower than a window: the rest must not wait
     for (coa_q::Window* w : ws) {
       for (uint32_t c : w->c_defer) {
-        w->c_out[c] = v_cert(&w->c_ids[c * 32], w->c_voff[c + 1] - w->c_voff[c]);
+        w->c_out[c] = v_cert(w->c_refs[c].id, w->c_refs[c].nv);
         g_resolved++;
       }
       if (w->g_defer)

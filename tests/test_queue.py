@@ -119,7 +119,8 @@ def test_queue_certificates_and_digests_gpu(engine):
 
 
 @pytest.mark.gpu
-def test_queue_pipelined_windows_gpu(engine):
+@pytest.mark.parametrize("borrow", [False, True])
+def test_queue_pipelined_windows_gpu(engine, borrow):
     """Many small windows in a row (max_batch 256) from four producers mixing
     every kind: windows overlap on the device slots (max_in_flight 2..4),
     every answer equals its expectation -- valid/corrupted signatures,
@@ -163,7 +164,7 @@ def test_queue_pipelined_windows_gpu(engine):
                               engine.Signature.from_bytes(bytes(batch.vote_sigs[j]))) for j in range(lo_, hi_)]
                     out.append(("cert", q.submit_certificate(batch.header_inputs[c], bytes(batch.ids[c]),
                                                              bytes(batch.authors[c]), bytes(batch.header_sigs[c]),
-                                                             batch.round, votes), want_cert[c]))
+                                                             batch.round, votes, borrow=borrow), want_cert[c]))
                 if i % 10 == t and i // 10 < len(blobs):
                     b = blobs[i // 10]
                     out.append(("dig", q.submit_digest(b), hashlib.sha512(b).digest()[:32]))
@@ -214,7 +215,8 @@ def test_queue_idle_launch_gpu(engine, monkeypatch, mode):
 
 
 @pytest.mark.gpu
-def test_open_certificate_does_not_hold_its_window_gpu(engine):
+@pytest.mark.parametrize("borrow", [False, True])
+def test_open_certificate_does_not_hold_its_window_gpu(engine, borrow):
     """A window holding one certificate with a vote key outside the registered
     committee (validly signed: the fused kernel cannot decide it, the exact
     path says Ok) answers every other request first: the open certificate
@@ -254,7 +256,7 @@ def test_open_certificate_does_not_hold_its_window_gpu(engine):
             votes = [(engine.PublicKey(bytes(b.vote_pks[j])), engine.Signature.from_bytes(bytes(b.vote_sigs[j])))
                      for j in range(int(b.offsets[i]), int(b.offsets[i + 1]))]
             f = q.submit_certificate(b.header_inputs[i], bytes(b.ids[i]), bytes(b.authors[i]),
-                                     bytes(b.header_sigs[i]), b.round, votes)
+                                     bytes(b.header_sigs[i]), b.round, votes, borrow=borrow)
             f.add_done_callback(done(("cert", i)))
             futs.append((f, int(exp[i])))
         for i in range(n):

@@ -133,7 +133,7 @@ def test_service_callbacks_match_coa_verdict_cb():
     names = {n for n, _, _ in cbs}
     submits = re.findall(r"ffi::(coa_queue_submit_\w+)\((.*?)\)\s*\}?;", src, flags=re.S)
     assert {s for s, _ in submits} >= {"coa_queue_submit_verify_many", "coa_queue_submit_batch",
-                                       "coa_queue_submit_certificate", "coa_queue_submit_digest"}
+                                       "coa_queue_submit_certificate_borrowed", "coa_queue_submit_digest"}
     for fn_name, args in submits:
         cb = re.search(r"Some\((\w+)\)", args)
         assert cb and cb.group(1) in names, fn_name

@@ -243,7 +243,7 @@ int latc_certificates_many(const uint8_t* hdata, const uint64_t* hoff, const uin
  * Returns wrong answers (>= 0); queue metrics into *m. */
 typedef struct {
   coa_queue* q;
-  int p, producers, rounds;
+  int p, producers, rounds, borrowed;
   size_t n;
   const uint8_t *hdata, *ids, *origins, *hsigs, *vpks, *vsigs, *expect;
   const uint64_t *hoff, *rounds_of, *voff;
@@ -272,7 +272,8 @@ static void* stream_thread(void* arg) {
       q->expect = j->expect + k;
       q->wrong = j->wrong;
       q->answered = j->answered;
-      const int rc = coa_queue_submit_certificate(j->q, j->hdata + j->hoff[k], j->hoff[k + 1] - j->hoff[k],
+      const int rc = (j->borrowed ? coa_queue_submit_certificate_borrowed : coa_queue_submit_certificate)(
+                                                  j->q, j->hdata + j->hoff[k], j->hoff[k + 1] - j->hoff[k],
                                                   j->ids + 32 * k, j->origins + 32 * k, j->hsigs + 64 * k,
                                                   j->rounds_of[k], j->vpks + 32 * j->voff[k],
                                                   j->vsigs + 64 * j->voff[k], j->voff[k + 1] - j->voff[k], stream_cb, q);
@@ -284,7 +285,7 @@ static void* stream_thread(void* arg) {
   return NULL;
 }
 
-int latc_stream_certificates(size_t max_batch, unsigned max_delay_us, int producers, int rounds,
+int latc_stream_certificates(size_t max_batch, unsigned max_delay_us, int producers, int rounds, int borrowed,
                              const uint8_t* hdata, const uint64_t* hoff, const uint8_t* ids, const uint8_t* origins,
                              const uint8_t* hsigs, const uint64_t* rounds_of, const uint8_t* vpks,
                              const uint8_t* vsigs, const uint64_t* voff, size_t n, const uint8_t* expect,
@@ -302,6 +303,7 @@ int latc_stream_certificates(size_t max_batch, unsigned max_delay_us, int produc
     j->p = p;
     j->producers = producers;
     j->rounds = rounds;
+    j->borrowed = borrowed;
     j->n = n;
     j->hdata = hdata;
     j->hoff = hoff;

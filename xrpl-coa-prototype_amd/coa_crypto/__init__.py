@@ -148,6 +148,8 @@ def lib():
         "coa_queue_submit_batch": ([vp, P8, P8, P8, sz, VERDICT_CB, vp], ctypes.c_int),
         "coa_queue_submit_certificate": ([vp, P8, sz, P8, P8, P8, ctypes.c_uint64, P8, P8, sz, VERDICT_CB, vp],
                                          ctypes.c_int),
+        "coa_queue_submit_certificate_borrowed": ([vp, P8, sz, P8, P8, P8, ctypes.c_uint64, P8, P8, sz, VERDICT_CB,
+                                                   vp], ctypes.c_int),
         "coa_queue_submit_digest": ([vp, P8, sz, VERDICT_CB, vp], ctypes.c_int),
         "coa_queue_digest_count": ([vp, P64], ctypes.c_int),
         "coa_queue_flush": ([vp], ctypes.c_int),
@@ -699,6 +701,7 @@ class AggregationQueue:
         self._cf = cf
         self._lock = threading.Lock()
         self._pending = {}
+        self._borrowed = {}  # key -> arrays a borrowed request's queue entry points into
         self._next = 1
         self._cb = VERDICT_CB(self._on_verdict)  # keep alive for the queue's lifetime
         self._q = lib().coa_queue_create(max_batch, max_delay_us)
@@ -706,6 +709,7 @@ class AggregationQueue:
     def _on_verdict(self, user, status, verdicts, n):
         with self._lock:
             fut, kind = self._pending.pop(user)
+            self._borrowed.pop(user, None)  # a borrowed request's arrays: the queue is done with them
         if status < 0:
             fut.set_exception(EngineError(f"{_ERRORS.get(status, status)}"))
         elif kind == "digest":
@@ -729,8 +733,10 @@ class AggregationQueue:
                 self._pending.pop(key, None)
             _check(rc)
 
-    def submit_certificate(self, header_input, id_, origin, header_sig, round_, votes):
-        """Future of the certificate's CERT_BAD_* bits (0 = all crypto Ok)."""
+    def submit_certificate(self, header_input, id_, origin, header_sig, round_, votes, borrow=False):
+        """Future of the certificate's CERT_BAD_* bits (0 = all crypto Ok).
+        borrow=True submits through coa_queue_submit_certificate_borrowed: the
+        arrays built here are kept alive until the callback (no intake copy)."""
         key, fut = self._register("certificate")
         votes = list(votes)
         h = np.frombuffer(bytes(header_input), np.uint8).copy() if len(header_input) else np.zeros(1, np.uint8)
@@ -740,8 +746,15 @@ class AggregationQueue:
                            np.uint8).copy()
         pks = _bytes_array([bytes(pk) for pk, _ in votes], 32) if votes else np.zeros(32, np.uint8)
         sgs = _bytes_array([s.flatten() for _, s in votes], 64) if votes else np.zeros(64, np.uint8)
-        rc = lib().coa_queue_submit_certificate(self._q, _u8p(h), len(header_input), _u8p(i), _u8p(o), _u8p(sg),
-                                                round_, _u8p(pks), _u8p(sgs), len(votes), self._cb, key)
+        if borrow:
+            with self._lock:
+                self._borrowed[key] = (h, i, o, sg, pks, sgs)
+        submit = lib().coa_queue_submit_certificate_borrowed if borrow else lib().coa_queue_submit_certificate
+        rc = submit(self._q, _u8p(h), len(header_input), _u8p(i), _u8p(o), _u8p(sg), round_, _u8p(pks), _u8p(sgs),
+                    len(votes), self._cb, key)
+        if rc < 0:
+            with self._lock:
+                self._borrowed.pop(key, None)
         self._submitted(key, rc)
         return fut
 

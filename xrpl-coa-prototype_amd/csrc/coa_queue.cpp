@@ -392,6 +392,7 @@ struct Lane {
     }
     f.L.parts.clear();
     for (Part& p : f.parts) {
+      p.w->bind();
       f.L.parts.push_back(p.w.get());
       f.L.stage_ns[COA_QSTAGE_INTAKE] += p.w->intake_ns;
     }
@@ -833,17 +834,56 @@ int coa_queue_submit_certificate(coa_queue* q, const uint8_t* header_data, size_
       !cb)
     return COA_EINVAL;
   COA_Q_INTAKE(q, K_CERT)
-  if (header_len) w.c_hdata.insert(w.c_hdata.end(), header_data, header_data + header_len);
-  w.c_hoff.push_back(w.c_hdata.size());
-  put<32>(w.c_ids, id);
-  put<32>(w.c_origins, origin);
-  put<64>(w.c_hsigs, header_sig);
-  w.c_rounds.push_back(round);
-  if (n_votes) {
-    w.c_pks.insert(w.c_pks.end(), vote_pks, vote_pks + n_votes * 32);
-    w.c_sigs.insert(w.c_sigs.end(), vote_sigs, vote_sigs + n_votes * 64);
-  }
-  w.c_voff.push_back(w.c_voff.back() + n_votes);
+  // one append per field into the window's own buffer; the ref keeps offsets
+  // (bind() turns them into pointers at the take)
+  std::vector<uint8_t>& o = w.c_own;
+  auto at = [&o] { return reinterpret_cast<const uint8_t*>(static_cast<uintptr_t>(o.size())); };
+  Window::CertRef r;
+  r.hdr = at();
+  if (header_len) o.insert(o.end(), header_data, header_data + header_len);
+  r.id = at();
+  put<32>(o, id);
+  r.origin = at();
+  put<32>(o, origin);
+  r.hsig = at();
+  put<64>(o, header_sig);
+  r.vpks = at();
+  if (n_votes) o.insert(o.end(), vote_pks, vote_pks + n_votes * 32);
+  r.vsigs = at();
+  if (n_votes) o.insert(o.end(), vote_sigs, vote_sigs + n_votes * 64);
+  r.hlen = header_len;
+  r.round = round;
+  r.nv = n_votes;
+  r.owned = true;
+  w.c_refs.push_back(r);
+  w.c_votes += n_votes;
+  w.c_hbytes += header_len;
+  submitted(ln, sh, sl, K_CERT, (uint32_t)w.nc++, 1, cb, user, 1 + n_votes, t_in);
+  return COA_OK;
+}
+
+int coa_queue_submit_certificate_borrowed(coa_queue* q, const uint8_t* header_data, size_t header_len,
+                                          const uint8_t id[32], const uint8_t origin[32], const uint8_t header_sig[64],
+                                          uint64_t round, const uint8_t* vote_pks, const uint8_t* vote_sigs,
+                                          size_t n_votes, coa_verdict_cb cb, void* user) {
+  if (!q || (header_len && !header_data) || !id || !origin || !header_sig || (n_votes && (!vote_pks || !vote_sigs)) ||
+      !cb)
+    return COA_EINVAL;
+  COA_Q_INTAKE(q, K_CERT)
+  Window::CertRef r;
+  r.hdr = header_data;
+  r.id = id;
+  r.origin = origin;
+  r.hsig = header_sig;
+  r.vpks = vote_pks;
+  r.vsigs = vote_sigs;
+  r.hlen = header_len;
+  r.round = round;
+  r.nv = n_votes;
+  r.owned = false;
+  w.c_refs.push_back(r);
+  w.c_votes += n_votes;
+  w.c_hbytes += header_len;
   submitted(ln, sh, sl, K_CERT, (uint32_t)w.nc++, 1, cb, user, 1 + n_votes, t_in);
   return COA_OK;
 }

@@ -29,11 +29,24 @@ struct Window {
   std::vector<uint8_t> g_msgs, g_pks, g_sigs;
   std::vector<uint64_t> g_offs;  // ng + 1
   std::vector<uint8_t> g_out;    // ng verdicts
-  // whole certificates (coa_certificate_verify_many semantics)
+  // whole certificates (coa_certificate_verify_many semantics), one CertRef
+  // each.  A copied request (coa_queue_submit_certificate) keeps its bytes in
+  // c_own -- header input | id | origin | header signature | vote keys | vote
+  // signatures -- and its ref holds offsets into c_own until bind(); a
+  // borrowed one (coa_queue_submit_certificate_borrowed) points at the
+  // caller's arrays, which stay valid until its callback.  After bind() (the
+  // collector's take) every ref holds pointers, which the backend packs from
+  // and the resolver reads.
+  struct CertRef {
+    const uint8_t *hdr, *id, *origin, *hsig, *vpks, *vsigs;
+    uint64_t hlen, round, nv;
+    bool owned;
+  };
   size_t nc = 0;
-  std::vector<uint8_t> c_hdata, c_ids, c_origins, c_hsigs, c_pks, c_sigs;
-  std::vector<uint64_t> c_hoff, c_rounds, c_voff;  // nc + 1, nc, nc + 1
-  std::vector<uint8_t> c_out;                      // nc status bytes (COA_CERT_* bits)
+  std::vector<CertRef> c_refs;
+  std::vector<uint8_t> c_own;
+  uint64_t c_votes = 0, c_hbytes = 0;  // totals over the window's certificates
+  std::vector<uint8_t> c_out;          // nc status bytes (COA_CERT_* bits)
   // worker batch digests (coa_sha512_trunc32_many semantics)
   size_t nd = 0;
   std::vector<uint8_t> d_data;
@@ -50,7 +63,18 @@ struct Window {
 
   bool deferred() const { return !c_defer.empty() || (g_defer && ng); }
   bool is_deferred_cert(uint32_t c) const { return std::binary_search(c_defer.begin(), c_defer.end(), c); }
-  size_t items() const { return nv + nd + nc + (c_voff.empty() ? 0 : c_voff.back()) + g_offs.back(); }
+  size_t items() const { return nv + nd + nc + c_votes + g_offs.back(); }
+  // Owned refs' offsets -> pointers into c_own (which no longer changes once
+  // the collector has taken the window).
+  void bind() {
+    const uintptr_t base = reinterpret_cast<uintptr_t>(c_own.data());
+    for (CertRef& r : c_refs)
+      if (r.owned) {
+        for (const uint8_t** f : {&r.hdr, &r.id, &r.origin, &r.hsig, &r.vpks, &r.vsigs})
+          *f = reinterpret_cast<const uint8_t*>(base + reinterpret_cast<uintptr_t>(*f));
+        r.owned = false;
+      }
+  }
   // Outputs sized and set to "failed" (verdict Err, all certificate bits,
   // zero digests) before a launch or a retry.
   void reset_outputs() {
@@ -76,10 +100,11 @@ struct Window {
       return;
     }
     v_msgs.reserve(items * 32), v_pks.reserve(items * 32), v_sigs.reserve(items * 64);
-    c_pks.reserve(items * 32), c_sigs.reserve(items * 64);
-    const size_t nc = items / 16 + 1;  // certificates of >= 15 votes (C1's committee of 4 has 3: they regrow)
-    c_hdata.reserve(nc * 4096), c_ids.reserve(nc * 32), c_origins.reserve(nc * 32), c_hsigs.reserve(nc * 64);
-    c_hoff.reserve(nc + 1), c_rounds.reserve(nc), c_voff.reserve(nc + 1);
+    // copied certificates: votes 96 B per item, a header input of up to ~4 KB
+    // and 128 B more per certificate of >= 15 votes (C1's committee of 4 has
+    // 3: those regrow)
+    c_own.reserve(items * 96 + (items / 16 + 1) * 4224);
+    c_refs.reserve(items / 16 + 1);
   }
   // Empty again for the next intake, keeping every vector's capacity (the
   // queue recycles answered windows, so a window fills without reallocating
@@ -90,13 +115,12 @@ struct Window {
     g_defer = false;
     c_raw.clear();
     c_defer.clear();
-    for (auto* v : {&v_msgs, &v_pks, &v_sigs, &v_out, &g_msgs, &g_pks, &g_sigs, &g_out, &c_hdata, &c_ids, &c_origins,
-                    &c_hsigs, &c_pks, &c_sigs, &c_out, &d_data, &d_out})
+    for (auto* v : {&v_msgs, &v_pks, &v_sigs, &v_out, &g_msgs, &g_pks, &g_sigs, &g_out, &c_own, &c_out, &d_data, &d_out})
       v->clear();
-    for (auto* v : {&g_offs, &c_hoff, &c_rounds, &c_voff, &d_offs}) v->clear();
+    for (auto* v : {&g_offs, &d_offs}) v->clear();
+    c_refs.clear();
+    c_votes = c_hbytes = 0;
     g_offs.push_back(0);
-    c_hoff.push_back(0);
-    c_voff.push_back(0);
     d_offs.push_back(0);
   }
 };
@@ -128,8 +152,8 @@ struct Launch {
       ng += w->ng;
       nc += w->nc;
       nd += w->nd;
-      nvotes += w->c_voff.back();
-      hbytes += w->c_hdata.size();
+      nvotes += w->c_votes;
+      hbytes += w->c_hbytes;
       dbytes += w->d_data.size();
       gvotes += w->g_offs.back();
     }

@@ -433,22 +433,22 @@ class HipBackend : public coa_q::Backend {
         copy(h + i_vs + v * 64, w->v_sigs.data(), w->nv * 64);
         v += w->nv;
       }
-      if (w->nc) {
-        const size_t nvt = w->c_voff.back();
-        copy(h + i_ch + hb, w->c_hdata.data(), w->c_hdata.size());
-        for (size_t i = 1; i <= w->nc; i++) {
-          cho[c + i] = hb + w->c_hoff[i];
-          cvo[c + i] = cv + w->c_voff[i];
-        }
-        copy(h + i_cid + c * 32, w->c_ids.data(), w->nc * 32);
-        copy(h + i_cor + c * 32, w->c_origins.data(), w->nc * 32);
-        copy(h + i_chs + c * 64, w->c_hsigs.data(), w->nc * 64);
-        copy(h + i_crd + c * 8, w->c_rounds.data(), w->nc * 8);
-        copy(h + i_cvp + cv * 32, w->c_pks.data(), nvt * 32);
-        copy(h + i_cvs + cv * 64, w->c_sigs.data(), nvt * 64);
-        c += w->nc;
-        cv += nvt;
-        hb += w->c_hdata.size();
+      // certificates from their refs (the window's own bytes, or a borrowed
+      // request's arrays): the small fixed fields here, the header input and
+      // the votes (~9.7 KB of a C3 certificate's 9.9) as bulk segments
+      for (size_t i = 0; i < w->nc; i++, c++) {
+        const coa_q::Window::CertRef& r = w->c_refs[i];
+        copy(h + i_ch + hb, r.hdr, r.hlen);
+        hb += r.hlen;
+        cho[c + 1] = hb;
+        std::memcpy(h + i_cid + c * 32, r.id, 32);
+        std::memcpy(h + i_cor + c * 32, r.origin, 32);
+        std::memcpy(h + i_chs + c * 64, r.hsig, 64);
+        std::memcpy(h + i_crd + c * 8, &r.round, 8);
+        copy(h + i_cvp + cv * 32, r.vpks, r.nv * 32);
+        copy(h + i_cvs + cv * 64, r.vsigs, r.nv * 64);
+        cv += r.nv;
+        cvo[c + 1] = cv;
       }
       if (w->nd) {
         copy(h + i_dd + db, w->d_data.data(), w->d_data.size());
@@ -576,13 +576,13 @@ class HipBackend : public coa_q::Backend {
     std::vector<uint64_t> go{0};
     for (const coa_q::Window* w : ws) {
       for (uint32_t c : w->c_defer) {
-        ids.insert(ids.end(), w->c_ids.begin() + (long)c * 32, w->c_ids.begin() + (long)c * 32 + 32);
-        org.insert(org.end(), w->c_origins.begin() + (long)c * 32, w->c_origins.begin() + (long)c * 32 + 32);
-        hs.insert(hs.end(), w->c_hsigs.begin() + (long)c * 64, w->c_hsigs.begin() + (long)c * 64 + 64);
-        rd.push_back(w->c_rounds[c]);
-        vp.insert(vp.end(), w->c_pks.begin() + (long)w->c_voff[c] * 32, w->c_pks.begin() + (long)w->c_voff[c + 1] * 32);
-        vs.insert(vs.end(), w->c_sigs.begin() + (long)w->c_voff[c] * 64,
-                  w->c_sigs.begin() + (long)w->c_voff[c + 1] * 64);
+        const coa_q::Window::CertRef& r = w->c_refs[c];
+        ids.insert(ids.end(), r.id, r.id + 32);
+        org.insert(org.end(), r.origin, r.origin + 32);
+        hs.insert(hs.end(), r.hsig, r.hsig + 64);
+        rd.push_back(r.round);
+        vp.insert(vp.end(), r.vpks, r.vpks + r.nv * 32);
+        vs.insert(vs.end(), r.vsigs, r.vsigs + r.nv * 64);
         vo.push_back(vp.size() / 32);
         raw.push_back(w->c_raw[c]);
       }
