@@ -230,25 +230,43 @@ class CopyPool {
       for (size_t o = 0; o < g.bytes; o += kPiece)
         pieces.push_back({static_cast<uint8_t*>(g.dst) + o, static_cast<const uint8_t*>(g.src) + o,
                           std::min(kPiece, g.bytes - o)});
+    // chunks of consecutive pieces of >= kChunk bytes, claimed with one atomic
+    // add each: a queue window of C3 certificates is ~2,000 segments of a few
+    // KB, and a mutex per segment made eight threads copy at 3 GB/s
+    std::vector<size_t> cuts{0};
+    size_t acc = 0;
+    for (size_t k = 0; k < pieces.size(); k++) {
+      acc += pieces[k].bytes;
+      if (acc >= kChunk) {
+        cuts.push_back(k + 1);
+        acc = 0;
+      }
+    }
+    if (cuts.back() != pieces.size()) cuts.push_back(pieces.size());
+    const size_t nchunks = cuts.size() - 1;
     // one job at a time on the pool; a caller that finds it busy (another
     // lane's window, a host call) copies on its own thread instead of waiting
     std::unique_lock<std::mutex> call(call_mu_, std::try_to_lock);
-    if (pieces.size() <= 1 || th_.empty() || !call.owns_lock()) {
+    if (nchunks <= 1 || th_.empty() || !call.owns_lock()) {
       for (const Seg& g : pieces) std::memcpy(g.dst, g.src, g.bytes);
       return;
     }
+    // the job's own counters: a worker that wakes late holds this job (never
+    // the next one's) and finds every chunk claimed
+    auto job = std::make_shared<Job>();
+    job->pieces = pieces.data();
+    job->cuts = cuts.data();
+    job->n = nchunks;
     {
       std::lock_guard<std::mutex> l(m_);
-      job_ = &pieces;
-      next_ = 0;
-      done_ = 0;
+      job_ = job;
       gen_++;
     }
     cv_.notify_all();
-    work();
+    work(*job);
     std::unique_lock<std::mutex> l(m_);
-    done_cv_.wait(l, [&] { return done_ == pieces.size(); });
-    job_ = nullptr;
+    done_cv_.wait(l, [&] { return job->done.load(std::memory_order_acquire) == nchunks; });
+    job_.reset();
   }
   ~CopyPool() {
     {
@@ -260,42 +278,48 @@ class CopyPool {
   }
 
  private:
+  struct Job {
+    const Seg* pieces = nullptr;
+    const size_t* cuts = nullptr;  // chunk k = pieces [cuts[k], cuts[k + 1])
+    size_t n = 0;                  // chunks
+    std::atomic<size_t> next{0}, done{0};
+  };
   static constexpr size_t kPiece = 1 << 20;
+  static constexpr size_t kChunk = 256 << 10;
   static constexpr size_t kInline = 512 << 10;  // ~50 us of one core's memcpy
   CopyPool() {
     const char* e = getenv("COA_PACK_THREADS");
     const int n = std::max(1, std::min(16, e ? atoi(e) : 8));
     for (int i = 1; i < n; i++) th_.emplace_back([this] { loop(); });
   }
-  void work() {
+  void work(Job& j) {
     for (;;) {
-      Seg g;
-      {
+      const size_t k = j.next.fetch_add(1, std::memory_order_relaxed);
+      if (k >= j.n) return;
+      for (size_t i = j.cuts[k]; i < j.cuts[k + 1]; i++) std::memcpy(j.pieces[i].dst, j.pieces[i].src, j.pieces[i].bytes);
+      if (j.done.fetch_add(1, std::memory_order_acq_rel) + 1 == j.n) {
         std::lock_guard<std::mutex> l(m_);
-        if (!job_ || next_ >= job_->size()) return;
-        g = (*job_)[next_++];
+        done_cv_.notify_all();
       }
-      std::memcpy(g.dst, g.src, g.bytes);
-      std::lock_guard<std::mutex> l(m_);
-      if (++done_ == job_->size()) done_cv_.notify_all();
     }
   }
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      std::shared_ptr<Job> j;
       {
         std::unique_lock<std::mutex> l(m_);
-        cv_.wait(l, [&] { return stop_ || (gen_ != seen && job_ && next_ < job_->size()); });
+        cv_.wait(l, [&] { return stop_ || (gen_ != seen && job_); });
         if (stop_) return;
         seen = gen_;
+        j = job_;
       }
-      work();
+      work(*j);
     }
   }
   std::mutex call_mu_, m_;
   std::condition_variable cv_, done_cv_;
-  const std::vector<Seg>* job_ = nullptr;
-  size_t next_ = 0, done_ = 0;
+  std::shared_ptr<Job> job_;  // the job in progress (null between jobs)
   uint64_t gen_ = 0;
   bool stop_ = false;
   std::vector<std::thread> th_;
