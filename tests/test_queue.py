@@ -275,3 +275,22 @@ def test_open_certificate_does_not_hold_its_window_gpu(engine, borrow):
     # they are the last answers of their window, decided in one resolver pass
     assert set(order[-2:]) == {("cert", 6), ("cert", 11)}, order[-5:]
     assert len(order) == len(futs)
+
+
+@pytest.mark.gpu
+def test_cold_lane_set_up_by_its_first_window_gpu(engine, monkeypatch):
+    """COA_QUEUE_LANES=verify (a primary never hashes worker
+    batches): only the verify lane's slots are set up at creation; the digest
+    lane's first window sets its own up, and its digests are still exact."""
+    import hashlib
+
+    monkeypatch.setenv("COA_QUEUE_LANES", "verify")
+    vecs = [v for v in load_golden("verify_vectors.json") if len(v["msg"]) == 64][:8]
+    with engine.AggregationQueue(max_batch=4096, max_delay_us=200) as q:
+        fs = [(q.submit_verify(bytes.fromhex(v["msg"]), bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"])), v["expect"])
+              for v in vecs]
+        blobs = [b"cold lane", b"x" * 1000]
+        ds = [q.submit_digest(b) for b in blobs]
+        q.flush()
+        assert [f.result(timeout=60) for f, _ in fs] == [e for _, e in fs]
+        assert [bytes(d.result(timeout=60)) for d in ds] == [hashlib.sha512(b).digest()[:32] for b in blobs]

@@ -254,6 +254,7 @@ struct AnswerPool {
 struct Lane {
   size_t max_batch = 65536;
   bool digest_lane = false;
+  bool prepared = false;  // slots' streams and staging set up (coa_queue_create or the first window)
   std::chrono::microseconds max_delay{500};
   std::unique_ptr<coa_q::Backend> be;
   std::unique_ptr<Shard[]> shards{new Shard[kShards]};
@@ -428,6 +429,10 @@ struct Lane {
       f.L.reset_outputs();
       f.L.attempts = 1;
       f.t_launch = now_ns();
+      if (!prepared) {  // a lane COA_QUEUE_LANES left cold: set up by its first window
+        be->prepare(max_batch);
+        prepared = true;
+      }
       be->launch(f.L);  // stages and enqueues; blocks only while every slot is busy
       f.L.stage_ns[COA_QSTAGE_SLOT_WAIT] += f.L.slot_wait_ns;
       l.lock();
@@ -770,7 +775,18 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
     if (const char* e = getenv("COA_QUEUE_IDLE_LAUNCH")) L.idle_launch = (size_t)std::max(0, std::min(64, atoi(e)));
     if (const char* e = getenv("COA_QUEUE_TRACE_SLOW_US")) L.trace_slow_us = atof(e);
     L.be.reset(coa_q::make_backend(k));
-    L.be->prepare(L.max_batch);
+    // COA_QUEUE_LANES=verify|digest|verify,digest (read at creation; default
+    // both): the lanes set up now -- streams, their first dispatch, staging
+    // (a verify slot ~23 MB page-locked + ~320 MB of HBM at max_batch 65,536,
+    // a digest slot 64 + 64 MB, four of each per GPU).  A primary that never
+    // hashes worker batches, or a worker that never verifies, names its lane;
+    // the other is set up by its first window (which then waits ~25-75 ms).
+    const char* lanes = getenv("COA_QUEUE_LANES");
+    const bool warm = !lanes || std::strstr(lanes, k == coa_q::LANE_DIGEST ? "digest" : "verify") != nullptr;
+    if (warm) {
+      L.be->prepare(L.max_batch);
+      L.prepared = true;
+    }
     L.start();
   }
   return q;
