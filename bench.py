@@ -1209,7 +1209,8 @@ def host_e2e(local, dev, msgs_h, pks_h, sigs_h, n_certs=10000):
     vp, sz, ci, dp = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double)
     lib.latc_verify_many.argtypes = [vp, vp, vp, sz, ci, ci, dp]
     lib.latc_certificates_many.argtypes = [vp] * 9 + [sz, vp, ci, ci, dp]
-    lib.latc_stream_certificates.argtypes = [sz, ctypes.c_uint, ci, ci, ci] + [vp] * 9 + [sz, vp, dp, vp]
+    lib.latc_stream_certificates.argtypes = [sz, ctypes.c_uint, ci, ci, ci, ctypes.c_double] + [vp] * 9 + [sz, vp, dp,
+                                                                                                          vp]
     for f in (lib.latc_verify_many, lib.latc_certificates_many, lib.latc_stream_certificates):
         f.restype = ci
     out = {"pcie_h2d_GBps": round(pcie_h2d_gbps(dev), 1)}
@@ -1259,7 +1260,7 @@ def host_e2e(local, dev, msgs_h, pks_h, sigs_h, n_certs=10000):
         for producers in (1, 4, 8):
             met = coa_crypto.QueueMetrics()
             rounds = 3
-            rc = lib.latc_stream_certificates(65536, 500, producers, rounds, borrowed, *ptrs, n_certs,
+            rc = lib.latc_stream_certificates(65536, 500, producers, rounds, borrowed, 0.0, *ptrs, n_certs,
                                               expect.ctypes.data, ctypes.byref(el), ctypes.addressof(met))
             assert rc == 0, f"streamed certificates: {rc} wrong"
             md = coa_crypto.metrics_dict(met)
@@ -1267,6 +1268,22 @@ def host_e2e(local, dev, msgs_h, pks_h, sigs_h, n_certs=10000):
             c3s[key] = {"certificates": n_certs * rounds, "certs_per_s": round(n_certs * rounds / el.value, 1),
                         "windows": int(md["windows"]), "wait_ms_p50": round(md["wait_us_p50"] * 1e-3, 3),
                         "wait_ms_p99": round(md["wait_us_p99"] * 1e-3, 3), "diag": queue_diag(md)}
+    # the same stream paced at a fixed aggregate rate from 4 producers (the
+    # waits above are a burst's: every certificate of a round submitted at
+    # once, faster than any path drains them); waits here are what a request
+    # sees at that sustained load (borrowed, max_batch 16,384 items: windows
+    # of ~240 certificates)
+    for rate in (1_000_000, 2_000_000, 3_000_000):
+        met = coa_crypto.QueueMetrics()
+        rounds = 6
+        rc = lib.latc_stream_certificates(16384, 200, 4, rounds, 1, float(rate), *ptrs, n_certs,
+                                          expect.ctypes.data, ctypes.byref(el), ctypes.addressof(met))
+        assert rc == 0, f"paced streamed certificates: {rc} wrong"
+        md = coa_crypto.metrics_dict(met)
+        c3s[f"paced_{rate // 1_000_000}M"] = {
+            "certificates": n_certs * rounds, "achieved_certs_per_s": round(n_certs * rounds / el.value, 1),
+            "windows": int(md["windows"]), "wait_ms_p50": round(md["wait_us_p50"] * 1e-3, 3),
+            "wait_ms_p99": round(md["wait_us_p99"] * 1e-3, 3), "diag": queue_diag(md)}
     out["c3_stream"] = c3s
     coa_crypto.committee_register(np.zeros((0, 32), np.uint8))
     return out
@@ -1488,6 +1505,9 @@ def summarize(value, sec, cpu):
     out["c3_stream_copied_certs_per_s"] = {p: get("host_e2e", "c3_stream", f"copied_producers_{p}", "certs_per_s")
                                            for p in "148"}
     out["c3_stream_wait_p99_ms"] = {p: get("host_e2e", "c3_stream", f"producers_{p}", "wait_ms_p99") for p in "148"}
+    out["c3_stream_paced_4_producers"] = {r: [get("host_e2e", "c3_stream", f"paced_{r}", k)
+                                              for k in ("achieved_certs_per_s", "wait_ms_p50", "wait_ms_p99")]
+                                          for r in ("1M", "2M", "3M")}
     if cpu:
         out["cpu_c2_verify_per_s"] = cpu.get("value")
     errs = [k for k, v in sec.items() if isinstance(v, dict) and "error" in v]

@@ -244,6 +244,8 @@ int latc_certificates_many(const uint8_t* hdata, const uint64_t* hoff, const uin
 typedef struct {
   coa_queue* q;
   int p, producers, rounds, borrowed;
+  double rate;   /* this producer's submissions per second (0: as fast as it can) */
+  double t0_us;  /* its schedule's start */
   size_t n;
   const uint8_t *hdata, *ids, *origins, *hsigs, *vpks, *vsigs, *expect;
   const uint64_t *hoff, *rounds_of, *voff;
@@ -266,8 +268,14 @@ static void stream_cb(void* user, int status, const uint8_t* v, size_t n) {
 
 static void* stream_thread(void* arg) {
   StreamJob* j = (StreamJob*)arg;
+  size_t sent = 0;
   for (int r = 0; r < j->rounds; r++)
-    for (size_t k = (size_t)j->p; k < j->n; k += (size_t)j->producers) {
+    for (size_t k = (size_t)j->p; k < j->n; k += (size_t)j->producers, sent++) {
+      if (j->rate > 0) {  /* paced: the i-th submission at t0 + i / rate */
+        const double due = j->t0_us + (double)sent * 1e6 / j->rate;
+        while (now_us() < due) {
+        }
+      }
       StreamReq* q = (StreamReq*)malloc(sizeof(StreamReq));
       q->expect = j->expect + k;
       q->wrong = j->wrong;
@@ -286,6 +294,7 @@ static void* stream_thread(void* arg) {
 }
 
 int latc_stream_certificates(size_t max_batch, unsigned max_delay_us, int producers, int rounds, int borrowed,
+                             double rate_per_s,
                              const uint8_t* hdata, const uint64_t* hoff, const uint8_t* ids, const uint8_t* origins,
                              const uint8_t* hsigs, const uint64_t* rounds_of, const uint8_t* vpks,
                              const uint8_t* vsigs, const uint64_t* voff, size_t n, const uint8_t* expect,
@@ -304,6 +313,7 @@ int latc_stream_certificates(size_t max_batch, unsigned max_delay_us, int produc
     j->producers = producers;
     j->rounds = rounds;
     j->borrowed = borrowed;
+    j->rate = 0;
     j->n = n;
     j->hdata = hdata;
     j->hoff = hoff;
@@ -328,8 +338,12 @@ int latc_stream_certificates(size_t max_batch, unsigned max_delay_us, int produc
   coa_queue_flush(q);
   coa_queue_metrics_reset(q);
   atomic_store(&answered, 0);
-  for (int p = 0; p < producers; p++) jobs[p].rounds = rounds;
   const double t0 = now_us();
+  for (int p = 0; p < producers; p++) {
+    jobs[p].rounds = rounds;
+    jobs[p].rate = rate_per_s / producers;
+    jobs[p].t0_us = t0;
+  }
   for (int p = 0; p < producers; p++) pthread_create(&th[p], NULL, stream_thread, &jobs[p]);
   for (int p = 0; p < producers; p++) pthread_join(th[p], NULL);
   coa_queue_flush(q);
