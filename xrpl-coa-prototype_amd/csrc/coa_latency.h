@@ -21,11 +21,13 @@ struct LatArgs {
   const uint32_t* ktabs;   // [nk] radix-256 combs of -A (coa_committee.h)
   uint32_t nk;
   const uint32_t* comb;    // radix-256 comb of B (coa_halved.h)
-  // verify_batch prefilter: a verdict of 0 also certifies [l]A == O (the
-  // registered key's flag, or [l](-A) computed in-kernel for an unregistered
-  // one), so a group whose votes all give 0 passes dalek's batch equation
-  // for every z (coa_committee.hip, "verify_batch exactness")
-  uint32_t batch;
+  // verify_batch prefilter for items [0, batch_n): a verdict of 0 also
+  // certifies [l]A == O (the registered key's flag, or [l](-A) computed
+  // in-kernel for an unregistered one), so a group whose votes all give 0
+  // passes dalek's batch equation for every z (coa_committee.hip,
+  // "verify_batch exactness"); items [batch_n, n) are plain verify_strict
+  // (one launch can carry a certificate's votes and its header signature)
+  uint32_t batch_n;
 };
 
 // One 256-thread workgroup (four waves) per signature.

@@ -397,7 +397,7 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
     if (wave == 1) {  // R's decompression on the rows, the compare, the verdict
       uint32_t pre = 0;
       const uint32_t res = rcmp::decompress_eq(cmp, rw, pre);
-      const bool tf = !a.batch || (coa_sha::uni(a.kflags[slot]) & COA_KEY_TORSION_FREE) != 0u;
+      const bool tf = item >= a.batch_n || (coa_sha::uni(a.kflags[slot]) & COA_KEY_TORSION_FREE) != 0u;
       if (lane == 0) publish(a, item, pre == 0 && res == 3u && tf);
       VMARK(3)
     } else if (wave == 2) {  // [s]B on the rows, published in row-limb layout
@@ -452,7 +452,7 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
   }
 
   // ------------------------------------------------------ uncached key
-  if (a.batch) {  // verify_batch prefilter: the same check plus [l]A == O
+  if (item < a.batch_n) {  // verify_batch prefilter: the same check plus [l]A == O
     uncached_batch(a, item, wave, lane, msg, pk, rw, sw, sh_rec, sh_ok, sh_pt, sh_tab);
     return;
   }

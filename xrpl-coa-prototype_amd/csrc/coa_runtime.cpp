@@ -722,9 +722,9 @@ int lat_res_wait(Dev& d, hipStream_t s, size_t n, uint32_t tag, uint32_t* out) {
 }
 
 // msg_of: item i's message is msgs + msg_of[i] * 32 (null: item i's own).
-// batch: the verify_batch prefilter (LatArgs::batch).
+// batch_n: items [0, batch_n) take the verify_batch prefilter (LatArgs::batch_n).
 int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, size_t n, uint8_t* out,
-               const uint32_t* msg_of = nullptr, bool batch = false) {
+               const uint32_t* msg_of = nullptr, size_t batch_n = 0) {
   uint32_t tag = 0;
   int rc = lat_res_prepare(d, n, tag);
   if (rc != COA_OK) return rc;
@@ -732,7 +732,7 @@ int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* s
   std::memset(&a, 0, sizeof(a));
   hipStream_t s = d.stream;
   a.n = (uint32_t)n;
-  a.batch = batch ? 1u : 0u;
+  a.batch_n = (uint32_t)batch_n;
   a.n_inline = (uint32_t)std::min<size_t>(n, COA_LAT_INLINE);
   auto msg = [&](size_t i) { return msgs + (msg_of ? (size_t)msg_of[i] : i) * 32; };
   for (size_t i = 0; i < a.n_inline; i++) {
@@ -1032,7 +1032,7 @@ int batch_prefilter(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs
     std::unique_lock<std::mutex> l;
     Dev& d = lat_dev(l);
     HIP_TRY(hipSetDevice(d.id));
-    const int rc = lat_verify(d, msgs, pks, sigs, total, v.data(), msg_of.data(), true);
+    const int rc = lat_verify(d, msgs, pks, sigs, total, v.data(), msg_of.data(), total);
     if (rc != COA_OK) return rc;
   }
   pass.assign(n_groups, 1);
@@ -1468,9 +1468,54 @@ int cert_resolve(const CertIn& in, const std::vector<size_t>& idx, bool hdr_too,
     vs.insert(vs.end(), in.vsigs + a * 64, in.vsigs + b * 64);
     goff[j + 1] = goff[j] + (b - a);
   }
+  std::vector<uint8_t> hv(m, 0);
+  const size_t nvotes = goff[m];
+  if (hdr_too && nvotes + m <= lat_max() && !env_is("COA_BATCH_LAT", "0") && !env_is("COA_RESOLVE_ONE_LAUNCH", "0")) {
+    // ONE latency launch for the votes (the verify_batch prefilter: items
+    // [0, nvotes)) and the header signatures (plain verify_strict: items
+    // [nvotes, nvotes + m)): a certificate with keys outside the committee
+    // took a prefilter launch and then a header launch, one after the other
+    std::vector<uint8_t> msgs(gm), pks(vp), sigs(vs);
+    std::vector<uint32_t> msg_of(nvotes + m);
+    for (size_t j = 0; j < m; j++) {
+      for (uint64_t i = goff[j]; i < goff[j + 1]; i++) msg_of[i] = (uint32_t)j;
+      msg_of[nvotes + j] = (uint32_t)(m + j);
+      const size_t c = idx[j];
+      msgs.insert(msgs.end(), in.ids + c * 32, in.ids + c * 32 + 32);
+      pks.insert(pks.end(), in.origins + c * 32, in.origins + c * 32 + 32);
+      sigs.insert(sigs.end(), in.hsigs + c * 64, in.hsigs + c * 64 + 64);
+    }
+    std::vector<uint8_t> v(nvotes + m);
+    {
+      std::unique_lock<std::mutex> l;
+      Dev& d = lat_dev(l);
+      HIP_TRY(hipSetDevice(d.id));
+      rc = lat_verify(d, msgs.data(), pks.data(), sigs.data(), nvotes + m, v.data(), msg_of.data(), nvotes);
+      if (rc != COA_OK) return rc;
+    }
+    // a group every vote of which passed is Ok for every z; the others take
+    // the exact path with their own weights (as batch_groups_impl's prefilter)
+    std::vector<size_t> open;
+    for (size_t j = 0; j < m; j++) {
+      bool pass = true;
+      for (uint64_t i = goff[j]; i < goff[j + 1]; i++) pass = pass && v[i] == 0;
+      gv[j] = pass ? 0 : 1;
+      if (!pass) open.push_back(j);
+      hv[j] = v[nvotes + j] ? 1 : 0;
+    }
+    for (size_t j : open) {
+      const uint64_t a = goff[j], n = goff[j + 1] - a;
+      const uint64_t offs[2] = {0, n};
+      rc = batch_groups_impl(&gm[j * 32], vp.data() + a * 32, vs.data() + a * 64, offs, 1, nullptr, seed, &gv[j], 0,
+                             false);
+      if (rc != COA_OK) return rc;
+    }
+    for (size_t j = 0; j < m; j++)
+      status[idx[j]] |= (gv[j] ? COA_CST_BAD_VOTES : 0u) | (hv[j] ? COA_CST_BAD_HEADER_SIG : 0u);
+    return COA_OK;
+  }
   rc = batch_groups_impl(gm.data(), vp.data(), vs.data(), goff.data(), m, nullptr, seed, gv.data());
   if (rc != COA_OK) return rc;
-  std::vector<uint8_t> hv(m, 0);
   if (hdr_too) {
     std::vector<uint8_t> hm(m * 32), hp(m * 32), hs(m * 64);
     for (size_t j = 0; j < m; j++) {
