@@ -253,6 +253,7 @@ struct AnswerPool {
 // One lane of a queue: intake shards, collector, backend slots, completer.
 struct Lane {
   size_t max_batch = 65536;
+  size_t reserve_items = 131072;  // Window::reserve_for's items (coa_queue_create)
   bool digest_lane = false;
   bool prepared = false;  // slots' streams and staging set up (coa_queue_create or the first window)
   std::chrono::microseconds max_delay{500};
@@ -376,7 +377,6 @@ struct Lane {
         } else {
           sh.w.reset(new Window());
           sh.w->reset();
-          sh.w->reserve_for(2 * max_batch, digest_lane);
         }
         if (!sh.spare_reqs.empty()) {
           sh.reqs.swap(sh.spare_reqs.back());
@@ -770,7 +770,10 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
     }
     L.max_delay = std::chrono::microseconds(max_delay_us);
     L.digest_lane = k == coa_q::LANE_DIGEST;
-    for (size_t i = 0; i < kShards; i++) L.shards[i].w->reserve_for(2 * L.max_batch, L.digest_lane);
+    // windows reserve their capacity on first use (a shard no producer
+    // thread maps to never does): twice max_batch items, capped at 2 x 65,536
+    // -- a larger max_batch's windows grow past it on demand
+    L.reserve_items = 2 * std::min<size_t>(L.max_batch, 65536);
     if (const char* e = getenv("COA_QUEUE_HELPERS")) L.n_helpers = std::max(0, std::min(15, atoi(e)));
     if (const char* e = getenv("COA_QUEUE_IDLE_LAUNCH")) L.idle_launch = (size_t)std::max(0, std::min(64, atoi(e)));
     if (const char* e = getenv("COA_QUEUE_TRACE_SLOW_US")) L.trace_slow_us = atof(e);
@@ -795,13 +798,14 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
 // The submissions: the request goes into the calling thread's shard of the
 // kind's lane under that shard's lock; then the lane's pending count (and, on
 // an edge, its collector) learns of it.
-#define COA_Q_INTAKE(q, kind)              \
-  const int64_t t_in = now_ns();           \
-  Lane* ln = &(q)->lane_of(kind);          \
-  std::unique_lock<std::mutex> sl;         \
-  Shard& sh = ln->intake(sl);              \
-  if (ln->stop.load()) return COA_EINVAL;  \
-  Window& w = *sh.w;
+#define COA_Q_INTAKE(q, kind)                                                \
+  const int64_t t_in = now_ns();                                             \
+  Lane* ln = &(q)->lane_of(kind);                                            \
+  std::unique_lock<std::mutex> sl;                                           \
+  Shard& sh = ln->intake(sl);                                                \
+  if (ln->stop.load()) return COA_EINVAL;                                    \
+  Window& w = *sh.w;                                                         \
+  if (!w.reserved) w.reserve_for(ln->reserve_items, ln->digest_lane);
 
 
 int coa_queue_submit_verify(coa_queue* q, const uint8_t msg[32], const uint8_t pk[32], const uint8_t sig[64],

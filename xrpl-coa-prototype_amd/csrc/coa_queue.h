@@ -93,7 +93,9 @@ struct Window {
   // collector's take waits for (round 4's streamed C3: 60-310 us per take).
   // Only address space until written (the pages of a large allocation are
   // faulted in on first touch); bare vote batches (rare) grow on demand.
+  bool reserved = false;  // reserve_for ran (capacity is kept across reset())
   void reserve_for(size_t items, bool digest_lane) {
+    reserved = true;
     if (digest_lane) {
       d_data.reserve(items * (512u << 10));  // ~500 KB worker batches
       d_offs.reserve(items + 1);
