@@ -311,7 +311,12 @@ int coa_ed25519_sign_many_device(int device, const uint8_t* d_seeds, const uint8
  * on its own hardware queue, COA_QUEUE_STREAMS) without waiting for the
  * previous window, and its completion thread answers windows in order: the
  * callback runs there with status (COA_OK or a negative engine error) and
- * the request's verdict byte(s).  Windows that read the committee key cache
+ * the request's verdict byte(s).  The requests a window's kernels cannot
+ * decide alone -- certificates with a key outside the registered committee
+ * or with votes that failed their own equation, and bare vote batches -- are
+ * answered later, by the lane's resolver thread (the exact path), so they
+ * never hold back the rest of their window; answers are therefore not in
+ * submission order across requests.  Windows that read the committee key cache
  * pin the generation they launched with; coa_committee_register builds the
  * next generation beside it, so registration neither waits for nor holds
  * back a window and stays verdict-neutral under load. */
