@@ -184,9 +184,17 @@ def test_queue_pipelined_windows_gpu(engine, borrow):
             else:
                 assert got == exp, (kind, got, exp)
         m = q.metrics()
+        q.metrics_reset()
+        m0 = q.metrics()
     assert m["requests"] == len(results) and m["signatures"] == n
     assert m["windows"] > 4 and 2 <= m["max_in_flight"] <= 4  # pipelined over the slots (4 per GPU)
     assert 0 < m["wait_us_p50"] <= m["wait_us_p99"] <= m["wait_us_max"] * 1.1
+    # per-stage time (COA_QSTAGE_*): every stage a window passes through was
+    # timed; certificate 4's foreign key went through the resolver
+    st = m["stage_us"]
+    assert all(st[k] > 0 for k in ("intake", "gather", "pack", "enqueue", "device_wait", "callbacks", "resolve"))
+    assert m["deferred_requests"] >= 1 and m["resolver_passes"] >= 1
+    assert m0["requests"] == 0 and m0["windows"] == 0 and sum(m0["stage_us"].values()) == 0.0
 
 
 @pytest.mark.gpu
