@@ -227,7 +227,9 @@ class HipBackend : public coa_q::Backend {
   // up to 107 K items, p99 wait 8-12 ms).
   void prepare(size_t max_batch) override {
     if (!ready()) return;
-    const size_t items = std::max<size_t>(max_batch, 1024);
+    // capped at 65,536 (a larger max_batch's windows regrow on demand): a
+    // queue made with max_batch 2^20 would otherwise stage ~20 GB of HBM
+    const size_t items = std::min<size_t>(std::max<size_t>(max_batch, 1024), 65536);
     const size_t pre_in = lane_ == coa_q::LANE_DIGEST ? (32u << 20) : items * 160 + (1u << 20);
     const size_t pre_out = lane_ == coa_q::LANE_DIGEST ? (256u << 10) : items * 4 + (64u << 10);
     // workspace for the widest window of each kind (each regrowth is a
