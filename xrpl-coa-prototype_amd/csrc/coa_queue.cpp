@@ -142,6 +142,7 @@ struct Flight {
 struct Deferred {
   std::unique_ptr<Window> w;
   std::vector<Req> reqs;
+  uint32_t shard;  // the window goes back to this shard's pool once answered
 };
 
 inline bool is_deferred(const Req& r, const Window& w) {
@@ -559,6 +560,7 @@ struct Lane {
             if (is_deferred(r, *p.w)) d.reqs.push_back(r);
           ndef += d.reqs.size();
           d.w = std::move(p.w);
+          d.shard = p.shard;
           jobs.push_back(std::move(d));
         }
       }
@@ -648,6 +650,12 @@ struct Lane {
         }
       }
       const int64_t t2 = now_ns();
+      for (Deferred& d : jobs) {  // the answered windows back to their shards' pools
+        d.w->reset();
+        Shard& sh = shards[d.shard];
+        std::lock_guard<std::mutex> g(sh.mu);
+        if (sh.spares.size() < kSpares) sh.spares.push_back(std::move(d.w));
+      }
       l.lock();
       for (int b = 0; b < HB; b++) m_hist[b] += hist[b];
       m_wait_sum += wsum;
