@@ -28,6 +28,12 @@ struct LatArgs {
   // "verify_batch exactness"); items [batch_n, n) are plain verify_strict
   // (one launch can carry a certificate's votes and its header signature)
   uint32_t batch_n;
+  // Certificate::digest inputs (id || round LE || origin, 72 bytes = 18
+  // dwords each), or null.  With them, a prefilter item's record carries the
+  // certificate's index in its first message dword, and its message is
+  // SHA-512(cd_in[index])[..32], hashed in the kernel (the exact certificate
+  // path no longer needs a digest launch and a host round trip first)
+  const uint32_t* cd_in;
 };
 
 // One 256-thread workgroup (four waves) per signature.

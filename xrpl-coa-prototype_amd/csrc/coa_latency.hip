@@ -187,6 +187,24 @@ COA_DEV void horner(ge_p3& out, const uint32_t* tab, const uint32_t* rec, int H,
 // synchronisation (one PCIe write per signature).  The word is the whole
 // message, so the store is relaxed: a release would first write back the L2
 // (buffer_wbl2) for data nobody reads.
+// A prefilter item of a certificate (LatArgs::cd_in): its message becomes
+// Certificate::digest = SHA-512(id || round || origin)[..32] of the
+// certificate whose index the record's first message dword holds.  Called by
+// the wave that hashes k = H(R || A || M), before it does.
+COA_DEV void cert_msg(const LatArgs& a, uint32_t item, uint32_t* msg) {
+  if (!a.cd_in || item >= a.batch_n) return;
+  const uint32_t* src = a.cd_in + (uint64_t)coa_sha::uni(msg[0]) * 18;
+  uint32_t in[18];  // 72-byte records: 8-byte aligned only, so dword loads
+#pragma unroll
+  for (int i = 0; i < 18; i++) in[i] = coa_sha::uni(src[i]);
+  uint64_t st[8];
+  uint32_t h[16];
+  coa_sha::hash_words<18>(st, in);
+  coa_sha::state_to_le_words(h, st);
+#pragma unroll
+  for (int i = 0; i < 8; i++) msg[i] = h[i];
+}
+
 COA_DEV void publish(const LatArgs& a, uint32_t item, bool ok) {
   __hip_atomic_store(a.res + item, (a.tag << 8) | (ok ? 0u : 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -289,8 +307,11 @@ COA_DEV void uncached_batch(const LatArgs& a, uint32_t item, uint32_t wave, uint
   if (threadIdx.x < 4) s_flag[threadIdx.x] = 0;
   __syncthreads();
   if (wave == 0) {
-    uint32_t e[8];
-    halve_item(sh_rec, s_meta, e, msg, pk, rw, sw, lane);
+    uint32_t e[8], m[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) m[i] = msg[i];
+    cert_msg(a, item, m);
+    halve_item(sh_rec, s_meta, e, m, pk, rw, sw, lane);
     if (lane == 0) flag_set(&s_flag[0]);
     ge_p3 E;
     comb_butterfly(E, e, a.comb, lane);
@@ -416,6 +437,7 @@ __global__ void __launch_bounds__(256) k_verify_lat(LatArgs a) {
     } else if (wave == 0) {
       uint64_t st[8];
       uint32_t h[16], w[24];
+      cert_msg(a, item, msg);
 #pragma unroll
       for (int i = 0; i < 8; i++) {
         w[i] = rw[i];

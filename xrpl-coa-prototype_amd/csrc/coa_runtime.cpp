@@ -723,8 +723,11 @@ int lat_res_wait(Dev& d, hipStream_t s, size_t n, uint32_t tag, uint32_t* out) {
 
 // msg_of: item i's message is msgs + msg_of[i] * 32 (null: item i's own).
 // batch_n: items [0, batch_n) take the verify_batch prefilter (LatArgs::batch_n).
+// cd_in / n_cd: Certificate::digest inputs (72 bytes each, LatArgs::cd_in);
+// a prefilter item's message is then its certificate's index (first dword).
 int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs, size_t n, uint8_t* out,
-               const uint32_t* msg_of = nullptr, size_t batch_n = 0) {
+               const uint32_t* msg_of = nullptr, size_t batch_n = 0, const uint8_t* cd_in = nullptr,
+               size_t n_cd = 0) {
   uint32_t tag = 0;
   int rc = lat_res_prepare(d, n, tag);
   if (rc != COA_OK) return rc;
@@ -740,8 +743,12 @@ int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* s
     std::memcpy(&a.inl[i][8], pks + i * 32, 32);
     std::memcpy(&a.inl[i][16], sigs + i * 64, 64);
   }
-  if (n > COA_LAT_INLINE) {  // the rest through one pinned staging buffer and one H2D
-    const size_t in_bytes = n * 128;
+  // the records past the inline ones, then the certificate digest inputs,
+  // through one pinned staging buffer and one H2D
+  const size_t rec_end = n > COA_LAT_INLINE ? n * 128 : 0;
+  const size_t cd_off = align_up(std::max<size_t>(rec_end, COA_LAT_INLINE * 128), 256);
+  const size_t in_bytes = n_cd ? cd_off + n_cd * 72 : rec_end;
+  if (in_bytes) {
     HIP_TRY(d.pin.ensure(in_bytes));
     HIP_TRY(d.lat.ensure(in_bytes));
     uint8_t* h = static_cast<uint8_t*>(d.pin.p);
@@ -750,9 +757,11 @@ int lat_verify(Dev& d, const uint8_t* msgs, const uint8_t* pks, const uint8_t* s
       std::memcpy(h + i * 128 + 32, pks + i * 32, 32);
       std::memcpy(h + i * 128 + 64, sigs + i * 64, 64);
     }
-    HIP_TRY(hipMemcpyAsync(d.lat.as<uint8_t>() + COA_LAT_INLINE * 128, h + COA_LAT_INLINE * 128,
-                           in_bytes - COA_LAT_INLINE * 128, hipMemcpyHostToDevice, s));
+    if (n_cd) std::memcpy(h + cd_off, cd_in, n_cd * 72);
+    const size_t from = rec_end ? (size_t)COA_LAT_INLINE * 128 : cd_off;
+    HIP_TRY(hipMemcpyAsync(d.lat.as<uint8_t>() + from, h + from, in_bytes - from, hipMemcpyHostToDevice, s));
     a.in = d.lat.as<uint32_t>();
+    if (n_cd) a.cd_in = reinterpret_cast<const uint32_t*>(d.lat.as<uint8_t>() + cd_off);
   }
   a.tag = tag;
   a.res = d.lat_res;
@@ -1446,23 +1455,31 @@ int cert_resolve(const CertIn& in, const std::vector<size_t>& idx, bool hdr_too,
   if (idx.empty()) return COA_OK;
   const size_t m = idx.size();
   // Certificate::digest inputs: id || round LE || origin (72 B)
-  std::vector<uint8_t> cin(m * 72), dig(m * 64);
-  std::vector<uint64_t> coff(m + 1);
+  std::vector<uint8_t> cin(m * 72);
   for (size_t j = 0; j < m; j++) {
     const size_t c = idx[j];
     std::memcpy(&cin[j * 72], in.ids + c * 32, 32);
     std::memcpy(&cin[j * 72 + 32], &in.rounds[c], 8);
     std::memcpy(&cin[j * 72 + 40], in.origins + c * 32, 32);
-    coff[j] = j * 72;
   }
-  coff[m] = m * 72;
-  int rc = coa_sha512_many(cin.data(), coff.data(), m, dig.data());
-  if (rc != COA_OK) return rc;
+  // the digests of certificates `sel` (indices into idx) into gm
   std::vector<uint8_t> gm(m * 32), gv(m), vp, vs;
+  auto digests = [&](const std::vector<size_t>& sel) -> int {
+    if (sel.empty()) return COA_OK;
+    std::vector<uint8_t> sin(sel.size() * 72), dig(sel.size() * 64);
+    std::vector<uint64_t> soff(sel.size() + 1);
+    for (size_t k = 0; k < sel.size(); k++) {
+      std::memcpy(&sin[k * 72], &cin[sel[k] * 72], 72);
+      soff[k] = k * 72;
+    }
+    soff[sel.size()] = sel.size() * 72;
+    const int r = coa_sha512_many(sin.data(), soff.data(), sel.size(), dig.data());
+    for (size_t k = 0; r == COA_OK && k < sel.size(); k++) std::memcpy(&gm[sel[k] * 32], &dig[k * 64], 32);
+    return r;
+  };
   std::vector<uint64_t> goff(m + 1, 0);
   for (size_t j = 0; j < m; j++) {
     const size_t c = idx[j];
-    std::memcpy(&gm[j * 32], &dig[j * 64], 32);
     const uint64_t a = in.voff[c], b = in.voff[c + 1];
     vp.insert(vp.end(), in.vpks + a * 32, in.vpks + b * 32);
     vs.insert(vs.end(), in.vsigs + a * 64, in.vsigs + b * 64);
@@ -1470,14 +1487,19 @@ int cert_resolve(const CertIn& in, const std::vector<size_t>& idx, bool hdr_too,
   }
   std::vector<uint8_t> hv(m, 0);
   const size_t nvotes = goff[m];
+  int rc;
   if (hdr_too && nvotes + m <= lat_max() && !env_is("COA_BATCH_LAT", "0") && !env_is("COA_RESOLVE_ONE_LAUNCH", "0")) {
     // ONE latency launch for the votes (the verify_batch prefilter: items
-    // [0, nvotes)) and the header signatures (plain verify_strict: items
-    // [nvotes, nvotes + m)): a certificate with keys outside the committee
-    // took a prefilter launch and then a header launch, one after the other
-    std::vector<uint8_t> msgs(gm), pks(vp), sigs(vs);
+    // [0, nvotes), each message Certificate::digest hashed in the kernel from
+    // cin, LatArgs::cd_in) and the header signatures (plain verify_strict:
+    // items [nvotes, nvotes + m)): a certificate with keys outside the
+    // committee took a digest launch, a prefilter launch and a header launch,
+    // one after the other
+    std::vector<uint8_t> msgs(m * 32, 0), pks(vp), sigs(vs);
     std::vector<uint32_t> msg_of(nvotes + m);
     for (size_t j = 0; j < m; j++) {
+      const uint32_t jj = (uint32_t)j;
+      std::memcpy(&msgs[j * 32], &jj, 4);  // the certificate's index: its digest input in cin
       for (uint64_t i = goff[j]; i < goff[j + 1]; i++) msg_of[i] = (uint32_t)j;
       msg_of[nvotes + j] = (uint32_t)(m + j);
       const size_t c = idx[j];
@@ -1490,7 +1512,8 @@ int cert_resolve(const CertIn& in, const std::vector<size_t>& idx, bool hdr_too,
       std::unique_lock<std::mutex> l;
       Dev& d = lat_dev(l);
       HIP_TRY(hipSetDevice(d.id));
-      rc = lat_verify(d, msgs.data(), pks.data(), sigs.data(), nvotes + m, v.data(), msg_of.data(), nvotes);
+      rc = lat_verify(d, msgs.data(), pks.data(), sigs.data(), nvotes + m, v.data(), msg_of.data(), nvotes,
+                      cin.data(), m);
       if (rc != COA_OK) return rc;
     }
     // a group every vote of which passed is Ok for every z; the others take
@@ -1503,6 +1526,8 @@ int cert_resolve(const CertIn& in, const std::vector<size_t>& idx, bool hdr_too,
       if (!pass) open.push_back(j);
       hv[j] = v[nvotes + j] ? 1 : 0;
     }
+    rc = digests(open);  // only the groups the prefilter did not accept need their digest on the host
+    if (rc != COA_OK) return rc;
     for (size_t j : open) {
       const uint64_t a = goff[j], n = goff[j + 1] - a;
       const uint64_t offs[2] = {0, n};
@@ -1514,6 +1539,10 @@ int cert_resolve(const CertIn& in, const std::vector<size_t>& idx, bool hdr_too,
       status[idx[j]] |= (gv[j] ? COA_CST_BAD_VOTES : 0u) | (hv[j] ? COA_CST_BAD_HEADER_SIG : 0u);
     return COA_OK;
   }
+  std::vector<size_t> all(m);
+  for (size_t j = 0; j < m; j++) all[j] = j;
+  rc = digests(all);
+  if (rc != COA_OK) return rc;
   rc = batch_groups_impl(gm.data(), vp.data(), vs.data(), goff.data(), m, nullptr, seed, gv.data());
   if (rc != COA_OK) return rc;
   if (hdr_too) {
