@@ -16,6 +16,8 @@
 //    4 mul_u32_u24  5 mul_hi_u32_u24  6 mad_u32_u24  7 add_u32  8 fma_f64
 //    10/11/12 mad_u64 + 1/2/3 independent adds  13 lshl_add_u64
 //    14 lshrrev_b64  15 add_co+addc pairs  16 add3_u32
+//    17 alignbit_b32  18 bitop3_b32  19 mov_b32_dpp quad_perm  20 and_b32
+//    (17-20: the SHA-512 lane-pair round's instruction classes, round 5)
 template <int V>
 __global__ void k(uint64_t* out, uint32_t a0, int n) {
   uint64_t acc[C];
@@ -46,6 +48,10 @@ __global__ void k(uint64_t* out, uint32_t a0, int n) {
       if constexpr (V == 13) asm volatile("v_lshl_add_u64 %0, %0, 0, %10\n\tv_lshl_add_u64 %1, %1, 0, %10\n\tv_lshl_add_u64 %2, %2, 0, %10\n\tv_lshl_add_u64 %3, %3, 0, %10\n\tv_lshl_add_u64 %4, %4, 0, %10\n\tv_lshl_add_u64 %5, %5, 0, %10\n\tv_lshl_add_u64 %6, %6, 0, %10\n\tv_lshl_add_u64 %7, %7, 0, %10" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]), "+v"(acc[7]) : "v"(a), "v"(b), "v"(wb), "v"(wb) : "vcc", "s20", "s21");
       if constexpr (V == 14) asm volatile("v_lshrrev_b64 %0, 1, %0\n\tv_lshrrev_b64 %1, 1, %1\n\tv_lshrrev_b64 %2, 1, %2\n\tv_lshrrev_b64 %3, 1, %3\n\tv_lshrrev_b64 %4, 1, %4\n\tv_lshrrev_b64 %5, 1, %5\n\tv_lshrrev_b64 %6, 1, %6\n\tv_lshrrev_b64 %7, 1, %7" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]), "+v"(acc[7]) : "v"(a), "v"(b), "v"(wb), "v"(wb) : "vcc", "s20", "s21");
       if constexpr (V == 16) asm volatile("v_add3_u32 %0, %0, %8, %9\n\tv_add3_u32 %1, %1, %8, %9\n\tv_add3_u32 %2, %2, %8, %9\n\tv_add3_u32 %3, %3, %8, %9\n\tv_add3_u32 %4, %4, %8, %9\n\tv_add3_u32 %5, %5, %8, %9\n\tv_add3_u32 %6, %6, %8, %9\n\tv_add3_u32 %7, %7, %8, %9" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7]) : "v"(a), "v"(b), "v"(wb), "v"(wb) : "vcc", "s20", "s21");
+      if constexpr (V == 17) asm volatile("v_alignbit_b32 %0, %0, %9, %8\n\tv_alignbit_b32 %1, %1, %9, %8\n\tv_alignbit_b32 %2, %2, %9, %8\n\tv_alignbit_b32 %3, %3, %9, %8\n\tv_alignbit_b32 %4, %4, %9, %8\n\tv_alignbit_b32 %5, %5, %9, %8\n\tv_alignbit_b32 %6, %6, %9, %8\n\tv_alignbit_b32 %7, %7, %9, %8" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7]) : "v"(a), "v"(b), "v"(wb), "v"(wb) : "vcc", "s20", "s21");
+      if constexpr (V == 18) asm volatile("v_bitop3_b32 %0, %0, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %2, %2, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %3, %3, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %4, %4, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %5, %5, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %6, %6, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %7, %7, %8, %9 bitop3:0x96" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7]) : "v"(a), "v"(b), "v"(wb), "v"(wb) : "vcc", "s20", "s21");
+      if constexpr (V == 19) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %2, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %3, %3 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %4, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %5, %5 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %6, %6 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %7, %7 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7]) : "v"(a), "v"(b), "v"(wb), "v"(wb) : "vcc", "s20", "s21");
+      if constexpr (V == 20) asm volatile("v_and_b32 %0, %0, %9\n\tv_and_b32 %1, %1, %9\n\tv_and_b32 %2, %2, %9\n\tv_and_b32 %3, %3, %9\n\tv_and_b32 %4, %4, %9\n\tv_and_b32 %5, %5, %9\n\tv_and_b32 %6, %6, %9\n\tv_and_b32 %7, %7, %9" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7]) : "v"(a), "v"(b), "v"(wb), "v"(wb) : "vcc", "s20", "s21");
       if constexpr (V == 10) asm volatile("v_mad_u64_u32 %0, s[20:21], %16, %17, %0\n\tv_add_u32 %8, %8, %17\n\tv_mad_u64_u32 %1, s[20:21], %16, %17, %1\n\tv_add_u32 %9, %9, %17\n\tv_mad_u64_u32 %2, s[20:21], %16, %17, %2\n\tv_add_u32 %10, %10, %17\n\tv_mad_u64_u32 %3, s[20:21], %16, %17, %3\n\tv_add_u32 %11, %11, %17\n\tv_mad_u64_u32 %4, s[20:21], %16, %17, %4\n\tv_add_u32 %12, %12, %17\n\tv_mad_u64_u32 %5, s[20:21], %16, %17, %5\n\tv_add_u32 %13, %13, %17\n\tv_mad_u64_u32 %6, s[20:21], %16, %17, %6\n\tv_add_u32 %14, %14, %17\n\tv_mad_u64_u32 %7, s[20:21], %16, %17, %7\n\tv_add_u32 %15, %15, %17" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]), "+v"(acc[7]), "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7]) : "v"(a), "v"(b) : "s20", "s21");
       if constexpr (V == 11) asm volatile("v_mad_u64_u32 %0, s[20:21], %16, %17, %0\n\tv_add_u32 %8, %8, %17\n\tv_add_u32 %9, %9, %17\n\tv_mad_u64_u32 %1, s[20:21], %16, %17, %1\n\tv_add_u32 %9, %9, %17\n\tv_add_u32 %10, %10, %17\n\tv_mad_u64_u32 %2, s[20:21], %16, %17, %2\n\tv_add_u32 %10, %10, %17\n\tv_add_u32 %11, %11, %17\n\tv_mad_u64_u32 %3, s[20:21], %16, %17, %3\n\tv_add_u32 %11, %11, %17\n\tv_add_u32 %12, %12, %17\n\tv_mad_u64_u32 %4, s[20:21], %16, %17, %4\n\tv_add_u32 %12, %12, %17\n\tv_add_u32 %13, %13, %17\n\tv_mad_u64_u32 %5, s[20:21], %16, %17, %5\n\tv_add_u32 %13, %13, %17\n\tv_add_u32 %14, %14, %17\n\tv_mad_u64_u32 %6, s[20:21], %16, %17, %6\n\tv_add_u32 %14, %14, %17\n\tv_add_u32 %15, %15, %17\n\tv_mad_u64_u32 %7, s[20:21], %16, %17, %7\n\tv_add_u32 %15, %15, %17\n\tv_add_u32 %8, %8, %17" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]), "+v"(acc[7]), "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7]) : "v"(a), "v"(b) : "s20", "s21");
       if constexpr (V == 12) asm volatile("v_mad_u64_u32 %0, s[20:21], %16, %17, %0\n\tv_add_u32 %8, %8, %17\n\tv_add_u32 %9, %9, %17\n\tv_add_u32 %10, %10, %17\n\tv_mad_u64_u32 %1, s[20:21], %16, %17, %1\n\tv_add_u32 %9, %9, %17\n\tv_add_u32 %10, %10, %17\n\tv_add_u32 %11, %11, %17\n\tv_mad_u64_u32 %2, s[20:21], %16, %17, %2\n\tv_add_u32 %10, %10, %17\n\tv_add_u32 %11, %11, %17\n\tv_add_u32 %12, %12, %17\n\tv_mad_u64_u32 %3, s[20:21], %16, %17, %3\n\tv_add_u32 %11, %11, %17\n\tv_add_u32 %12, %12, %17\n\tv_add_u32 %13, %13, %17\n\tv_mad_u64_u32 %4, s[20:21], %16, %17, %4\n\tv_add_u32 %12, %12, %17\n\tv_add_u32 %13, %13, %17\n\tv_add_u32 %14, %14, %17\n\tv_mad_u64_u32 %5, s[20:21], %16, %17, %5\n\tv_add_u32 %13, %13, %17\n\tv_add_u32 %14, %14, %17\n\tv_add_u32 %15, %15, %17\n\tv_mad_u64_u32 %6, s[20:21], %16, %17, %6\n\tv_add_u32 %14, %14, %17\n\tv_add_u32 %15, %15, %17\n\tv_add_u32 %8, %8, %17\n\tv_mad_u64_u32 %7, s[20:21], %16, %17, %7\n\tv_add_u32 %15, %15, %17\n\tv_add_u32 %8, %8, %17\n\tv_add_u32 %9, %9, %17" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]), "+v"(acc[7]), "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7]) : "v"(a), "v"(b) : "s20", "s21");
@@ -100,5 +106,9 @@ int main() {
   run<14>(d, "v_lshrrev_b64", 1);
   run<15>(d, "v_add_co + v_addc (pair)", 2);
   run<16>(d, "v_add3_u32", 1);
+  run<17>(d, "v_alignbit_b32", 1);
+  run<18>(d, "v_bitop3_b32", 1);
+  run<19>(d, "v_mov_b32_dpp quad_perm", 1);
+  run<20>(d, "v_and_b32", 1);
   return 0;
 }
