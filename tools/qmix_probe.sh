@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out/qmix
+for i in 1 2 3; do
+  COA_QUEUE_TRACE_SLOW_US=3000 timeout -k 10 240 python bench.py --no-cpu-baseline --sections c4_stream,queue_round_mix > gpurun_out/qmix/run$i.json 2> gpurun_out/qmix/run$i.err || exit 1
+  echo "run $i done"
+done
