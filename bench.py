@@ -663,7 +663,10 @@ def paced_queue(arrive_s, kind, item, vm=None, vp=None, vs=None, vexp=None, cert
     """One paced run through the aggregation queue (tools/latc.c latc_paced):
     requests arrive at arrive_s (seconds), each answer is checked against its
     expectation; returns the latencies (ms, from the scheduled arrival to the
-    callback), the wall time and the queue metrics."""
+    callback), the wall time and the queue metrics.  The queue is new for
+    each run and first answers the schedule's first 64 requests, untimed
+    (round 5: a node creates its queue once; the metrics cover the paced
+    run only)."""
     import ctypes
 
     import numpy as np

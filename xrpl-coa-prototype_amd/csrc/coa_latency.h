@@ -42,10 +42,17 @@ hipError_t coa_launch_verify_lat(const LatArgs& a, hipStream_t s);
 // The latency kernel over device-resident inputs, enqueued on `stream`
 // (coa_runtime.cpp; the aggregation queue's small signature windows):
 // d_in [n][128 B] = msg | pk | R | s, d_res [n] words (1 << 8) | verdict.
-// Reads device `device`'s committee key cache: the caller holds that
-// device's key-cache read gate (coa_committee.h) until the kernel has run.
-// Returns COA_OK or a negative COA_E*.
+// Reads device `device`'s committee key cache: the generation the calling
+// thread pinned (coa_keycache_use, held until the kernel has run), else the
+// current one.  Returns COA_OK or a negative COA_E*.
 extern "C" int coa_lat_verify_device(int device, const uint8_t* d_in, size_t n, uint32_t* d_res, void* stream);
+// The same for n <= COA_LAT_INLINE records in host memory, passed in the
+// kernel arguments (no host-to-device copy), the result words
+// (tag << 8) | verdict written straight into `res` (page-locked host memory
+// the caller polls for `tag`, nonzero; no device-to-host copy): the queue's
+// windows of a few signatures (coa_queue_hip.cpp).
+extern "C" int coa_lat_verify_inline(int device, const uint8_t* h_records, size_t n, uint32_t* res, uint32_t tag,
+                                     void* stream);
 // Calls of at most this many signatures (32-byte messages) take the latency
 // kernel (COA_LAT_MAX, default 2048).
 extern "C" size_t coa_lat_max(void);

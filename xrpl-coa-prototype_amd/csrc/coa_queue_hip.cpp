@@ -98,6 +98,12 @@ struct Slot {
   bool launched = false;  // device work was enqueued (complete() must drain it)
   void* keys = nullptr;   // the key-cache generation the launch pinned (coa_keycache_pin)
   bool lat = false;       // the launch's signatures took the latency kernel (result words)
+  // a window of at most COA_LAT_INLINE signatures and nothing else: records in
+  // the kernel arguments, verdict words straight into lres (page-locked,
+  // coherent), which complete() polls for ltag -- no copies, no event wait
+  bool inl = false;
+  uint32_t* lres = nullptr;
+  uint32_t ltag = 0;
   // output offsets of the current launch
   size_t o_v = 0, o_c = 0, o_d = 0;
 };
@@ -191,6 +197,7 @@ void free_slot(Slot& sl) {
   if (sl.din) (void)hipFree(sl.din);
   if (sl.dout) (void)hipFree(sl.dout);
   if (sl.ws) (void)hipFree(sl.ws);
+  if (sl.lres) (void)hipHostFree(sl.lres);
   if (sl.ev) (void)hipEventDestroy(sl.ev);
   if (sl.s) (void)hipStreamDestroy(sl.s);
   bury(sl.grave);
@@ -240,6 +247,7 @@ class HipBackend : public coa_q::Backend {
                               : std::max(coa_verify_workspace_bytes(items),
                                          coa_certificate_workspace_bytes(items / 68 + 1, items)) + 256;
     for (Slot& sl : slots_) {
+      if (lane_ == coa_q::LANE_VERIFY && hipSetDevice(sl.dev) == hipSuccess) (void)lat_words(sl);
       if (hipSetDevice(sl.dev) != hipSuccess || grow_pinned(sl.hin, sl.cap_hin, pre_in, sl.grave) != hipSuccess ||
           grow_pinned(sl.hout, sl.cap_hout, pre_out, sl.grave) != hipSuccess ||
           grow_dev(sl.din, sl.cap_din, pre_in, sl.grave) != hipSuccess ||
@@ -253,6 +261,19 @@ class HipBackend : public coa_q::Backend {
     (void)hipGetLastError();
   }
   int stream_kind() const override { return kind_; }
+
+  // The slot's page-locked result words for inline latency windows
+  // (allocated once; null when the allocation failed: such windows then take
+  // the staged path)
+  static uint32_t* lat_words(Slot& sl) {
+    if (!sl.lres &&
+        hipHostMalloc(reinterpret_cast<void**>(&sl.lres), COA_LAT_INLINE * sizeof(uint32_t), hipHostMallocCoherent) !=
+            hipSuccess) {
+      sl.lres = nullptr;
+      (void)hipGetLastError();
+    }
+    return sl.lres;
+  }
 
   void launch(coa_q::Launch& L) override {
     if (!ready()) {
@@ -345,6 +366,8 @@ class HipBackend : public coa_q::Backend {
       if (v >= 1 && v <= 8) per = (size_t)v;
     }
     if (const char* e = getenv("COA_QUEUE_FAULT")) fault_every_ = strtoull(e, nullptr, 10);
+    // COA_QUEUE_INLINE=0: small signature windows take the staged path too (A/B)
+    if (const char* e = getenv("COA_QUEUE_INLINE")) inline_ok_ = e[0] != '0';
     kind_ = stream_kind_env();
     slots_.resize(per * devs_.size());
     // (page-locked staging is sized by prepare(): a reallocation on the
@@ -474,6 +497,25 @@ class HipBackend : public coa_q::Backend {
       std::chrono::steady_clock::time_point t;
       ~EnqClock() { L.stage_ns[COA_QSTAGE_ENQUEUE] += ns_between(t, std::chrono::steady_clock::now()); }
     } enq_clock{L, t_enq};
+    sl.inl = inline_ok_ && sl.lat && L.nv <= COA_LAT_INLINE && L.nc == 0 && L.nd == 0 && lat_words(sl) != nullptr;
+    if (sl.inl) {
+      // a few signatures alone (Header::verify / Vote::verify at low load):
+      // the packed records go in the kernel arguments and the verdict words
+      // come back by the kernel's own stores, as coa_ed25519_verify_strict
+      // does -- the staged path's two copies (and the event wait) were most
+      // of such a window's time besides the kernel
+      std::memset(sl.lres, 0, L.nv * sizeof(uint32_t));  // no tag matches 0
+      sl.ltag = (sl.ltag + 1) & 0xffffffu;
+      if (sl.ltag == 0) sl.ltag = 1;
+      sl.launched = true;
+      if (inject) return COA_EHIP;  // fault injection: nothing launched
+      if (!sl.keys) sl.keys = coa_keycache_pin(sl.dev);
+      coa_keycache_use(sl.keys);
+      const int rc = coa_lat_verify_inline(sl.dev, h + i_vm, L.nv, sl.lres, sl.ltag, sl.s);
+      coa_keycache_use(nullptr);
+      if (rc != COA_OK) return rc;
+      return hipEventRecord(sl.ev, sl.s) == hipSuccess ? COA_OK : COA_EHIP;
+    }
     uint8_t* d = static_cast<uint8_t*>(sl.din);
     uint8_t* dout = static_cast<uint8_t*>(sl.dout);
     if (hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, sl.s) != hipSuccess) return COA_EHIP;
@@ -514,7 +556,9 @@ class HipBackend : public coa_q::Backend {
     const auto t_wait = std::chrono::steady_clock::now();
     if (sl.launched) {
       (void)hipSetDevice(sl.dev);
-      if (L.rc == COA_OK) {
+      if (L.rc == COA_OK && sl.inl) {
+        L.rc = poll_words(sl, L.nv);
+      } else if (L.rc == COA_OK) {
         if (hipEventSynchronize(sl.ev) != hipSuccess) L.rc = COA_EHIP;
       } else {
         (void)hipStreamSynchronize(sl.s);  // nothing may still read the staging when the slot is reused
@@ -528,7 +572,7 @@ class HipBackend : public coa_q::Backend {
       size_t v = 0, c = 0, dn = 0;
       for (coa_q::Window* w : L.parts) {
         if (w->nv && sl.lat) {
-          const uint32_t* words = reinterpret_cast<const uint32_t*>(h + sl.o_v) + v;
+          const uint32_t* words = (sl.inl ? sl.lres : reinterpret_cast<const uint32_t*>(h + sl.o_v)) + v;
           for (size_t i = 0; i < w->nv; i++) w->v_out[i] = (uint8_t)(words[i] & 0xffu);
         } else if (w->nv) {
           std::memcpy(w->v_out.data(), h + sl.o_v + v, w->nv);
@@ -546,6 +590,27 @@ class HipBackend : public coa_q::Backend {
       sl.keys = nullptr;
     }
     L.stage_ns[COA_QSTAGE_SCATTER] += ns_between(t_scatter, std::chrono::steady_clock::now());
+  }
+
+  // An inline latency window's n result words, polled for the slot's tag.
+  // A kernel that ended without publishing (a fault) ends the wait through
+  // the slot's event; a bound stops a hang.  On failure the stream is
+  // drained before the slot is reused.
+  static int poll_words(Slot& sl, size_t n) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (size_t i = 0; i < n; i++) {
+      const volatile uint32_t* w = sl.lres + i;
+      for (uint64_t spin = 0; (*w >> 8) != sl.ltag; spin++) {
+        if ((spin & 1023) != 1023) continue;
+        const hipError_t q = hipEventQuery(sl.ev);
+        const bool stuck = std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10);
+        if ((q != hipSuccess && q != hipErrorNotReady) || (q == hipSuccess && (*w >> 8) != sl.ltag) || stuck) {
+          (void)hipStreamSynchronize(sl.s);
+          return COA_EHIP;
+        }
+      }
+    }
+    return COA_OK;
   }
 
   // Raw certificate status words -> COA_CERT_* bits; the certificates the
@@ -630,6 +695,7 @@ class HipBackend : public coa_q::Backend {
   bool inited_ = false;
   int init_rc_ = COA_OK;
   unsigned long long fault_every_ = 0, launches_ = 0;
+  bool inline_ok_ = true;  // COA_QUEUE_INLINE
 };
 
 }  // namespace

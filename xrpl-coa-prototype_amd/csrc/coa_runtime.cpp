@@ -2244,6 +2244,31 @@ int coa_lat_verify_device(int device, const uint8_t* d_in, size_t n, uint32_t* d
   return COA_OK;
 }
 
+int coa_lat_verify_inline(int device, const uint8_t* h_records, size_t n, uint32_t* res, uint32_t tag, void* stream) {
+  const int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  if (n == 0) return COA_OK;
+  if (!h_records || !res || tag == 0) return fail(COA_EINVAL, "null argument or zero tag");
+  if (n > COA_LAT_INLINE) return fail(COA_EINVAL, "more records than the kernel arguments hold");
+  Dev* d = dev_by_id(device);
+  if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
+  HIP_TRY(hipSetDevice(device));
+  LatArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.n = a.n_inline = (uint32_t)n;
+  std::memcpy(a.inl, h_records, n * 128);  // msg | pk | R | s, as the device records
+  a.res = res;
+  a.tag = tag;
+  const KeySetP ks = keys_now(*d);  // pinned (the queue) or current; see coa_lat_verify_device
+  a.keys = ks->ckeys.as<uint32_t>();
+  a.kflags = ks->kflags.as<uint32_t>();
+  a.ktabs = ks->ktabs.as<uint32_t>();
+  a.nk = ks->nkeys;
+  a.comb = d->comb;
+  HIP_TRY(coa_launch_verify_lat(a, stream ? (hipStream_t)stream : d->stream));
+  return COA_OK;
+}
+
 int coa_engine_recoveries(uint64_t* contexts_rebuilt, uint64_t* shards_rerun) {
   if (contexts_rebuilt) *contexts_rebuilt = g_ctx_rebuilt.load();
   if (shards_rerun) *shards_rerun = g_shards_rerun.load();
