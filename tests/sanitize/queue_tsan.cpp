@@ -131,6 +131,7 @@ coa_q::Backend* coa_q::make_backend(int) { return new StubBackend(); }
 struct Req {
   uint8_t expect[32];
   size_t n_expect;
+  std::vector<uint8_t> hold;  // a borrowed certificate's bytes, valid until the end of the run
   std::atomic<int> done{0};
   std::atomic<int> bad{0};
 };
@@ -185,8 +186,24 @@ int main(int argc, char** argv) {
             std::vector<uint8_t> hdr(rng() % 100), pks(nv * 32 + 1, 3), sigs(nv * 64 + 1, 4);
             r.n_expect = 1;
             r.expect[0] = v_cert(a, nv);
-            rc = coa_queue_submit_certificate(q, hdr.data(), hdr.size(), a, c, b, 9, pks.data(), sigs.data(), nv,
-                                              check_cb, &r);
+            if (rng() % 2) {
+              rc = coa_queue_submit_certificate(q, hdr.data(), hdr.size(), a, c, b, 9, pks.data(), sigs.data(), nv,
+                                                check_cb, &r);
+            } else {  // borrowed: the queue reads the caller's arrays until the callback
+              r.hold.resize(32 + 32 + 64 + hdr.size() + nv * 96);
+              uint8_t* h = r.hold.data();
+              auto put = [](uint8_t* d, const uint8_t* src, size_t len) {
+                if (len) std::memcpy(d, src, len);
+              };
+              put(h, a, 32);
+              put(h + 32, c, 32);
+              put(h + 64, b, 64);
+              put(h + 128, hdr.data(), hdr.size());
+              put(h + 128 + hdr.size(), pks.data(), nv * 32);
+              put(h + 128 + hdr.size() + nv * 32, sigs.data(), nv * 64);
+              rc = coa_queue_submit_certificate_borrowed(q, h + 128, hdr.size(), h, h + 32, h + 64, 9, h + 128 + hdr.size(),
+                                                         h + 128 + hdr.size() + nv * 32, nv, check_cb, &r);
+            }
             break;
           }
           default: {
