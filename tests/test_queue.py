@@ -85,6 +85,32 @@ def test_queue_verdicts_gpu(engine):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("inline", ["1", "0"])
+def test_queue_small_signature_windows_gpu(engine, monkeypatch, inline):
+    """Windows of at most 16 signatures and nothing else take the latency
+    kernel with the records in its arguments and the verdict words polled
+    from page-locked memory (coa_queue_hip.cpp, coa_lat_verify_inline);
+    COA_QUEUE_INLINE=0 stages them like larger windows.  Every golden vector
+    (canonical, non-canonical, small-order, mixed-order...) in windows of
+    1..16, both ways, gives the oracle's verdict."""
+    monkeypatch.setenv("COA_QUEUE_INLINE", inline)
+    vecs = [v for v in load_golden("verify_vectors.json") if len(v["msg"]) == 64]
+    with engine.AggregationQueue(max_batch=4096, max_delay_us=2_000_000) as q:
+        i, size = 0, 1
+        while i < len(vecs):
+            part = vecs[i:i + size]
+            futs = [(q.submit_verify(bytes.fromhex(v["msg"]), bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"])),
+                     v["expect"]) for v in part]
+            q.flush()
+            for f, exp in futs:
+                assert f.result(timeout=30) == exp
+            i += size
+            size = size % 16 + 1
+        m = q.metrics()
+    assert m["windows"] >= 2 and m["failed_windows"] == 0
+
+
+@pytest.mark.gpu
 def test_queue_certificates_and_digests_gpu(engine):
     """Whole certificates (fused Certificate::verify crypto) and worker batch
     digests through the queue: one coalesced launch each, results equal the
