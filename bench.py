@@ -711,6 +711,9 @@ def queue_diag(met):
     the longest wait for a free slot, staging reallocations, and how the
     slots' streams were made."""
     return {"window_ms_max": round(met["window_us_max"] * 1e-3, 3), "window_max_items": int(met["window_max_items"]),
+            # when the slowest window was launched (ms into the run) and its device wait
+            "window_max_at_ms": round(met["window_max_at_ms"], 2),
+            "window_max_device_ms": round(met["window_max_device_us"] * 1e-3, 3),
             "window_max_kinds": [n for b, n in KIND_BITS if met["window_max_kinds"] & b],
             "slot_wait_ms_max": round(met["slot_wait_us_max"] * 1e-3, 3), "staging_grows": int(met["staging_grows"]),
             "max_in_flight": int(met["max_in_flight"]), "slots": [int(met["slots_verify"]), int(met["slots_digest"])],

@@ -412,6 +412,13 @@ typedef struct {
   /* Where the time goes, summed over every window (microseconds, COA_QSTAGE_*
    * indices; divide by `windows` for a mean per window). */
   double stage_us[12];
+  /* When the slowest window (window_us_max) was launched, in milliseconds
+   * since the queue's creation or its last coa_queue_metrics_reset, and how
+   * much of it was spent waiting for its device work (COA_QSTAGE_DEVICE_WAIT):
+   * a one-off tail at a run's start points at set-up costs, one in the
+   * device wait at the device. */
+  double window_max_at_ms;
+  double window_max_device_us;
 } coa_queue_metrics_t;
 #define COA_QSTAGE_INTAKE 0      /* producers: shard lock + copy of the request into the shard */
 #define COA_QSTAGE_GATHER 1      /* collector: taking the shards' windows */

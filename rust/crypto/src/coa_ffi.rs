@@ -69,6 +69,10 @@ pub struct CoaQueueMetrics {
     /// COA_QSTAGE_* (intake, gather, slot_wait, pack, enqueue, device_wait,
     /// scatter, callbacks, resolve), microseconds summed over windows
     pub stage_us: [f64; 12],
+    /// when the slowest window was launched (ms since creation or reset) and
+    /// its device wait (µs)
+    pub window_max_at_ms: f64,
+    pub window_max_device_us: f64,
 }
 
 /// void (*coa_verdict_cb)(void* user, int status, const uint8_t* verdicts, size_t n)

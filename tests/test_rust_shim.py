@@ -222,3 +222,46 @@ def test_engine_failure_policy_uses_the_reference_code_not_the_oracle():
                 if f in ("gpu.rs", "service.rs", "gpu_certificate.rs"):
                     assert "engine failure" not in src.replace("degrade::engine_failed", ""), f
                     assert not re.search(r"panic!\(\"MI355X verification engine failure", src), f
+
+
+def _c_struct_fields(name):
+    """(field, kind) of a typedef struct in include/coa_verify.h, in order
+    (comma lists split, arrays as kind[n])."""
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    body = re.search(r"typedef struct \{([^}]*)\}\s*" + name + r"\s*;", text).group(1)
+    out = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        ctype, names = decl.split(None, 1)
+        kind = {"uint64_t": "u64", "uint32_t": "u32", "int32_t": "i32", "double": "f64"}[ctype]
+        for n in names.split(","):
+            n = n.strip()
+            m = re.match(r"(\w+)\[(\d+)\]", n)
+            out.append((m.group(1), f"{kind}[{m.group(2)}]") if m else (n, kind))
+    return out
+
+
+def test_queue_metrics_struct_matches_header():
+    """coa_queue_metrics_t is passed by pointer: the Rust mirror
+    (coa_ffi.rs CoaQueueMetrics) and the Python one (coa_crypto.QueueMetrics)
+    must list the same fields, in the same order, with the same types."""
+    import ctypes
+    import sys
+
+    c = _c_struct_fields("coa_queue_metrics_t")
+    src = open(os.path.join(RUST, "crypto", "src", "coa_ffi.rs")).read()
+    body = re.search(r"pub struct CoaQueueMetrics \{(.*?)\n\}", src, re.S).group(1)
+    body = re.sub(r"//[^\n]*", "", body)
+    rust = [(n, re.sub(r"\[(\w+);\s*(\d+)\]", r"\1[\2]", t.strip()))
+            for n, t in re.findall(r"pub (\w+):\s*([^,]+),", body)]
+    assert rust == c
+    sys.path.insert(0, os.path.join(ROOT, "xrpl-coa-prototype_amd"))
+    import coa_crypto
+
+    kinds = {ctypes.c_uint64: "u64", ctypes.c_uint32: "u32", ctypes.c_int32: "i32", ctypes.c_double: "f64"}
+    py = []
+    for n, t in coa_crypto.QueueMetrics._fields_:
+        py.append((n, f"{kinds[t._type_]}[{t._length_}]" if hasattr(t, "_length_") else kinds[t]))
+    assert py == c

@@ -63,7 +63,8 @@ class QueueMetrics(ctypes.Structure):
                 ("slot_wait_us_max", ctypes.c_double), ("staging_grows", ctypes.c_uint64),
                 ("slots_verify", ctypes.c_uint32), ("slots_digest", ctypes.c_uint32),
                 ("deferred_requests", ctypes.c_uint64), ("resolver_passes", ctypes.c_uint64),
-                ("resolve_us_max", ctypes.c_double), ("stage_us", ctypes.c_double * 12)]
+                ("resolve_us_max", ctypes.c_double), ("stage_us", ctypes.c_double * 12),
+                ("window_max_at_ms", ctypes.c_double), ("window_max_device_us", ctypes.c_double)]
 
     # COA_QSTAGE_* indices of stage_us
     STAGES = ("intake", "gather", "slot_wait", "pack", "enqueue", "device_wait", "scatter", "callbacks", "resolve")

@@ -288,6 +288,8 @@ struct Lane {
   // longest wait for a free slot
   double m_window_us_max = 0.0, m_slot_wait_us_max = 0.0;
   uint64_t m_window_max_items = 0;
+  int64_t m_epoch_ns = now_ns();  // creation or the last reset_metrics
+  double m_window_max_at_ms = 0.0, m_window_max_dev_us = 0.0;
   uint32_t m_window_max_kinds = 0;
   uint64_t m_deferred = 0, m_passes = 0;
   double m_resolve_us_max = 0.0;
@@ -592,6 +594,8 @@ struct Lane {
         m_window_us_max = window_us;
         m_window_max_items = f.L.items();
         m_window_max_kinds = f.L.kinds();
+        m_window_max_at_ms = (double)(f.t_launch - m_epoch_ns) * 1e-6;
+        m_window_max_dev_us = (double)f.L.stage_ns[COA_QSTAGE_DEVICE_WAIT] * 1e-3;
       }
       m_slot_wait_us_max = std::max(m_slot_wait_us_max, (double)f.L.slot_wait_ns * 1e-3);
       if (rc != COA_OK) m_failed++;
@@ -682,6 +686,8 @@ struct Lane {
     m_window_us_max = m_slot_wait_us_max = 0.0;
     m_window_max_items = 0;
     m_window_max_kinds = 0;
+    m_epoch_ns = now_ns();
+    m_window_max_at_ms = m_window_max_dev_us = 0.0;
     m_deferred = m_passes = 0;
     m_resolve_us_max = 0.0;
     std::fill(m_stage_us, m_stage_us + COA_QSTAGES, 0.0);
@@ -991,6 +997,8 @@ int coa_queue_metrics(coa_queue* q, coa_queue_metrics_t* out) {
       out->window_us_max = L.m_window_us_max;
       out->window_max_items = L.m_window_max_items;
       out->window_max_kinds = L.m_window_max_kinds;
+      out->window_max_at_ms = L.m_window_max_at_ms;
+      out->window_max_device_us = L.m_window_max_dev_us;
     }
     out->slot_wait_us_max = std::max(out->slot_wait_us_max, L.m_slot_wait_us_max);
     out->staging_grows += L.be->grows();
