@@ -145,6 +145,46 @@ def test_queue_certificates_and_digests_gpu(engine):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("inline", ["1", "0"])
+def test_queue_small_certificate_windows_gpu(engine, monkeypatch, inline):
+    """Windows of a few certificates and nothing else take the latency kernel
+    with its last block writing the status words into page-locked memory,
+    the arrays in the kernel arguments when they fit (C1's committee of 4:
+    ~0.6 KB a certificate), else one copy (coa_queue_hip.cpp Slot::cpub,
+    coa_certificate_verify_publish); COA_QUEUE_INLINE=0 stages them.  Windows
+    of 1, 2 and 3 certificates with a bad vote (left open by the fused
+    kernel, decided by the resolver), a bad header signature and a bad header
+    id give the same bits as the host path, both ways."""
+    import certificates as C
+
+    monkeypatch.setenv("COA_QUEUE_INLINE", inline)
+    committee, batch = C.synth_certificates(9, committee_size=4, n_payload=1, seed=29)
+    committee.register()
+    batch.vote_sigs[int(batch.offsets[1]) + 1, 40] ^= 1   # certificate 1: bad vote
+    batch.header_sigs[4, 33] ^= 1                          # certificate 4: bad header signature
+    h = bytearray(batch.header_inputs[6]); h[-1] ^= 1; batch.header_inputs[6] = bytes(h)  # 6: bad id
+    want = C.verify_certificate_batch(batch, committee, rng_seed=1)
+    with engine.AggregationQueue(max_batch=4096, max_delay_us=2_000_000) as q:
+        got, i, size = [], 0, 1
+        while i < len(batch):
+            fs = []
+            for c in range(i, min(i + size, len(batch))):
+                lo, hi = int(batch.offsets[c]), int(batch.offsets[c + 1])
+                votes = [(engine.PublicKey(bytes(batch.vote_pks[j])),
+                          engine.Signature.from_bytes(bytes(batch.vote_sigs[j]))) for j in range(lo, hi)]
+                fs.append(q.submit_certificate(batch.header_inputs[c], bytes(batch.ids[c]), bytes(batch.authors[c]),
+                                               bytes(batch.header_sigs[c]), batch.round, votes))
+            q.flush()
+            got += [f.result(timeout=60) for f in fs]
+            i += size
+            size = size % 3 + 1
+        m = q.metrics()
+    assert [int(g != 0) for g in got] == list(want)
+    assert got[1] == engine.CERT_BAD_VOTES and got[4] == engine.CERT_BAD_HEADER_SIG and got[6] & engine.CERT_BAD_HEADER_ID
+    assert m["failed_windows"] == 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("borrow", [False, True])
 def test_queue_pipelined_windows_gpu(engine, borrow):
     """Many small windows in a row (max_batch 256) from four producers mixing

@@ -108,6 +108,24 @@ extern "C" int coa_certificate_resolve_raw(const uint8_t* ids, const uint8_t* or
                                            const uint64_t* vote_offsets, size_t n, uint32_t* raw,
                                            uint8_t* status_out);
 
+// The aggregation queue's certificate windows of at most 64 certificates
+// whose jobs take the latency kernel (coa_queue_hip.cpp): the window's arrays
+// packed in page-locked h_base at the byte offsets `off` (header offsets
+// relative to off->hdr, vote offsets window-relative), device copy d_base of
+// in_bytes.  Inline in the kernel arguments when they fit
+// COA_CERT_INLINE_BYTES (no copy), else one H2D copy into d_base; either way
+// the kernel's last block writes (tag << 8) | status for each certificate
+// into host_res (page-locked, polled by the caller) and re-zeroes d_ctr[0..64]
+// (a device block of 65 words, zero before the first call).  Returns 1 when
+// the window is not of that size (nothing enqueued), else COA_OK or a
+// negative COA_E*.
+struct CoaCertOffsets {
+  uint64_t hdr, hoff, ids, origins, hsigs, rounds, vpks, vsigs, voff;
+};
+extern "C" int coa_certificate_verify_publish(int device, const uint8_t* h_base, uint8_t* d_base, size_t in_bytes,
+                                              const CoaCertOffsets* off, size_t n, size_t n_votes, uint32_t* d_ctr,
+                                              uint32_t* host_res, uint32_t tag, void* stream);
+
 // Host copies spread over the runtime's copy threads (COA_PACK_THREADS):
 // the aggregation queue packs large windows into page-locked staging with
 // it.  Returns when every segment is copied.

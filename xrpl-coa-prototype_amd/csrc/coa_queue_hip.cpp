@@ -68,6 +68,7 @@
 #include "coa_queue.h"
 
 #define COA_QUEUE_SLOTS_DEFAULT 4
+#define COA_LAT_RES_WORDS 64  // result words of an inline latency or published certificate window
 
 namespace {
 
@@ -102,8 +103,14 @@ struct Slot {
   // the kernel arguments, verdict words straight into lres (page-locked,
   // coherent), which complete() polls for ltag -- no copies, no event wait
   bool inl = false;
-  uint32_t* lres = nullptr;
+  uint32_t* lres = nullptr;  // COA_LAT_RES_WORDS words
   uint32_t ltag = 0;
+  // a window of at most 64 certificates and nothing else, on the latency
+  // kernel: its last block writes the status words into lres (no status
+  // memset, no D2H copy, no event wait; inline arguments when the window
+  // fits, coa_certificate_verify_publish); dctr is its device counter block
+  bool cpub = false;
+  uint32_t* dctr = nullptr;  // 65 device words, zero between launches
   // output offsets of the current launch
   size_t o_v = 0, o_c = 0, o_d = 0;
 };
@@ -152,7 +159,7 @@ int make_stream(Slot& sl) {
     (void)hipEventDestroy(sl.ev);
     sl.ev = nullptr;
   }
-  for (void** p : {&sl.din, &sl.dout, &sl.ws})
+  for (void** p : {&sl.din, &sl.dout, &sl.ws, reinterpret_cast<void**>(&sl.dctr)})
     if (*p) {
       (void)hipFree(*p);
       *p = nullptr;
@@ -198,6 +205,7 @@ void free_slot(Slot& sl) {
   if (sl.dout) (void)hipFree(sl.dout);
   if (sl.ws) (void)hipFree(sl.ws);
   if (sl.lres) (void)hipHostFree(sl.lres);
+  if (sl.dctr) (void)hipFree(sl.dctr);
   if (sl.ev) (void)hipEventDestroy(sl.ev);
   if (sl.s) (void)hipStreamDestroy(sl.s);
   bury(sl.grave);
@@ -247,7 +255,10 @@ class HipBackend : public coa_q::Backend {
                               : std::max(coa_verify_workspace_bytes(items),
                                          coa_certificate_workspace_bytes(items / 68 + 1, items)) + 256;
     for (Slot& sl : slots_) {
-      if (lane_ == coa_q::LANE_VERIFY && hipSetDevice(sl.dev) == hipSuccess) (void)lat_words(sl);
+      if (lane_ == coa_q::LANE_VERIFY && hipSetDevice(sl.dev) == hipSuccess) {
+        (void)lat_words(sl);
+        (void)ctr_words(sl);
+      }
       if (hipSetDevice(sl.dev) != hipSuccess || grow_pinned(sl.hin, sl.cap_hin, pre_in, sl.grave) != hipSuccess ||
           grow_pinned(sl.hout, sl.cap_hout, pre_out, sl.grave) != hipSuccess ||
           grow_dev(sl.din, sl.cap_din, pre_in, sl.grave) != hipSuccess ||
@@ -266,13 +277,25 @@ class HipBackend : public coa_q::Backend {
   // (allocated once; null when the allocation failed: such windows then take
   // the staged path)
   static uint32_t* lat_words(Slot& sl) {
-    if (!sl.lres &&
-        hipHostMalloc(reinterpret_cast<void**>(&sl.lres), COA_LAT_INLINE * sizeof(uint32_t), hipHostMallocCoherent) !=
-            hipSuccess) {
+    if (!sl.lres && hipHostMalloc(reinterpret_cast<void**>(&sl.lres), COA_LAT_RES_WORDS * sizeof(uint32_t),
+                                  hipHostMallocCoherent) != hipSuccess) {
       sl.lres = nullptr;
       (void)hipGetLastError();
     }
     return sl.lres;
+  }
+  // ... and its device counter block for published certificate windows
+  // (zeroed once; the kernel re-zeroes it after each window)
+  static uint32_t* ctr_words(Slot& sl) {
+    if (!sl.dctr) {
+      if (hipMalloc(reinterpret_cast<void**>(&sl.dctr), 65 * sizeof(uint32_t)) != hipSuccess ||
+          hipMemset(sl.dctr, 0, 65 * sizeof(uint32_t)) != hipSuccess) {
+        if (sl.dctr) (void)hipFree(sl.dctr);
+        sl.dctr = nullptr;
+        (void)hipGetLastError();
+      }
+    }
+    return sl.dctr;
   }
 
   void launch(coa_q::Launch& L) override {
@@ -497,6 +520,7 @@ class HipBackend : public coa_q::Backend {
       std::chrono::steady_clock::time_point t;
       ~EnqClock() { L.stage_ns[COA_QSTAGE_ENQUEUE] += ns_between(t, std::chrono::steady_clock::now()); }
     } enq_clock{L, t_enq};
+    sl.cpub = false;
     sl.inl = inline_ok_ && sl.lat && L.nv <= COA_LAT_INLINE && L.nc == 0 && L.nd == 0 && lat_words(sl) != nullptr;
     if (sl.inl) {
       // a few signatures alone (Header::verify / Vote::verify at low load):
@@ -515,6 +539,33 @@ class HipBackend : public coa_q::Backend {
       coa_keycache_use(nullptr);
       if (rc != COA_OK) return rc;
       return hipEventRecord(sl.ev, sl.s) == hipSuccess ? COA_OK : COA_EHIP;
+    }
+    sl.cpub = inline_ok_ && L.nc > 0 && L.nc <= COA_LAT_RES_WORDS && L.nv == 0 && L.nd == 0 &&
+              lat_words(sl) != nullptr && ctr_words(sl) != nullptr;
+    if (sl.cpub) {
+      // certificates alone, few (Certificate::verify at low load): see Slot::cpub
+      if (inject) {
+        sl.launched = true;
+        return COA_EHIP;  // fault injection: nothing launched
+      }
+      std::memset(sl.lres, 0, L.nc * sizeof(uint32_t));
+      sl.ltag = (sl.ltag + 1) & 0xffffffu;
+      if (sl.ltag == 0) sl.ltag = 1;
+      if (!sl.keys) sl.keys = coa_keycache_pin(sl.dev);
+      coa_keycache_use(sl.keys);
+      const CoaCertOffsets off{i_ch, i_cho, i_cid, i_cor, i_chs, i_crd, i_cvp, i_cvs, i_cvo};
+      const int rc = coa_certificate_verify_publish(sl.dev, h, static_cast<uint8_t*>(sl.din), in_bytes, &off, L.nc,
+                                                    L.nvotes, sl.dctr, sl.lres, sl.ltag, sl.s);
+      coa_keycache_use(nullptr);
+      if (rc == COA_OK) {
+        sl.launched = true;
+        return hipEventRecord(sl.ev, sl.s) == hipSuccess ? COA_OK : COA_EHIP;
+      }
+      if (rc != 1) {
+        sl.launched = true;  // something may be enqueued: finish() drains the stream
+        return rc;
+      }
+      sl.cpub = false;  // too many jobs for the latency kernel: the staged path below
     }
     uint8_t* d = static_cast<uint8_t*>(sl.din);
     uint8_t* dout = static_cast<uint8_t*>(sl.dout);
@@ -556,8 +607,8 @@ class HipBackend : public coa_q::Backend {
     const auto t_wait = std::chrono::steady_clock::now();
     if (sl.launched) {
       (void)hipSetDevice(sl.dev);
-      if (L.rc == COA_OK && sl.inl) {
-        L.rc = poll_words(sl, L.nv);
+      if (L.rc == COA_OK && (sl.inl || sl.cpub)) {
+        L.rc = poll_words(sl, sl.inl ? L.nv : L.nc);
       } else if (L.rc == COA_OK) {
         if (hipEventSynchronize(sl.ev) != hipSuccess) L.rc = COA_EHIP;
       } else {
@@ -578,7 +629,13 @@ class HipBackend : public coa_q::Backend {
           std::memcpy(w->v_out.data(), h + sl.o_v + v, w->nv);
         }
         for (size_t i = 0; i < w->nd; i++) std::memcpy(&w->d_out[i * 32], h + sl.o_d + (dn + i) * 64, 32);
-        if (w->nc) scatter_certs(*w, reinterpret_cast<const uint32_t*>(h + sl.o_c) + c);
+        if (w->nc && sl.cpub) {
+          uint32_t st[COA_LAT_RES_WORDS];
+          for (size_t i = 0; i < w->nc; i++) st[i] = sl.lres[c + i] & 0xffu;  // the tag off
+          scatter_certs(*w, st);
+        } else if (w->nc) {
+          scatter_certs(*w, reinterpret_cast<const uint32_t*>(h + sl.o_c) + c);
+        }
         w->g_defer = w->ng > 0;
         v += w->nv;
         c += w->nc;

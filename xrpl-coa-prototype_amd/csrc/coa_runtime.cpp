@@ -1235,11 +1235,11 @@ CertArgs cert_args(Dev& d, const KeySet& ks, uint8_t* base, const CertPack& p, s
 // The latency launch with the certificates inline in the kernel arguments
 // (no pinned staging copy, no H2D transfer): for calls whose arrays fit
 // COA_CERT_INLINE_BYTES.  Returns 1 when they do not fit (nothing launched).
-int cert_inline(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_out) {
+// Certificates [lo, hi) of `in` into ci's buffer; false when they do not fit.
+bool cert_inl_build(CertInl& ci, const CertIn& in, size_t lo, size_t hi) {
   const size_t nc = hi - lo;
   const uint64_t h0 = in.hdr_off[lo], hb = in.hdr_off[hi] - h0;
   const uint64_t v0 = in.voff[lo], nv = in.voff[hi] - v0;
-  static thread_local CertInl ci;  // ~3 KB, staged on the host; copied into the launch
   size_t o = 0;
   auto take = [&](size_t bytes) {
     const size_t at = o;
@@ -1255,7 +1255,7 @@ int cert_inline(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status
   ci.off_vpks = take(nv * 32);
   ci.off_vsigs = take(nv * 64);
   ci.off_hdr = take(hb + 16);
-  if (o > COA_CERT_INLINE_BYTES || nc > 64) return 1;
+  if (o > COA_CERT_INLINE_BYTES || nc > 64) return false;
   uint8_t* b = ci.buf;
   uint64_t* ho = reinterpret_cast<uint64_t*>(b + ci.off_hoff);
   uint64_t* vo = reinterpret_cast<uint64_t*>(b + ci.off_voff);
@@ -1273,6 +1273,14 @@ int cert_inline(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status
   }
   if (hb) std::memcpy(b + ci.off_hdr, in.hdr_data + h0, hb);
   std::memset(b + ci.off_hdr + hb, 0, 16);
+  return true;
+}
+
+int cert_inline(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_out) {
+  const size_t nc = hi - lo;
+  const uint64_t nv = in.voff[hi] - in.voff[lo];
+  static thread_local CertInl ci;  // ~3 KB, staged on the host; copied into the launch
+  if (!cert_inl_build(ci, in, lo, hi)) return 1;
   hipStream_t s = d.stream;
   if (!d.lat_ctr) {  // [0] block counter, [1..64] status words; the kernel re-zeroes both
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.lat_ctr), 65 * 4));
@@ -2266,6 +2274,59 @@ int coa_lat_verify_inline(int device, const uint8_t* h_records, size_t n, uint32
   a.nk = ks->nkeys;
   a.comb = d->comb;
   HIP_TRY(coa_launch_verify_lat(a, stream ? (hipStream_t)stream : d->stream));
+  return COA_OK;
+}
+
+int coa_certificate_verify_publish(int device, const uint8_t* h_base, uint8_t* d_base, size_t in_bytes,
+                                   const CoaCertOffsets* off, size_t n, size_t n_votes, uint32_t* d_ctr,
+                                   uint32_t* host_res, uint32_t tag, void* stream) {
+  const int rc = ensure_init();
+  if (rc != COA_OK) return rc;
+  if (n == 0) return COA_OK;
+  if (n > 64 || cert_lanes(n + n_votes) != 64) return 1;  // not the latency kernel's size: nothing enqueued
+  if (!h_base || !d_base || !off || !d_ctr || !host_res || tag == 0) return fail(COA_EINVAL, "null argument");
+  Dev* d = dev_by_id(device);
+  if (!d) return fail(COA_EINVAL, "device not opened by coa_init");
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  const CertIn in{h_base + off->hdr,
+                  reinterpret_cast<const uint64_t*>(h_base + off->hoff),
+                  h_base + off->ids,
+                  h_base + off->origins,
+                  h_base + off->hsigs,
+                  reinterpret_cast<const uint64_t*>(h_base + off->rounds),
+                  h_base + off->vpks,
+                  h_base + off->vsigs,
+                  reinterpret_cast<const uint64_t*>(h_base + off->voff)};
+  const KeySetP ks = keys_now(*d);  // pinned (the queue) or current; see coa_lat_verify_device
+  static thread_local CertInl ci;
+  if (!env_is("COA_CERT_INLINE", "0") && cert_inl_build(ci, in, 0, n)) {
+    CertArgs& a = ci.a;
+    a = cert_args(*d, *ks, nullptr, CertPack{}, n, n_votes);
+    a.status = d_ctr + 1;
+    a.host_res = host_res;
+    a.done_ctr = d_ctr;
+    a.tag = tag;
+    HIP_TRY(coa_launch_cert_verify_inl(ci, s));
+    return COA_OK;
+  }
+  HIP_TRY(hipMemcpyAsync(d_base, h_base, in_bytes, hipMemcpyHostToDevice, s));
+  CertPack p{};
+  p.hdata = off->hdr;
+  p.hoff = off->hoff;
+  p.ids = off->ids;
+  p.origins = off->origins;
+  p.hsigs = off->hsigs;
+  p.rounds = off->rounds;
+  p.vpks = off->vpks;
+  p.vsigs = off->vsigs;
+  p.voff = off->voff;
+  CertArgs a = cert_args(*d, *ks, d_base, p, n, n_votes);
+  a.status = d_ctr + 1;
+  a.host_res = host_res;
+  a.done_ctr = d_ctr;
+  a.tag = tag;
+  HIP_TRY(coa_launch_cert_verify(a, 64, nullptr, s));
   return COA_OK;
 }
 
