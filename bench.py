@@ -810,7 +810,8 @@ def queue_round_mix(rates=(5, 10, 100, 300, 1000), seconds=0.6, committee_size=1
 
     rnd = random.Random(5)
     ct = []
-    for c in range(min(40, committee_size)):
+    for t in range(40):  # 40 samples over the round's certificates (the first 5 dropped below)
+        c = t % committee_size
         lo, hi = int(certs.offsets[c]), int(certs.offsets[c + 1])
         zs = [rnd.getrandbits(128) for _ in range(hi - lo)]
         t1 = time.perf_counter()
@@ -1498,6 +1499,9 @@ def summarize(value, sec, cpu):
     out["c4_stream_p50_p99_ms"] = {r: p50p99(get("c4_stream", f"rate_{r}")) for r in ("1000", "4000")}
     out["c4_sha512_GBps_16384"] = get("c4_sha512", "batches_16384", "GBps")
     out["round_mix_1000_p50_p99_ms"] = p50p99(get("queue_round_mix", "rates", "1000", "certificate"))
+    # C1 through the queue at a low rate, idle launch (the Rust service's policy)
+    out["round_mix_c1_10_idle_cert_sig_p50_ms"] = [
+        get("queue_round_mix_c1", "rates_idle_launch", "10", k, "p50_ms") for k in ("certificate", "signature")]
     adv = get("queue_round_mix_adversarial", "1000")
     if isinstance(adv, dict):
         out["round_mix_adversarial_1000_p50_p99_ms"] = {k: p50p99(adv.get(k)) for k in
@@ -1689,6 +1693,9 @@ def main():
                                                .get("cpu_one_core_p50_ms")))
         section("queue_round_mix", queue_round_mix)
         section("queue_round_mix_adversarial", queue_round_mix_adversarial)
+        # the reference's own CPU-runnable configuration (BASELINE configs[0],
+        # C1: a committee of 4, 3-vote certificates) through the queue
+        section("queue_round_mix_c1", lambda: queue_round_mix(rates=(10, 100, 1000), committee_size=4, n_payload=1))
         section("host_e2e", lambda: host_e2e(local, dev, msgs_h, pks.cpu().numpy(), sigs.cpu().numpy()))
 
     if rank == 0:

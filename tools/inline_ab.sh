@@ -1,10 +1,11 @@
-# GPU session: queue tests, then an A/B of the inline latency windows
-# (COA_QUEUE_INLINE) on the round mix; every step under its own time limit.
+# GPU session: queue tests, then an A/B of the queue's inline / published
+# small windows (COA_QUEUE_INLINE) on the round mix; every step under its own
+# time limit.
 set -o pipefail
 mkdir -p gpurun_out/inl
-timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_queue.py tests/test_gpu_queue_harness.py tests/test_gpu_recovery.py tests/test_gpu_latency.py tests/test_gpu_resolve.py > gpurun_out/inl/tests.log 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_queue.py tests/test_gpu_queue_harness.py tests/test_gpu_recovery.py tests/test_gpu_resolve.py tests/test_gpu_certificates.py > gpurun_out/inl/tests.log 2>&1 || exit 1
 for r in 1 2; do
   for v in 1 0; do
-    COA_QUEUE_INLINE=$v timeout -k 10 240 python bench.py --no-cpu-baseline --sections queue_round_mix > gpurun_out/inl/mix_${v}_$r.json 2> gpurun_out/inl/mix_${v}_$r.err || exit 1
+    COA_QUEUE_INLINE=$v timeout -k 10 240 python bench.py --no-cpu-baseline --sections queue_round_mix,queue_round_mix_c1 > gpurun_out/inl/mix_${v}_$r.json 2> gpurun_out/inl/mix_${v}_$r.err || exit 1
   done
 done
