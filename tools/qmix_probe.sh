@@ -1,3 +1,7 @@
+# Round-mix tail probe (round 5): the c4_stream and queue_round_mix bench
+# sections three times in fresh processes with slow-window tracing
+# (COA_QUEUE_TRACE_SLOW_US), each under its own time limit
+# (profiles/r05_round_mix_rate5_probe.jsonl).
 set -o pipefail
 mkdir -p gpurun_out/qmix
 for i in 1 2 3; do
