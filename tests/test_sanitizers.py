@@ -71,6 +71,14 @@ def test_queue_many_producers_tsan():
     # retried == recovered == injected and no callback saw an engine error)
     out = _run([exe, "16", "500", "7"], {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"})
     assert "8000/8000 answered, 0 wrong" in out and "injected 0," not in out, out
+    # idle launch: windows also launched by submitting threads that find the
+    # engine idle (beside the collector), with and without injected failures
+    for k in ("1", "2"):
+        env = {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1", "COA_QUEUE_IDLE_LAUNCH": k}
+        out = _run([exe, "16", "500"], env)
+        assert "8000/8000 answered, 0 wrong" in out, out
+        out = _run([exe, "16", "300", "7"], env)
+        assert "4800/4800 answered, 0 wrong" in out and "injected 0," not in out, out
 
 
 def test_queue_many_producers_asan_ubsan():
@@ -84,3 +92,5 @@ def test_queue_many_producers_asan_ubsan():
     # get the engine error (counted as failed windows), the rest are exact
     out = _run([exe, "8", "300", "5", "1"], env)
     assert "2400/2400 answered, 0 wrong" in out and "recovered 0" in out and "engine errors 0" not in out, out
+    out = _run([exe, "16", "500"], dict(env, COA_QUEUE_IDLE_LAUNCH="1"))
+    assert "8000/8000 answered, 0 wrong" in out, out

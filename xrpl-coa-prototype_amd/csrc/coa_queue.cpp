@@ -256,7 +256,7 @@ struct Lane {
   size_t max_batch = 65536;
   size_t reserve_items = 131072;  // Window::reserve_for's items (coa_queue_create)
   bool digest_lane = false;
-  bool prepared = false;  // slots' streams and staging set up (coa_queue_create or the first window)
+  std::atomic<bool> prepared{false};  // slots' streams and staging set up (coa_queue_create or the first window)
   std::chrono::microseconds max_delay{500};
   std::unique_ptr<coa_q::Backend> be;
   std::unique_ptr<Shard[]> shards{new Shard[kShards]};
@@ -302,6 +302,11 @@ struct Lane {
   // COA_QUEUE_IDLE_LAUNCH (read at creation; 0 = off, the default): a window
   // closes at once while fewer than this many windows are in flight
   size_t idle_launch = 0;
+  // With idle launch, a request that finds the engine idle is launched by
+  // the submitting thread itself (COA_QUEUE_DIRECT=0: by the collector, as
+  // before): no wake-up of the collector thread on a lone request's path
+  bool direct_ok = true;
+  std::mutex gather_mu;  // one gather at a time (the collector, or a submitter launching directly)
   double trace_slow_us = 0;  // COA_QUEUE_TRACE_SLOW_US (read at creation): report slower windows on stderr
 
   Lane() {
@@ -344,8 +349,16 @@ struct Lane {
     const bool first = old <= 0 && now_pend > 0;
     const bool crossed = old < (int64_t)max_batch && now_pend >= (int64_t)max_batch;
     if (first || crossed) {
-      std::lock_guard<std::mutex> l(mu);
+      std::unique_lock<std::mutex> l(mu);
       if (first) oldest = std::chrono::steady_clock::now();
+      // idle launch on an idle engine: this thread takes the window and
+      // launches it at once (the collector's wake-up was most of a lone
+      // request's queueing at low rates, where its thread has gone to sleep)
+      if (first && direct_ok && busy < idle_launch && !stop.load() && !flush && prepared.load() && pend.load() > 0) {
+        busy++;
+        launch_window(l);
+        return;
+      }
       cv.notify_one();
     }
   }
@@ -416,35 +429,46 @@ struct Lane {
       }
       flush = false;
       busy++;  // before the take: flush must not see pend == 0 and busy == 0 meanwhile
-      Flight f;
-      l.unlock();
-      const int64_t tg = now_ns();
-      gather(f);
-      f.L.stage_ns[COA_QSTAGE_GATHER] += now_ns() - tg;
-      l.lock();
-      if (f.parts.empty()) {  // every pending item was taken by an earlier window
-        busy--;
-        if (idle()) idle_cv.notify_all();
-        continue;
-      }
-      m_max_window = std::max<uint64_t>(m_max_window, f.L.items());
-      l.unlock();
-      f.L.reset_outputs();
-      f.L.attempts = 1;
-      f.t_launch = now_ns();
-      if (!prepared) {  // a lane COA_QUEUE_LANES left cold: set up by its first window
-        be->prepare(max_batch);
-        prepared = true;
-      }
-      be->launch(f.L);  // stages and enqueues; blocks only while every slot is busy
-      f.L.stage_ns[COA_QSTAGE_SLOT_WAIT] += f.L.slot_wait_ns;
-      l.lock();
-      m_windows++;
-      flight.push_back(std::move(f));
-      m_max_in_flight = std::max<uint64_t>(m_max_in_flight, flight.size());
-      flight_cv.notify_one();
+      launch_window(l);
     }
     collector_done = true;
+    flight_cv.notify_one();
+  }
+
+  // Takes the pending requests as one window and launches it: the collector,
+  // or (idle launch) a submitting thread that found the engine idle.  Called
+  // with `l` holding mu and busy already counting the window; returns with
+  // `l` held.
+  void launch_window(std::unique_lock<std::mutex>& l) {
+    Flight f;
+    l.unlock();
+    const int64_t tg = now_ns();
+    {
+      std::lock_guard<std::mutex> g(gather_mu);
+      gather(f);
+    }
+    f.L.stage_ns[COA_QSTAGE_GATHER] += now_ns() - tg;
+    l.lock();
+    if (f.parts.empty()) {  // every pending item was taken by an earlier window
+      busy--;
+      if (idle()) idle_cv.notify_all();
+      return;
+    }
+    m_max_window = std::max<uint64_t>(m_max_window, f.L.items());
+    l.unlock();
+    f.L.reset_outputs();
+    f.L.attempts = 1;
+    f.t_launch = now_ns();
+    if (!prepared.load()) {  // a lane COA_QUEUE_LANES left cold: set up by its first window (the collector's)
+      be->prepare(max_batch);
+      prepared.store(true);
+    }
+    be->launch(f.L);  // stages and enqueues; blocks only while every slot is busy
+    f.L.stage_ns[COA_QSTAGE_SLOT_WAIT] += f.L.slot_wait_ns;
+    l.lock();
+    m_windows++;
+    flight.push_back(std::move(f));
+    m_max_in_flight = std::max<uint64_t>(m_max_in_flight, flight.size());
     flight_cv.notify_one();
   }
 
@@ -790,6 +814,7 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
     L.reserve_items = 2 * std::min<size_t>(L.max_batch, 65536);
     if (const char* e = getenv("COA_QUEUE_HELPERS")) L.n_helpers = std::max(0, std::min(15, atoi(e)));
     if (const char* e = getenv("COA_QUEUE_IDLE_LAUNCH")) L.idle_launch = (size_t)std::max(0, std::min(64, atoi(e)));
+    if (const char* e = getenv("COA_QUEUE_DIRECT")) L.direct_ok = e[0] != '0';
     if (const char* e = getenv("COA_QUEUE_TRACE_SLOW_US")) L.trace_slow_us = atof(e);
     L.be.reset(coa_q::make_backend(k));
     // COA_QUEUE_LANES=verify|digest|verify,digest (read at creation; default
@@ -802,7 +827,7 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
     const bool warm = !lanes || std::strstr(lanes, k == coa_q::LANE_DIGEST ? "digest" : "verify") != nullptr;
     if (warm) {
       L.be->prepare(L.max_batch);
-      L.prepared = true;
+      L.prepared.store(true);
     }
     L.start();
   }
