@@ -692,12 +692,41 @@ def paced_queue(arrive_s, kind, item, vm=None, vp=None, vs=None, vexp=None, cert
     lat = np.zeros(max(n, 1), np.float64)
     el = ctypes.c_double()
     m = coa_crypto.QueueMetrics()
+    host0 = _host_cpu()
     wrong = lib.latc_paced(max_batch, max_delay_us, n, arrive.ctypes.data, kind_a.ctypes.data, item_a.ctypes.data,
                            *[a.ctypes.data for a in keep], lat.ctypes.data, ctypes.addressof(el),
                            ctypes.addressof(m))
+    host1 = _host_cpu()
     assert wrong == 0, f"paced queue run: {wrong} wrong answers"
     met = coa_crypto.metrics_dict(m)
+    # where a host-side tail comes from: this process's CPU use over the run
+    # (cores busy on average) and the cgroup's CPU throttling meanwhile
+    met["host"] = {k: (None if host0[k] is None or host1[k] is None else round(host1[k] - host0[k], 3))
+                   for k in host0}
+    if met["host"]["cpu_s"] is not None and el.value > 0:
+        met["host"]["cores_busy"] = round(met["host"]["cpu_s"] / el.value, 2)
     return lat[:n] * 1e-3, el.value, met
+
+
+def _host_cpu():
+    """This process's CPU seconds and its cgroup's throttling counters
+    (cpu.stat: periods throttled, milliseconds throttled -- cgroup v2's
+    throttled_usec or v1's throttled_time in ns; None where unreadable)."""
+    import resource
+
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    out = {"cpu_s": ru.ru_utime + ru.ru_stime, "throttled_periods": None, "throttled_ms": None}
+    for path, key, scale in (("/sys/fs/cgroup/cpu.stat", "throttled_usec", 1e-3),
+                             ("/sys/fs/cgroup/cpu/cpu.stat", "throttled_time", 1e-6)):
+        try:
+            with open(path) as f:
+                st = dict(line.split() for line in f if len(line.split()) == 2)
+            out["throttled_periods"] = float(st["nr_throttled"])
+            out["throttled_ms"] = float(st[key]) * scale
+            break
+        except (OSError, ValueError, KeyError):
+            continue
+    return out
 
 
 STREAM_KINDS = {0: "plain (shared hardware queues)", 1: "CU-masked (a hardware queue each)",
@@ -721,6 +750,8 @@ def queue_diag(met):
             # requests the resolver answered after their window (open
             # certificates, bare vote batches) and its slowest pass
             "deferred_requests": int(met["deferred_requests"]), "resolver_passes": int(met["resolver_passes"]),
+            # this process's CPU use and its cgroup's throttling over the run (paced_queue)
+            "host": met.get("host"),
             "resolve_ms_max": round(met["resolve_us_max"] * 1e-3, 3),
             # mean microseconds per window in each stage (COA_QSTAGE_*)
             "stage_us_per_window": {k: round(v / max(1, met["windows"]), 1) for k, v in met["stage_us"].items()}}
