@@ -1297,7 +1297,7 @@ def host_e2e(local, dev, msgs_h, pks_h, sigs_h, n_certs=10000):
     for borrowed in (1, 0):
         for producers in (1, 4, 8):
             met = coa_crypto.QueueMetrics()
-            rounds = 3
+            rounds = 20  # 200k certificates, ~50-70 ms: 3 rounds (~8 ms) varied by up to 40 % between runs
             rc = lib.latc_stream_certificates(65536, 500, producers, rounds, borrowed, 0.0, *ptrs, n_certs,
                                               expect.ctypes.data, ctypes.byref(el), ctypes.addressof(met))
             assert rc == 0, f"streamed certificates: {rc} wrong"
@@ -1313,7 +1313,7 @@ def host_e2e(local, dev, msgs_h, pks_h, sigs_h, n_certs=10000):
     # of ~240 certificates)
     for rate in (1_000_000, 2_000_000, 3_000_000):
         met = coa_crypto.QueueMetrics()
-        rounds = 6
+        rounds = 12
         rc = lib.latc_stream_certificates(16384, 200, 4, rounds, 1, float(rate), *ptrs, n_certs,
                                           expect.ctypes.data, ctypes.byref(el), ctypes.addressof(met))
         assert rc == 0, f"paced streamed certificates: {rc} wrong"
