@@ -44,7 +44,7 @@ if [[ $STEPS == *fullprof* ]]; then
   run fullprof && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/fullprof -o run --output-format csv \
       -- python3 bench.py > gpurun_out/bench_fullprof.json 2> gpurun_out/fullprof.err \
     || { tail -30 gpurun_out/fullprof.err; exit 1; }
-  python3 tools/kernel_trace_summary.py gpurun_out/fullprof gpurun_out/fullprof_by_grid.json | head -40
+  python3 tools/kernel_trace_summary.py gpurun_out/fullprof gpurun_out/fullprof_by_grid.json > gpurun_out/fullprof_summary.txt
 fi
 if [[ $STEPS == *verifypmc* ]]; then
   # three counter passes of the C2 verify call -> profiles JSON tied to this build
