@@ -306,8 +306,8 @@ int coa_ed25519_sign_many_device(int device, const uint8_t* d_seeds, const uint8
  * each with its own collector, device slots and completion thread: one for
  * signatures, vote batches and certificates, one for digests (a digest
  * window is a 14 ms serial chain; it never delays a verdict).  A lane's
- * collector launches each window on a free slot (four per GPU per lane,
- * COA_QUEUE_SLOTS / COA_QUEUE_DIGEST_SLOTS; pinned staging, its own stream
+ * collector launches each window on a free slot (four per GPU for verdicts,
+ * eight for digests, COA_QUEUE_SLOTS / COA_QUEUE_DIGEST_SLOTS; pinned staging, its own stream
  * on its own hardware queue, COA_QUEUE_STREAMS) without waiting for the
  * previous window, and its completion thread answers windows in order: the
  * callback runs there with status (COA_OK or a negative engine error) and

@@ -820,7 +820,7 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
     // COA_QUEUE_LANES=verify|digest|verify,digest (read at creation; default
     // both): the lanes set up now -- streams, their first dispatch, staging
     // (a verify slot ~23 MB page-locked + ~320 MB of HBM at max_batch 65,536,
-    // a digest slot 64 + 64 MB, four of each per GPU).  A primary that never
+    // a digest slot 64 + 64 MB; four verify and eight digest slots per GPU).  A primary that never
     // hashes worker batches, or a worker that never verifies, names its lane;
     // the other is set up by its first window (which then waits ~25-75 ms).
     const char* lanes = getenv("COA_QUEUE_LANES");

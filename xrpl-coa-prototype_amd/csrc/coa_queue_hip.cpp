@@ -68,6 +68,11 @@
 #include "coa_queue.h"
 
 #define COA_QUEUE_SLOTS_DEFAULT 4
+// The digest lane's windows are one ~14 ms SHA-512 chain each on a few
+// waves (L = 64 lanes per batch), so more of them in flight cost the GPU
+// nothing and shorten the wait for a slot: at C4's 1,000 batches/s, 8 slots
+// give p50 16.0 ms against 19.6 with 4 (profiles/r05_digest_slots_ab.jsonl)
+#define COA_QUEUE_DIGEST_SLOTS_DEFAULT 8
 #define COA_LAT_RES_WORDS 64  // result words of an inline latency or published certificate window
 
 namespace {
@@ -383,7 +388,7 @@ class HipBackend : public coa_q::Backend {
     // 8-context engine): windows in flight at once (1..8; COA_QUEUE_SLOTS for
     // the verify lane, COA_QUEUE_DIGEST_SLOTS for the digest lane;
     // tools/queue_probe.c measures the choice)
-    size_t per = COA_QUEUE_SLOTS_DEFAULT;
+    size_t per = lane_ == coa_q::LANE_DIGEST ? COA_QUEUE_DIGEST_SLOTS_DEFAULT : COA_QUEUE_SLOTS_DEFAULT;
     if (const char* e = getenv(lane_ == coa_q::LANE_DIGEST ? "COA_QUEUE_DIGEST_SLOTS" : "COA_QUEUE_SLOTS")) {
       const int v = atoi(e);
       if (v >= 1 && v <= 8) per = (size_t)v;
