@@ -253,7 +253,8 @@ def test_queue_pipelined_windows_gpu(engine, borrow):
         q.metrics_reset()
         m0 = q.metrics()
     assert m["requests"] == len(results) and m["signatures"] == n
-    assert m["windows"] > 4 and 2 <= m["max_in_flight"] <= 4  # pipelined over the slots (4 per GPU)
+    # pipelined over the slots (per GPU: 4 for verdicts, 8 for digests)
+    assert m["windows"] > 4 and 2 <= m["max_in_flight"] <= 8
     assert 0 < m["wait_us_p50"] <= m["wait_us_p99"] <= m["wait_us_max"] * 1.1
     # per-stage time (COA_QSTAGE_*): every stage a window passes through was
     # timed; certificate 4's foreign key went through the resolver
