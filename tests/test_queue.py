@@ -188,7 +188,7 @@ def test_queue_small_certificate_windows_gpu(engine, monkeypatch, inline):
 @pytest.mark.parametrize("borrow", [False, True])
 def test_queue_pipelined_windows_gpu(engine, borrow):
     """Many small windows in a row (max_batch 256) from four producers mixing
-    every kind: windows overlap on the device slots (max_in_flight 2..4),
+    every kind: windows overlap on the device slots (max_in_flight 2..8),
     every answer equals its expectation -- valid/corrupted signatures,
     certificates including ones that need the exact host re-decision (a vote
     key outside the registered committee, a corrupted vote), digests -- and
