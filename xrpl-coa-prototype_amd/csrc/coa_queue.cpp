@@ -183,6 +183,11 @@ constexpr int kHelpersDefault = 3;         // COA_QUEUE_HELPERS overrides (0..15
 constexpr size_t kParallelAnswer = 8192;  // requests per launch from which the helpers join
 constexpr size_t kRun = 4096;             // requests per run
 
+// True on the queue's own completion, helper and resolver threads: a
+// callback that submits must not launch from there (a launch can wait for a
+// free slot, and only those threads free slots).
+thread_local bool t_queue_thread = false;
+
 struct AnswerPool {
   std::mutex m;
   std::condition_variable cv, done_cv;
@@ -193,7 +198,11 @@ struct AnswerPool {
   std::vector<std::thread> th;
 
   void start(int n) {
-    for (int i = 0; i < n; i++) th.emplace_back([this] { loop(); });
+    for (int i = 0; i < n; i++)
+      th.emplace_back([this] {
+        t_queue_thread = true;
+        loop();
+      });
   }
   ~AnswerPool() {
     {
@@ -354,7 +363,8 @@ struct Lane {
       // idle launch on an idle engine: this thread takes the window and
       // launches it at once (the collector's wake-up was most of a lone
       // request's queueing at low rates, where its thread has gone to sleep)
-      if (first && direct_ok && busy < idle_launch && !stop.load() && !flush && prepared.load() && pend.load() > 0) {
+      if (first && direct_ok && !t_queue_thread && busy < idle_launch && busy < (size_t)be->slots() && !stop.load() &&
+          !flush && prepared.load() && pend.load() > 0) {
         busy++;
         launch_window(l);
         return;
@@ -487,6 +497,7 @@ struct Lane {
   }
 
   void answer() {
+    t_queue_thread = true;
     std::unique_lock<std::mutex> l(mu);
     for (;;) {
       flight_cv.wait(l, [&] { return !flight.empty() || collector_done; });
@@ -639,6 +650,7 @@ struct Lane {
   // answers their callbacks -- off the completion thread, so the windows
   // behind an open certificate are answered while it is being decided.
   void resolve_loop() {
+    t_queue_thread = true;
     std::unique_lock<std::mutex> l(mu);
     for (;;) {
       resolve_cv.wait(l, [&] { return !open.empty() || resolver_stop; });
