@@ -1409,10 +1409,18 @@ def timed_steps(step, steps, warmup, world, dist, sync, before_timed=None):
 def _latc():
     """tools/latc.c (lib/liblatc.so): the same one-item calls timed in a C
     loop, as the Rust crate's extern "C" binding makes them (no Python
-    argument marshalling in the clock)."""
+    argument marshalling in the clock).  It is the liblatc.so beside the
+    engine library coa_crypto loaded (COA_VERIFY_LIB for A/B builds,
+    tools/build_variant.py builds both): one beside another build would bind
+    a second engine instance through its rpath and time that one."""
     import ctypes
 
-    lib = ctypes.CDLL(os.path.join(PKG, "lib", "liblatc.so"))
+    import coa_crypto
+
+    path = os.path.join(os.path.dirname(coa_crypto.LIB_PATH), "liblatc.so")
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path}: no C-caller loop beside {coa_crypto.LIB_PATH}")
+    lib = ctypes.CDLL(path)
     vp, sz, dp = ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_double)
     lib.latc_certificate.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                      ctypes.c_uint64, vp, vp, sz, ctypes.c_int, dp]

@@ -5,8 +5,12 @@
 #include <stdint.h>
 
 // wide HBM comb of B (coa_smul.h): positions x magnitudes, 24 dwords each
+// (overridable for A/B builds, tools/build_variant.py: W = 26 with 10
+// positions is a 32 GB comb)
+#ifndef COA_WCOMB_W
 #define COA_WCOMB_W 24
 #define COA_WCOMB_POS 11
+#endif
 #define COA_WCOMB_MAG (1u << (COA_WCOMB_W - 1))
 #define COA_WCOMB_ENTRIES ((uint64_t)COA_WCOMB_POS * COA_WCOMB_MAG)
 #define COA_WCOMB_DWORDS (COA_WCOMB_ENTRIES * 24)
