@@ -290,6 +290,45 @@ def test_queue_idle_launch_gpu(engine, monkeypatch, mode):
 
 
 @pytest.mark.gpu
+def test_queue_submit_from_callback_gpu(engine):
+    """A verdict callback that submits the next request (the Rust service's
+    continuations do): the callback runs on the queue's completion thread,
+    which never launches a window itself (coa_queue.cpp t_queue_thread), so
+    the collector launches it once the finishing window leaves the slot.
+    24 chained requests under idle launch, each submitted from the previous
+    one's callback, answer exactly and without waiting out the 2 s
+    deadline."""
+    import time
+
+    vecs = [v for v in load_golden("verify_vectors.json") if len(v["msg"]) == 64][:24]
+    got, done = [], threading.Event()
+    with engine.AggregationQueue(max_batch=4096, max_delay_us=2_000_000) as q:
+        q.set_idle_launch(1)
+
+        def submit(i):
+            v = vecs[i]
+            f = q.submit_verify(bytes.fromhex(v["msg"]), bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]))
+            f.add_done_callback(lambda f, i=i: on_done(i, f))
+
+        def on_done(i, f):
+            got.append((i, f.exception() or f.result()))
+            if i + 1 < len(vecs):
+                submit(i + 1)
+            else:
+                done.set()
+
+        t0 = time.perf_counter()
+        submit(0)
+        assert done.wait(30)
+        el = time.perf_counter() - t0
+        m = q.metrics()
+    assert [i for i, _ in got] == list(range(len(vecs)))
+    assert [r for _, r in got] == [v["expect"] for v in vecs]
+    assert el < 2.0, el  # one deadline wait would be 2 s
+    assert m["windows"] == len(vecs) and m["failed_windows"] == 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("borrow", [False, True])
 def test_open_certificate_does_not_hold_its_window_gpu(engine, borrow):
     """A window holding one certificate with a vote key outside the registered
