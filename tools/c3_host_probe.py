@@ -1,7 +1,8 @@
 """Probe: the host-pointer C3 round (10,000 certificates, committee 100, one
 coa_certificate_verify_many call per round from C, tools/latc.c) under the
 pipelined certificate path's switches, read per call: COA_CERT_BUFFERS
-(chunks in flight) x COA_CERT_CHUNK_JOBS.  COA_PACK_THREADS is read once per
+(chunks in flight) x COA_CERT_CHUNK_JOBS x COA_CERT_RAMP (smaller first
+chunks); C3_PROBE_CONFIGS="bufs:chunk:ramp,..." replaces the default list.  COA_PACK_THREADS is read once per
 process (CopyPool), so it is set by the caller.  One JSON line per
 configuration, plus the pipeline's own pack / wait split (COA_CERT_TRACE) on
 stderr for one call each.
@@ -16,7 +17,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "xrpl-coa-prototype_amd"))
 sys.path.insert(0, ROOT)
 
-CONFIGS = [(2, 1 << 17), (3, 1 << 17), (4, 1 << 17), (3, 1 << 16), (4, 1 << 16), (4, 1 << 15)]
+CONFIGS = [(2, 1 << 17, 0), (3, 1 << 17, 0), (4, 1 << 17, 0), (3, 1 << 16, 0), (4, 1 << 16, 0), (4, 1 << 15, 0)]
+if os.environ.get("C3_PROBE_CONFIGS"):
+    CONFIGS = [tuple(int(x) for x in c.split(":")) for c in os.environ["C3_PROBE_CONFIGS"].split(",")]
 
 
 def main():
@@ -46,9 +49,10 @@ def main():
     ptrs = [a.ctypes.data for a in arrs]
     expect = np.zeros(n_certs, np.uint8)
     el = ctypes.c_double()
-    for bufs, chunk in CONFIGS:
+    for bufs, chunk, ramp in CONFIGS:
         os.environ["COA_CERT_BUFFERS"] = str(bufs)
         os.environ["COA_CERT_CHUNK_JOBS"] = str(chunk)
+        os.environ["COA_CERT_RAMP"] = str(ramp)
         assert lib.latc_certificates_many(*ptrs, n_certs, expect.ctypes.data, 2, 1, ctypes.byref(el)) == 0
         os.environ["COA_CERT_TRACE"] = "1"
         assert lib.latc_certificates_many(*ptrs, n_certs, expect.ctypes.data, 1, 1, ctypes.byref(el)) == 0
@@ -58,7 +62,7 @@ def main():
             assert lib.latc_certificates_many(*ptrs, n_certs, expect.ctypes.data, calls, 1, ctypes.byref(el)) == 0
             best = el.value if best is None else min(best, el.value)
         print(json.dumps({"pack_threads": os.environ.get("COA_PACK_THREADS", "8"), "buffers": bufs,
-                          "chunk_jobs": chunk, "certs_per_s": round(n_certs * calls / best, 1),
+                          "chunk_jobs": chunk, "ramp": ramp, "certs_per_s": round(n_certs * calls / best, 1),
                           "ms_per_round": round(best / calls * 1e3, 3)}), flush=True)
 
 

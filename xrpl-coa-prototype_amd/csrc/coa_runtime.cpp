@@ -1335,6 +1335,16 @@ size_t cert_chunk_jobs() {
   const long v = e ? atol(e) : 0;
   return v >= (1 << 12) ? (size_t)v : ((size_t)1 << 17);
 }
+// The first chunks of a pipelined call are smaller (COA_CERT_RAMP = r, read
+// per call, default 1: chunk k < r takes chunk_jobs >> (r - k) jobs), so the
+// GPU starts after a half chunk's pack and copy instead of a full one's.
+// Host C3 round, same box, 8 alternating pairs: r = 1 +1.4 to +6.7 % over
+// r = 0; r = 2 and 3 slower (more chunks); profiles/r05_c3_host_ramp_ab.txt.
+int cert_ramp() {
+  const char* e = getenv("COA_CERT_RAMP");
+  const int v = e ? atoi(e) : 1;
+  return v < 0 ? 0 : (v > 4 ? 4 : v);
+}
 int cert_buffers() {
   const char* e = getenv("COA_CERT_BUFFERS");
   const int v = e ? atoi(e) : 3;
@@ -1351,11 +1361,13 @@ int cert_buffers() {
 int cert_shard_pipelined(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_out) {
   const size_t chunk_jobs = cert_chunk_jobs();
   const int nb = cert_buffers();
+  const int ramp = cert_ramp();
   std::vector<size_t> cuts{lo};
   size_t jobs = 0;
   for (size_t c = lo; c < hi; c++) {
     jobs += 1 + (in.voff[c + 1] - in.voff[c]);
-    if (jobs >= chunk_jobs && c + 1 < hi) {
+    const int k = (int)cuts.size() - 1;  // the chunk being cut
+    if (jobs >= (chunk_jobs >> std::max(0, ramp - k)) && c + 1 < hi) {
       cuts.push_back(c + 1);
       jobs = 0;
     }
