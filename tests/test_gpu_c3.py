@@ -7,7 +7,8 @@ bit for status bit with the C restatement of dalek run the reference's way,
 per certificate (oracle/coa_oracle.c coa_oracle_certificate_verify_many:
 Header::digest == id, Signature::verify(id, author),
 verify_batch(Certificate::digest, votes), each check evaluated on its own --
-primary/src/messages.rs:48-84,189-234)."""
+primary/src/messages.rs:48-84,189-234).  The round runs with the fused
+kernel's jobs in key order (the default) and in certificate order."""
 import os
 import struct
 
@@ -27,7 +28,7 @@ KINDS = ("header_byte", "header_sig_flip", "header_sig_small_R", "vote_sig_flip"
 
 
 @pytest.mark.timeout(600)
-def test_c3_round_full_size_with_injected_failures(engine):
+def test_c3_round_full_size_with_injected_failures(engine, monkeypatch):
     import certificates as C
     import workloads
 
@@ -81,6 +82,12 @@ def test_c3_round_full_size_with_injected_failures(engine):
             vpks[lo:lo + 67], vsigs[lo:lo + 67] = p, s
     rounds = np.full(n, b.round, np.uint64)
     got = engine.certificate_verify_many(hin, ids, authors, hsigs, rounds, vpks, vsigs, b.offsets, rng_seed=17)
+    # the fused kernel takes its jobs in key order (k_job_count/k_job_place);
+    # in certificate order (COA_CERT_KEYSORT=0) every status word is the same
+    monkeypatch.setenv("COA_CERT_KEYSORT", "0")
+    unsorted = engine.certificate_verify_many(hin, ids, authors, hsigs, rounds, vpks, vsigs, b.offsets, rng_seed=17)
+    monkeypatch.delenv("COA_CERT_KEYSORT")
+    assert (unsorted == got).all()
 
     zs = np.random.default_rng(1).integers(0, 256, (int(b.offsets[-1]), 16), dtype=np.uint8)
     exp = co.certificate_verify_many(hin, ids, authors, hsigs, b.round, vpks, vsigs, b.offsets, zs,

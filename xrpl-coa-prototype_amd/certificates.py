@@ -291,13 +291,14 @@ class CertificateBatch:
         return Certificate(h, votes)
 
 
-def synth_certificates(n_certs, committee_size=100, n_votes=None, n_payload=32, round_=1, seed=0):
+def synth_certificates(n_certs, committee_size=100, n_votes=None, n_payload=32, round_=1, seed=0, rotate=True):
     """Synthetic round of certificates in the reference's byte formats
     (SURVEY.md 8(d) C3/C1): committee keys seed_i = SHA512("coa-key"||i),
     header author = member c mod N with n_payload batch digests (worker 0)
     and the previous round's 2f+1 certificate digests as parents (shared by
     every header of the round, as in Narwhal), votes from n_votes distinct
-    members rotated by certificate index, all signed on the device."""
+    members rotated by certificate index (rotate=False: the same members in
+    the same positions), all signed on the device."""
     import workloads
 
     N = committee_size
@@ -324,7 +325,8 @@ def synth_certificates(n_certs, committee_size=100, n_votes=None, n_payload=32, 
     authors = pks[author_idx].copy()
     cin = [bytes(ids[c]) + struct.pack("<Q", round_) + bytes(authors[c]) for c in range(n_certs)]
     cdg = coa_crypto.sha512_many(cin)[:, :32].copy()
-    voter_idx = ((np.arange(n_certs)[:, None] + np.arange(n_votes)[None, :]) % N).reshape(-1)
+    # rotate=False: vote position v is member v in every certificate
+    voter_idx = ((np.arange(n_certs)[:, None] * int(rotate) + np.arange(n_votes)[None, :]) % N).reshape(-1)
     vmsgs = np.repeat(cdg, n_votes, axis=0)
     vpks, vsigs = coa_crypto.sign_many(seeds[voter_idx], vmsgs)
     offs = np.arange(0, n_certs * n_votes + 1, n_votes, dtype=np.uint64)

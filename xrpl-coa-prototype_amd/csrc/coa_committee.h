@@ -69,6 +69,9 @@ struct CertArgs {
   uint32_t* done_ctr = nullptr;  // device word, 0 between calls
   uint32_t tag = 0;
   uint32_t total_blocks = 0;     // set by the launcher
+  // throughput variant: the jobs in key order (set by the launcher, null =
+  // in order; see k_cert_verify)
+  const uint32_t* perm = nullptr;
 };
 
 // A small certificate passed inline in the kernel arguments of the latency

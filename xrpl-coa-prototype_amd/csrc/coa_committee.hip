@@ -436,7 +436,8 @@ __global__ void __launch_bounds__(256, WAVES) k_cert_verify(CertArgs a, uint32_t
     if (sub == 0) chunk = atomicAdd(ctr, 1u);
     chunk = __builtin_amdgcn_readfirstlane(__shfl(chunk, 0));
     if (chunk >= chunks) break;
-    const uint64_t job = (uint64_t)chunk * 64 + sub;
+    uint64_t job = (uint64_t)chunk * 64 + sub;
+    if (a.perm && job < jobs) job = a.perm[job];  // key order (k_job_count, k_job_place)
     ge_p3 P;
     uint32_t pre = PRE_NONE, cert = 0;
     if (job < jobs) job_comb(a, (uint32_t)job, P, pre, cert);
@@ -855,6 +856,75 @@ hipError_t coa_launch_cert_verify_inl(const CertInl& ci, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Jobs in key order for the throughput kernel.  A chunk of 64 consecutive
+// jobs in certificate order holds 64 different keys (a certificate's votes
+// come from distinct members), so each of the 13 key-comb additions reads 64
+// random entries of 64 different 654 MB combs: half the kernel's requests
+// missed the per-CU translation cache (profiles/r05_cert_tlb_pmc.txt).  Sorted
+// by key slot, a chunk's lanes read one key's comb.  A counting sort without
+// global atomics (one counter per key took 680k contended atomics, 0.4 ms):
+// COA_SORT_WGS workgroups each count a contiguous range of jobs per slot in
+// LDS (unregistered keys in the last bin) into counts[bin][wg]; one block
+// scans that bin-major matrix into start offsets; each workgroup then places
+// its jobs from its own offsets (LDS counters: the order inside a bin is
+// arbitrary, and every job's verdict depends on its own inputs only).
+#define COA_SORT_BINS 4096
+#define COA_SORT_WGS 256
+__global__ void __launch_bounds__(1024) k_job_count(CertArgs a, uint32_t bins, uint32_t per,
+                                                   uint32_t* __restrict__ counts, uint32_t* __restrict__ bin) {
+  __shared__ uint32_t h[COA_SORT_BINS];
+  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) h[k] = 0;
+  __syncthreads();
+  const uint64_t jobs = (uint64_t)a.nc + a.nv;
+  const uint64_t lo = (uint64_t)blockIdx.x * per, hi = lo + per < jobs ? lo + per : jobs;
+  for (uint64_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+    uint32_t pk[8];
+    load8(pk, j < a.nc ? a.origins + j * 8 : a.vpks + (j - a.nc) * 8);
+    const int slot = key_lookup(a.keys, a.nk, pk);
+    const uint32_t b = slot < 0 ? a.nk : (uint32_t)slot;
+    bin[j] = b;
+    atomicAdd(h + b, 1u);
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) counts[(uint64_t)k * COA_SORT_WGS + blockIdx.x] = h[k];
+}
+// Exclusive scan in place of n words by one block.
+__global__ void __launch_bounds__(1024) k_job_scan(uint32_t* __restrict__ v, uint32_t n) {
+  __shared__ uint32_t part[1024];
+  const uint32_t t = threadIdx.x, per = (n + 1023) / 1024;
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < per; i++) {
+    const uint32_t k = t * per + i;
+    if (k < n) sum += v[k];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan of the per-thread sums
+    const uint32_t x = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;  // exclusive start of this thread's words
+  for (uint32_t i = 0; i < per; i++) {
+    const uint32_t k = t * per + i;
+    if (k < n) {
+      const uint32_t c = v[k];
+      v[k] = run;
+      run += c;
+    }
+  }
+}
+__global__ void __launch_bounds__(1024) k_job_place(uint64_t jobs, uint32_t bins, uint32_t per,
+                                                   const uint32_t* __restrict__ offs, const uint32_t* __restrict__ bin,
+                                                   uint32_t* __restrict__ perm) {
+  __shared__ uint32_t cur[COA_SORT_BINS];
+  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) cur[k] = offs[(uint64_t)k * COA_SORT_WGS + blockIdx.x];
+  __syncthreads();
+  const uint64_t lo = (uint64_t)blockIdx.x * per, hi = lo + per < jobs ? lo + per : jobs;
+  for (uint64_t j = lo + threadIdx.x; j < hi; j += blockDim.x) perm[atomicAdd(cur + bin[j], 1u)] = (uint32_t)j;
+}
+
 // Signature chunks one wave of the throughput grid may take (its slab
 // capacity): the even share plus slack for the waves that run ahead.
 static uint32_t cert_tp_jcap(uint64_t jobs, uint64_t lanes) {
@@ -868,9 +938,12 @@ static size_t cert_slab_bytes(uint64_t jobs, uint64_t lanes) {
   return (size_t)(lanes * cert_tp_jcap(jobs, lanes) * PSCR_ROWS * 16);
 }
 
+// ... | key-order sort: counts / offsets [COA_SORT_BINS][COA_SORT_WGS], each
+// job's bin [jobs], the permutation [jobs]
 size_t coa_cert_scratch_bytes(uint64_t jobs) {
   const uint64_t lanes = cert_tp_lanes(jobs ? jobs : 1);
-  return 256 + cert_slab_bytes(jobs, lanes) + (size_t)(jobs ? jobs : 1) * 32 + 256;
+  return 256 + cert_slab_bytes(jobs, lanes) + (size_t)(jobs ? jobs : 1) * 32 + 256 +
+         (size_t)COA_SORT_BINS * COA_SORT_WGS * 4 + (size_t)(jobs ? jobs : 1) * 8;
 }
 
 hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr, hipStream_t s) {
@@ -896,6 +969,21 @@ hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr,
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     a.cdig = cdig;
+  }
+  // jobs in key order when the committee fits the bins and the call is
+  // large enough to pay for the sort (COA_CERT_KEYSORT=0: certificate order)
+  const char* ks = getenv("COA_CERT_KEYSORT");
+  if (a.nk > 0 && a.nk + 1 <= COA_SORT_BINS && jobs >= 16384 && !(ks && ks[0] == '0' && ks[1] == 0)) {
+    uint32_t* counts = pscr + 64 + cert_slab_bytes(jobs, lanes) / 4 + (size_t)jobs * 8 + 64;
+    uint32_t* bin = counts + (size_t)COA_SORT_BINS * COA_SORT_WGS;
+    uint32_t* perm = bin + jobs;
+    const uint32_t bins = a.nk + 1, per = (uint32_t)((jobs + COA_SORT_WGS - 1) / COA_SORT_WGS);
+    hipLaunchKernelGGL(k_job_count, dim3(COA_SORT_WGS), dim3(1024), 0, s, a, bins, per, counts, bin);
+    hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(1024), 0, s, counts, bins * COA_SORT_WGS);
+    hipLaunchKernelGGL(k_job_place, dim3(COA_SORT_WGS), dim3(1024), 0, s, jobs, bins, per, counts, bin, perm);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    a.perm = perm;
   }
   if (cert_tp_waves() == 3)
     hipLaunchKernelGGL(k_cert_verify<3>, dim3((uint32_t)(a.hdr_blocks + lanes / 256)), dim3(256), 0, s, a, pscr,
