@@ -82,12 +82,37 @@ def test_c3_round_full_size_with_injected_failures(engine, monkeypatch):
             vpks[lo:lo + 67], vsigs[lo:lo + 67] = p, s
     rounds = np.full(n, b.round, np.uint64)
     got = engine.certificate_verify_many(hin, ids, authors, hsigs, rounds, vpks, vsigs, b.offsets, rng_seed=17)
-    # the fused kernel takes its jobs in key order (k_job_count/k_job_place);
-    # in certificate order (COA_CERT_KEYSORT=0) every status word is the same
-    monkeypatch.setenv("COA_CERT_KEYSORT", "0")
-    unsorted = engine.certificate_verify_many(hin, ids, authors, hsigs, rounds, vpks, vsigs, b.offsets, rng_seed=17)
+    # the same round with the fused kernel's jobs in key order
+    # (k_job_count/k_job_place; COA_CERT_PIPE_KEYSORT=1 asks for it on the
+    # host path's chunks): every status word is the same
+    monkeypatch.setenv("COA_CERT_PIPE_KEYSORT", "1")
+    keyed = engine.certificate_verify_many(hin, ids, authors, hsigs, rounds, vpks, vsigs, b.offsets, rng_seed=17)
+    monkeypatch.delenv("COA_CERT_PIPE_KEYSORT")
+    assert (keyed == got).all()
+    # device-resident (coa_certificate_verify_many_device, the fused kernel's
+    # raw status words, key order by default): the same words in certificate
+    # order (COA_CERT_KEYSORT=0), and Ok exactly where the host path says Ok
+    # and the fused kernel could decide (no key outside the committee)
+    import torch
+
+    dev = torch.device("cuda:0")
+    hd = np.frombuffer(b"".join(hin) + bytes(16), np.uint8)
+    hoff = np.zeros(n + 1, np.int64)
+    hoff[1:] = np.cumsum([len(h) for h in hin])
+    t = lambda a: torch.from_numpy(np.array(a)).to(dev)  # noqa: E731
+    args = (t(hd), t(hoff), t(ids), t(authors), t(hsigs), t(rounds.view(np.int64)), t(vpks), t(vsigs),
+            t(b.offsets.view(np.int64)))
+    raws = []
+    for order in ("1", "0"):
+        monkeypatch.setenv("COA_CERT_KEYSORT", order)
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+        engine.certificate_verify_many_device(0, *args, status)
+        torch.cuda.synchronize()
+        raws.append(status.cpu().numpy())
     monkeypatch.delenv("COA_CERT_KEYSORT")
-    assert (unsorted == got).all()
+    assert (raws[0] == raws[1]).all()
+    decided = np.array([kind_of.get(c) not in (6, 9) for c in range(n)])
+    assert ((raws[0] == 0)[decided] == (got == 0)[decided]).all()
 
     zs = np.random.default_rng(1).integers(0, 256, (int(b.offsets[-1]), 16), dtype=np.uint8)
     exp = co.certificate_verify_many(hin, ids, authors, hsigs, b.round, vpks, vsigs, b.offsets, zs,

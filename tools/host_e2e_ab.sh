@@ -9,6 +9,6 @@ for rep in $(seq ${REPS:-3}); do
   for kind in ${KINDS:?}; do
     env ${VAR:?}=$kind timeout -k 10 200 python bench.py --no-cpu-baseline --steps 10 --warmup 2 --sections host_e2e \
       > gpurun_out/he_$kind.json 2> gpurun_out/he_$kind.err || exit 1
-    python -c "import json;s=json.load(open('gpurun_out/he_$kind.json'))['summary'];print('$kind', $rep, s['host_c2_verify_per_s'], s['host_c3_certs_per_s'])"
+    python -c "import json;s=json.load(open('gpurun_out/he_$kind.json'))['summary'];print('$kind', $rep, s['host_c2_verify_per_s'], s['host_c3_certs_per_s'], s['c3_stream_certs_per_s'])"
   done
 done

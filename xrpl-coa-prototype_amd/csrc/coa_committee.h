@@ -72,6 +72,9 @@ struct CertArgs {
   // throughput variant: the jobs in key order (set by the launcher, null =
   // in order; see k_cert_verify)
   const uint32_t* perm = nullptr;
+  // 1: the caller asks for key order (the launcher sorts when the call is
+  // large enough and COA_CERT_KEYSORT is not 0)
+  uint32_t key_order = 0;
 };
 
 // A small certificate passed inline in the kernel arguments of the latency

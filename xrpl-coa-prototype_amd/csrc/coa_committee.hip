@@ -861,17 +861,20 @@ hipError_t coa_launch_cert_verify_inl(const CertInl& ci, hipStream_t s) {
 // come from distinct members), so each of the 13 key-comb additions reads 64
 // random entries of 64 different 654 MB combs: half the kernel's requests
 // missed the per-CU translation cache (profiles/r05_cert_tlb_pmc.txt).  Sorted
-// by key slot, a chunk's lanes read one key's comb.  A counting sort without
-// global atomics (one counter per key took 680k contended atomics, 0.4 ms):
-// COA_SORT_WGS workgroups each count a contiguous range of jobs per slot in
-// LDS (unregistered keys in the last bin) into counts[bin][wg]; one block
-// scans that bin-major matrix into start offsets; each workgroup then places
-// its jobs from its own offsets (LDS counters: the order inside a bin is
-// arbitrary, and every job's verdict depends on its own inputs only).
+// by key slot, a chunk's lanes read one key's comb.  A counting sort with
+// few contended atomics (one global counter per key took 680k of them,
+// 0.4 ms): COA_SORT_WGS workgroups each count a contiguous range of jobs
+// per slot in LDS (unregistered keys in the last bin), keep the counts
+// (counts[wg][bin]) and add them to the bin totals (one atomic per
+// workgroup and bin); one block turns the totals into start cursors; each
+// workgroup then reserves its range in every bin it uses (one atomic each)
+// and places its jobs with LDS counters.  The order inside a bin is
+// arbitrary: every job's verdict depends on its own inputs only.
 #define COA_SORT_BINS 4096
 #define COA_SORT_WGS 256
-__global__ void __launch_bounds__(1024) k_job_count(CertArgs a, uint32_t bins, uint32_t per,
-                                                   uint32_t* __restrict__ counts, uint32_t* __restrict__ bin) {
+__global__ void __launch_bounds__(256) k_job_count(CertArgs a, uint32_t bins, uint32_t per,
+                                                   uint32_t* __restrict__ total, uint32_t* __restrict__ counts,
+                                                   uint32_t* __restrict__ bin) {
   __shared__ uint32_t h[COA_SORT_BINS];
   for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) h[k] = 0;
   __syncthreads();
@@ -886,16 +889,22 @@ __global__ void __launch_bounds__(1024) k_job_count(CertArgs a, uint32_t bins, u
     atomicAdd(h + b, 1u);
   }
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) counts[(uint64_t)k * COA_SORT_WGS + blockIdx.x] = h[k];
+  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) {
+    const uint32_t c = h[k];
+    counts[(uint64_t)blockIdx.x * COA_SORT_BINS + k] = c;
+    if (c) atomicAdd(total + k, c);
+  }
 }
-// Exclusive scan in place of n words by one block.
+// Bin totals -> exclusive start cursors, in place, one block.
 __global__ void __launch_bounds__(1024) k_job_scan(uint32_t* __restrict__ v, uint32_t n) {
   __shared__ uint32_t part[1024];
   const uint32_t t = threadIdx.x, per = (n + 1023) / 1024;
-  uint32_t sum = 0;
-  for (uint32_t i = 0; i < per; i++) {
+  uint32_t mine[COA_SORT_BINS / 1024], sum = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < COA_SORT_BINS / 1024; i++) {
     const uint32_t k = t * per + i;
-    if (k < n) sum += v[k];
+    mine[i] = (i < per && k < n) ? v[k] : 0u;
+    sum += mine[i];
   }
   part[t] = sum;
   __syncthreads();
@@ -905,21 +914,22 @@ __global__ void __launch_bounds__(1024) k_job_scan(uint32_t* __restrict__ v, uin
     part[t] += x;
     __syncthreads();
   }
-  uint32_t run = part[t] - sum;  // exclusive start of this thread's words
-  for (uint32_t i = 0; i < per; i++) {
+  uint32_t run = part[t] - sum;  // exclusive start of this thread's bins
+#pragma unroll
+  for (uint32_t i = 0; i < COA_SORT_BINS / 1024; i++) {
     const uint32_t k = t * per + i;
-    if (k < n) {
-      const uint32_t c = v[k];
-      v[k] = run;
-      run += c;
-    }
+    if (i < per && k < n) v[k] = run;
+    run += mine[i];
   }
 }
-__global__ void __launch_bounds__(1024) k_job_place(uint64_t jobs, uint32_t bins, uint32_t per,
-                                                   const uint32_t* __restrict__ offs, const uint32_t* __restrict__ bin,
-                                                   uint32_t* __restrict__ perm) {
+__global__ void __launch_bounds__(256) k_job_place(uint64_t jobs, uint32_t bins, uint32_t per,
+                                                   uint32_t* __restrict__ cursor, const uint32_t* __restrict__ counts,
+                                                   const uint32_t* __restrict__ bin, uint32_t* __restrict__ perm) {
   __shared__ uint32_t cur[COA_SORT_BINS];
-  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) cur[k] = offs[(uint64_t)k * COA_SORT_WGS + blockIdx.x];
+  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) {
+    const uint32_t c = counts[(uint64_t)blockIdx.x * COA_SORT_BINS + k];
+    cur[k] = c ? atomicAdd(cursor + k, c) : 0u;  // this workgroup's range in bin k
+  }
   __syncthreads();
   const uint64_t lo = (uint64_t)blockIdx.x * per, hi = lo + per < jobs ? lo + per : jobs;
   for (uint64_t j = lo + threadIdx.x; j < hi; j += blockDim.x) perm[atomicAdd(cur + bin[j], 1u)] = (uint32_t)j;
@@ -938,12 +948,12 @@ static size_t cert_slab_bytes(uint64_t jobs, uint64_t lanes) {
   return (size_t)(lanes * cert_tp_jcap(jobs, lanes) * PSCR_ROWS * 16);
 }
 
-// ... | key-order sort: counts / offsets [COA_SORT_BINS][COA_SORT_WGS], each
-// job's bin [jobs], the permutation [jobs]
+// ... | key-order sort: bin totals / cursors [COA_SORT_BINS], counts
+// [COA_SORT_WGS][COA_SORT_BINS], each job's bin [jobs], the permutation [jobs]
 size_t coa_cert_scratch_bytes(uint64_t jobs) {
   const uint64_t lanes = cert_tp_lanes(jobs ? jobs : 1);
   return 256 + cert_slab_bytes(jobs, lanes) + (size_t)(jobs ? jobs : 1) * 32 + 256 +
-         (size_t)COA_SORT_BINS * COA_SORT_WGS * 4 + (size_t)(jobs ? jobs : 1) * 8;
+         (size_t)COA_SORT_BINS * (COA_SORT_WGS + 1) * 4 + (size_t)(jobs ? jobs : 1) * 8;
 }
 
 hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr, hipStream_t s) {
@@ -970,17 +980,24 @@ hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr,
     if (e != hipSuccess) return e;
     a.cdig = cdig;
   }
-  // jobs in key order when the committee fits the bins and the call is
-  // large enough to pay for the sort (COA_CERT_KEYSORT=0: certificate order)
+  // jobs in key order when the caller asks for it, the committee fits the
+  // bins and the call is large enough to pay for the sort
+  // (COA_CERT_KEYSORT=0: certificate order everywhere, A/B).  The callers
+  // that ask: the device-resident round (+16-18 %); not the pipelined host
+  // chunks nor the queue's windows, whose concurrent launches lost more to
+  // the sort's own launches than the order gained (profiles/r05_cert_keysort_ab.txt)
   const char* ks = getenv("COA_CERT_KEYSORT");
-  if (a.nk > 0 && a.nk + 1 <= COA_SORT_BINS && jobs >= 16384 && !(ks && ks[0] == '0' && ks[1] == 0)) {
-    uint32_t* counts = pscr + 64 + cert_slab_bytes(jobs, lanes) / 4 + (size_t)jobs * 8 + 64;
+  if (a.key_order && a.nk > 0 && a.nk + 1 <= COA_SORT_BINS && jobs >= 16384 && !(ks && ks[0] == '0' && ks[1] == 0)) {
+    uint32_t* total = pscr + 64 + cert_slab_bytes(jobs, lanes) / 4 + (size_t)jobs * 8 + 64;
+    uint32_t* counts = total + COA_SORT_BINS;
     uint32_t* bin = counts + (size_t)COA_SORT_BINS * COA_SORT_WGS;
     uint32_t* perm = bin + jobs;
     const uint32_t bins = a.nk + 1, per = (uint32_t)((jobs + COA_SORT_WGS - 1) / COA_SORT_WGS);
-    hipLaunchKernelGGL(k_job_count, dim3(COA_SORT_WGS), dim3(1024), 0, s, a, bins, per, counts, bin);
-    hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(1024), 0, s, counts, bins * COA_SORT_WGS);
-    hipLaunchKernelGGL(k_job_place, dim3(COA_SORT_WGS), dim3(1024), 0, s, jobs, bins, per, counts, bin, perm);
+    e = hipMemsetAsync(total, 0, bins * 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_job_count, dim3(COA_SORT_WGS), dim3(256), 0, s, a, bins, per, total, counts, bin);
+    hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(1024), 0, s, total, bins);
+    hipLaunchKernelGGL(k_job_place, dim3(COA_SORT_WGS), dim3(256), 0, s, jobs, bins, per, total, counts, bin, perm);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     a.perm = perm;

@@ -1345,6 +1345,9 @@ int cert_ramp() {
   const int v = e ? atoi(e) : 1;
   return v < 0 ? 0 : (v > 4 ? 4 : v);
 }
+// COA_CERT_PIPE_KEYSORT=1: the pipelined host path's chunks also take
+// their jobs in key order (A/B; see coa_committee.hip k_job_count)
+bool pipe_keysort() { return env_is("COA_CERT_PIPE_KEYSORT", "1"); }
 int cert_buffers() {
   const char* e = getenv("COA_CERT_BUFFERS");
   const int v = e ? atoi(e) : 3;
@@ -1412,6 +1415,7 @@ int cert_shard_pipelined(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_
     if (trace) t_pack += now() - t0;
     HIP_TRY(hipMemcpyAsync(d.certc[b].p, h, p.total, hipMemcpyHostToDevice, st[b]));
     CertArgs a = cert_args(d, *ks, d.certc[b].as<uint8_t>(), p, nc, nv);
+    a.key_order = pipe_keysort() ? 1u : 0u;
     HIP_TRY(coa_launch_cert_verify(a, 1, d.cscrc[b].as<uint32_t>(), st[b]));
     HIP_TRY(hipMemcpyAsync(h + p.status, d.certc[b].as<uint8_t>() + p.status, nc * 4, hipMemcpyDeviceToHost, st[b]));
     pend[b] = {true, clo, chi, p.status};
@@ -2443,6 +2447,7 @@ int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data,
   a.kwtabs = (ks->kwide && !env_is("COA_KEY_WCOMB", "0")) ? ks->kwtabs.as<uint32_t>() : nullptr;
   a.kw20 = ks->kw20 ? 1u : 0u;
   a.status = d_status;
+  a.key_order = 1;  // one device-resident round: jobs in key order
   const int lanes = cert_lanes(n + n_votes);
   HIP_TRY(hipMemsetAsync(d_status, 0, n * 4, s));
   if (workspace || lanes == 64) {
