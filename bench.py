@@ -63,7 +63,7 @@ C2_N = 65536
 PMC_JSON = "r05_verify_pmc.json"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -82,7 +82,9 @@ def parse():
     ap.add_argument("--c4-batches", type=str, default="1024,16384")
     ap.add_argument("--sections", type=str, default="",
                     help="comma list: run only these secondary sections (A/B runs; default all)")
-    return ap.parse_args()
+    ap.add_argument("--secondary-out", type=str, default=os.path.join("gpurun_out", "bench_secondary.json"),
+                    help="where the secondary sections go (a file, not stdout: the headline line stays compact)")
+    return ap.parse_args(argv)
 
 
 def cgroup_cpu_quota():
@@ -1378,7 +1380,7 @@ def load_pmc(n):
     return pj, None
 
 
-def timed_steps(step, steps, warmup, world, dist, sync, before_timed=None):
+def timed_steps(step, steps, warmup, world, dist, sync, before_timed=None, local_out=None):
     """The contract's timed region: `warmup` untimed steps, then exactly
     `steps` steps bracketed by a barrier + device sync on both sides; returns
     the MAX over ranks of the elapsed seconds (gloo all-reduce, control only:
@@ -1403,6 +1405,8 @@ def timed_steps(step, steps, warmup, world, dist, sync, before_timed=None):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if local_out is not None:
+        local_out.append(elapsed)  # this rank's own clock (the line's per-rank record)
     return sharding.max_over_ranks(elapsed, dist, None)
 
 
@@ -1569,8 +1573,137 @@ def summarize(value, sec, cpu):
     return out
 
 
-def main():
-    args = parse()
+def free_port():
+    """A TCP port on 127.0.0.1 nobody listens on (the ranks' rendezvous)."""
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(rank, world, port, base=None):
+    """The environment torch.distributed.run gives rank `rank` of `world` on
+    one node (one process per GPU, LOCAL_RANK = its device)."""
+    env = dict(os.environ if base is None else base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(port)})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def spawn_ranks(world, argv, poll_s=0.05):
+    """`bench.py --gpus N` without a launcher: N child processes, one per GPU
+    (rank r on device r), started BEFORE this parent makes any HIP call (it
+    makes none; exec from a process that initialised the GPU is refused on
+    this pool, so children are started, never exec'd).  Rank 0 prints the
+    line on the inherited stdout.  If any rank fails the others are
+    terminated (their exact PIDs).  Returns the worst exit code."""
+    import subprocess
+
+    port = free_port()
+    procs = [subprocess.Popen(argv, env=rank_env(r, world, port)) for r in range(world)]
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in live:
+                        q.terminate()
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
+def rank_argv(argv):
+    """The command each spawned rank runs: this bench with the same flags."""
+    return [sys.executable, "-u", os.path.abspath(__file__)] + list(argv)
+
+
+def gather_ranks(rec, world, dist):
+    """Every rank's record (device, index range, its own clock) on every rank
+    (gloo all_gather_object: control only, no data-path collective)."""
+    if world == 1:
+        return [rec]
+    out = [None] * world
+    dist.all_gather_object(out, rec)
+    return out
+
+
+# keys of the headline line, in order; the driver parses the LAST stdout line
+HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                 "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
+HEADLINE_MAX_BYTES = 8192  # the driver keeps an ~8 KB tail of stdout
+
+
+def compact_cpu_baseline(cpu):
+    """The CPU baseline without its per-thread-count sweep detail (kept in
+    the secondary file)."""
+    if not cpu:
+        return cpu
+    keep = ("value", "unit", "cores", "kind", "sample", "single_thread_value", "single_verify_p50_ms")
+    out = {k: cpu[k] for k in keep if k in cpu}
+    host = cpu.get("host") or {}
+    out["host"] = {k: host.get(k) for k in ("cpu_model", "usable_cpus", "nproc")}
+    sr = cpu.get("second_reference")
+    if sr:
+        out["second_reference"] = {k: sr.get(k) for k in ("value", "cores", "kind")}
+    return out
+
+
+def compact_roofline(roof):
+    """roofline with the long explanatory strings shortened (the full
+    strings stay in the secondary file)."""
+    out = dict(roof)
+    for k in ("kernel", "alg_model", "counters"):
+        if isinstance(out.get(k), str) and len(out[k]) > 200:
+            out[k] = out[k][:197] + "..."
+    return out
+
+
+def headline(base, roof, cpu, summary, ranks=None, secondary_path=None):
+    """The one JSON line the driver parses: the contract's keys, roofline,
+    cpu_baseline and summary; secondary sections go to a file (named here).
+    Raises if the line would not fit the driver's tail."""
+    line = {k: base[k] for k in HEADLINE_KEYS if k in base and k not in ("roofline", "cpu_baseline")}
+    line["roofline"] = compact_roofline(roof)
+    line["cpu_baseline"] = compact_cpu_baseline(cpu)
+    for k in ("kernel_ms", "verdicts_ok", "build"):
+        if k in base:
+            line[k] = base[k]
+    if ranks is not None:
+        line["ranks"] = ranks
+    line["secondary_file"] = secondary_path
+    line["summary"] = summary
+    s = json.dumps(line)
+    if len(s) > HEADLINE_MAX_BYTES:
+        # drop summary entries from the end until it fits (never the contract keys)
+        keys = list(summary or {})
+        while len(s) > HEADLINE_MAX_BYTES and keys:
+            summary.pop(keys.pop())
+            summary["truncated"] = True
+            s = json.dumps(line)
+    if len(s) > HEADLINE_MAX_BYTES:
+        raise ValueError(f"headline line is {len(s)} B > {HEADLINE_MAX_BYTES}")
+    return line
+
+
+def main(argv=None):
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's `bench.py --gpus N` (no torchrun): one child per GPU
+        raise SystemExit(spawn_ranks(args.gpus, rank_argv(sys.argv[1:] if argv is None else list(argv))))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -1589,6 +1722,9 @@ def main():
         local = 0
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    if local >= torch.cuda.device_count():
+        raise SystemExit(f"rank {rank}: device {local} requested, {torch.cuda.device_count()} visible "
+                         f"(--gpus larger than the node; COA_BENCH_ONE_DEVICE=1 rehearses on one GPU)")
     torch.cuda.set_device(local)  # one process per GPU
     dev = torch.device("cuda", local)
     if world > 1:
@@ -1651,13 +1787,20 @@ def main():
         torch.cuda.synchronize()
     # every verdict set to Err right before the timed steps: verdicts_ok then
     # reports what the timed calls themselves wrote
+    rank_elapsed = []
     elapsed = timed_steps(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize,
-                          before_timed=lambda: verdicts.fill_(1))
+                          before_timed=lambda: verdicts.fill_(1), local_out=rank_elapsed)
     if args.per_call_events:
         verify_ms = sum(a.elapsed_time(b) for a, b in per_call) / args.steps
     else:
         verify_ms = ev0.elapsed_time(ev1) / args.steps  # per call, HIP events on the calls' stream
     ok = int(verdicts.sum().item()) == 0
+    props = torch.cuda.get_device_properties(local)
+    ranks = gather_ranks({"rank": rank, "device": local,
+                          "pci_bus": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
+                          "index_range": [base, base + n], "verify_per_s": round(n * args.steps / rank_elapsed[0], 1),
+                          "verify_call_ms": round(verify_ms, 4), "verdicts_ok": ok}, world, dist)
+    ok = all(r["verdicts_ok"] for r in ranks)
 
     total = n * world * args.steps
     value = total / elapsed
@@ -1742,7 +1885,7 @@ def main():
         section("host_e2e", lambda: host_e2e(local, dev, msgs_h, pks.cpu().numpy(), sigs.cpu().numpy()))
 
     if rank == 0:
-        line = {
+        base = {
             "metric": "ed25519 verifications/sec",
             "value": round(value, 1),
             "unit": "verifications/s",
@@ -1760,14 +1903,22 @@ def main():
                        "triples_per_gpu": n, "parallelism": f"index-range shards x{world}"},
             "kernel_ms": {"verify_call": round(verify_ms, 4)},
             "verdicts_ok": ok,
-            "env": HIP_ENV_AT_START,
             "build": build_identity(),
-            "roofline": roof,
-            "cpu_baseline": cpu,
-            "secondary": secondary,
-            # last key: the driver keeps only the tail of the line
-            "summary": summarize(value, secondary, cpu),
         }
+        summary = summarize(value, secondary, cpu)
+        sec_path = None
+        if secondary is not None:
+            # everything else to a file: the driver parses only the last line
+            # of stdout, and round 5's 37.6 KB line (secondary inline) was not
+            # parsed at all
+            sec_path = args.secondary_out
+            full = dict(base, env=HIP_ENV_AT_START, roofline=roof, cpu_baseline=cpu, ranks=ranks,
+                        secondary=secondary, summary=summary)
+            d = os.path.dirname(os.path.join(ROOT, sec_path))
+            os.makedirs(d, exist_ok=True)
+            with open(os.path.join(ROOT, sec_path), "w") as f:
+                json.dump(full, f)
+        line = headline(base, roof, cpu, summary, ranks=ranks, secondary_path=sec_path)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -238,7 +238,9 @@ int coa_certificate_verify(const uint8_t* header_data, size_t header_len, const 
  * (coa_ed25519_verify_batch_groups) and 16 = a key is not registered (use the
  * uncached entry points).  The host-pointer calls above resolve both.
  * `workspace`: NULL (engine-owned; the call then waits for its stream) or
- * coa_certificate_workspace_bytes(n, n_votes) bytes of device memory. */
+ * coa_certificate_workspace_bytes(n, n_votes) bytes of device memory.  A
+ * call of >= 16,384 jobs (certificates + votes) takes its jobs in committee-key
+ * order, and the size then includes the sort's area (~4.2 MB + 8 B per job). */
 size_t coa_certificate_workspace_bytes(size_t n, size_t n_votes);
 int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data, const uint64_t* d_header_offsets,
                                        const uint8_t* d_ids, const uint8_t* d_origins, const uint8_t* d_header_sigs,

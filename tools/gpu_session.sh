@@ -1,11 +1,11 @@
 #!/bin/bash
 # One parameterised GPU-session script (it replaces round 3's 26 one-off
 # tools/gpu_r3_*.sh compositions): tools/gpu_session.sh <step> [args]
-#   env              box environment relevant to HIP queues -> gpurun_out/r4_env.txt
-#   hwq              hardware-queue probe matrix (tools/hwq_probe) -> r4_hwq.jsonl
-#   tests [ARGS]     the GPU test suite (pytest -m gpu ARGS) -> r4_tests.log
+#   env              box environment relevant to HIP queues -> gpurun_out/${R:-r6}_env.txt
+#   hwq              hardware-queue probe matrix (tools/hwq_probe) -> ${R:-r6}_hwq.jsonl
+#   tests [ARGS]     the GPU test suite (pytest -m gpu ARGS) -> ${R:-r6}_tests.log
 #   bench HQ TAG ARGS  bench.py ARGS with GPU_MAX_HW_QUEUES=HQ ("-": as the box
-#                    has it) -> r4_bench_TAG.json
+#                    has it) -> ${R:-r6}_bench_TAG.json
 #   ab ENVS [N]      same-box A/B of runtime switches on the C2 line
 #                    (tools/ab_env.sh; ENVS="name=VAR=value ... default")
 #   probe SCRIPT ARGS  a tools/ probe under its own time limit
@@ -22,11 +22,11 @@ step=$1
 shift
 case "$step" in
   env)
-    env | grep -E '^(GPU_|HIP_|HSA_|ROC|AMD_|OMP_)' | sort > gpurun_out/r4_env.txt
-    (nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null) >> gpurun_out/r4_env.txt
+    env | grep -E '^(GPU_|HIP_|HSA_|ROC|AMD_|OMP_)' | sort > gpurun_out/${R:-r6}_env.txt
+    (nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null) >> gpurun_out/${R:-r6}_env.txt
     ;;
   hwq)
-    out=gpurun_out/r4_hwq.jsonl
+    out=gpurun_out/${R:-r6}_hwq.jsonl
     : > $out
     for hq in unset 4 8; do
       for kind in plain cumask hi lo; do
@@ -45,13 +45,13 @@ case "$step" in
     tag=$2
     shift 2
     if [ "$hq" = "-" ]; then
-      timeout -k 10 400 python -u bench.py "$@" > gpurun_out/r4_bench_$tag.json 2> gpurun_out/r4_bench_$tag.err || exit 1
+      timeout -k 10 400 python -u bench.py "$@" > gpurun_out/${R:-r6}_bench_$tag.json 2> gpurun_out/${R:-r6}_bench_$tag.err || exit 1
     else
-      GPU_MAX_HW_QUEUES=$hq timeout -k 10 400 python -u bench.py "$@" > gpurun_out/r4_bench_$tag.json 2> gpurun_out/r4_bench_$tag.err || exit 1
+      GPU_MAX_HW_QUEUES=$hq timeout -k 10 400 python -u bench.py "$@" > gpurun_out/${R:-r6}_bench_$tag.json 2> gpurun_out/${R:-r6}_bench_$tag.err || exit 1
     fi
     ;;
   tests)
-    timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > gpurun_out/r4_tests.log 2>&1 || exit 1
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > gpurun_out/${R:-r6}_tests.log 2>&1 || exit 1
     ;;
   ab)
     ENVS="$1" N=${2:-65536} REPS=${REPS:-3} bash tools/ab_env.sh || exit 1

@@ -150,9 +150,21 @@ hipError_t coa_launch_key_wcombs20(const uint32_t* tabs, uint32_t nk, uint32_t* 
 // lanes_per_sig: 64 (latency: two waves per signature, comb terms split over
 // a wave's lanes and summed by a butterfly) or 1 (throughput: K signatures
 // per lane, K from the job count).
-// pscr: device scratch of coa_cert_scratch_bytes(nc + nv) bytes (throughput
-// variant only; may be null for lanes_per_sig == 64).
-size_t coa_cert_scratch_bytes(uint64_t jobs);
+// pscr: device scratch of coa_cert_scratch_bytes(nc + nv, a.key_order)
+// bytes (throughput variant only; may be null for lanes_per_sig == 64).
+size_t coa_cert_scratch_bytes(uint64_t jobs, bool key_order);
+
+// coa_certificate_verify_many_device with the job order chosen by the caller:
+// key_order 1 (the public device-resident round) sorts a call of >= 16,384
+// jobs by committee key, 0 keeps certificate order (the aggregation queue's
+// windows: concurrent windows lost more to the sort's launches than the order
+// gained, profiles/r05_cert_keysort_ab.txt).  The workspace must hold
+// coa_cert_scratch_bytes(n + n_votes, key_order) bytes.
+extern "C" int coa_certificate_verify_many_device_order(
+    int device, const uint8_t* d_header_data, const uint64_t* d_header_offsets, const uint8_t* d_ids,
+    const uint8_t* d_origins, const uint8_t* d_header_sigs, const uint64_t* d_rounds, const uint8_t* d_vote_pks,
+    const uint8_t* d_vote_sigs, const uint64_t* d_vote_offsets, size_t n, size_t n_votes, uint32_t* d_status,
+    void* workspace, void* stream, int key_order);
 hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr, hipStream_t s);
 
 // Row-parallel field arithmetic (coa_fe_wave.h) against coa_fe.h, one wave per

@@ -872,6 +872,8 @@ hipError_t coa_launch_cert_verify_inl(const CertInl& ci, hipStream_t s) {
 // arbitrary: every job's verdict depends on its own inputs only.
 #define COA_SORT_BINS 4096
 #define COA_SORT_WGS 256
+// smallest call the key-order sort pays for (its three launches)
+#define COA_SORT_MIN_JOBS 16384
 __global__ void __launch_bounds__(256) k_job_count(CertArgs a, uint32_t bins, uint32_t per,
                                                    uint32_t* __restrict__ total, uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ bin) {
@@ -948,12 +950,16 @@ static size_t cert_slab_bytes(uint64_t jobs, uint64_t lanes) {
   return (size_t)(lanes * cert_tp_jcap(jobs, lanes) * PSCR_ROWS * 16);
 }
 
-// ... | key-order sort: bin totals / cursors [COA_SORT_BINS], counts
+// ... | key-order sort, only for a call that may sort (key_order and at
+// least COA_SORT_MIN_JOBS jobs): bin totals / cursors [COA_SORT_BINS], counts
 // [COA_SORT_WGS][COA_SORT_BINS], each job's bin [jobs], the permutation [jobs]
-size_t coa_cert_scratch_bytes(uint64_t jobs) {
+// (~4.2 MB + 8 B per job; a latency, pipelined-chunk or queue workspace does
+// not carry it)
+size_t coa_cert_scratch_bytes(uint64_t jobs, bool key_order) {
   const uint64_t lanes = cert_tp_lanes(jobs ? jobs : 1);
-  return 256 + cert_slab_bytes(jobs, lanes) + (size_t)(jobs ? jobs : 1) * 32 + 256 +
-         (size_t)COA_SORT_BINS * (COA_SORT_WGS + 1) * 4 + (size_t)(jobs ? jobs : 1) * 8;
+  const size_t base = 256 + cert_slab_bytes(jobs, lanes) + (size_t)(jobs ? jobs : 1) * 32;
+  if (!key_order || jobs < COA_SORT_MIN_JOBS) return base;
+  return base + 256 + (size_t)COA_SORT_BINS * (COA_SORT_WGS + 1) * 4 + (size_t)jobs * 8;
 }
 
 hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr, hipStream_t s) {
@@ -987,7 +993,8 @@ hipError_t coa_launch_cert_verify(CertArgs a, int lanes_per_sig, uint32_t* pscr,
   // chunks nor the queue's windows, whose concurrent launches lost more to
   // the sort's own launches than the order gained (profiles/r05_cert_keysort_ab.txt)
   const char* ks = getenv("COA_CERT_KEYSORT");
-  if (a.key_order && a.nk > 0 && a.nk + 1 <= COA_SORT_BINS && jobs >= 16384 && !(ks && ks[0] == '0' && ks[1] == 0)) {
+  if (a.key_order && a.nk > 0 && a.nk + 1 <= COA_SORT_BINS && jobs >= COA_SORT_MIN_JOBS &&
+      !(ks && ks[0] == '0' && ks[1] == 0)) {
     uint32_t* total = pscr + 64 + cert_slab_bytes(jobs, lanes) / 4 + (size_t)jobs * 8 + 64;
     uint32_t* counts = total + COA_SORT_BINS;
     uint32_t* bin = counts + (size_t)COA_SORT_BINS * COA_SORT_WGS;

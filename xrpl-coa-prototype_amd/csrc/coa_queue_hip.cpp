@@ -151,10 +151,62 @@ void bury(std::vector<Grave>& grave) {
   grave.clear();
 }
 
+// Process-wide pool of the slots' streams.  Every queue used to create its
+// slots' streams and destroy them with the queue: a CU-masked stream is a
+// hardware queue of its own, so a process that makes many queues (bench.py
+// makes ~40) created and tore down ~500 hardware queues.  Under
+// `rocprofv3 --kernel-trace` that ended in a SIGSEGV at address 0x34 inside
+// hipExtStreamCreateWithCUMask (round 5, gpurun_out/fullprof.err: stack
+// make_stream <- HipBackend::ready <- coa_queue_create <-
+// latc_stream_certificates, late in the run; the same section alone
+// profiled clean).  A healthy slot's stream now returns here when its queue
+// is destroyed and the next queue takes it, so a process holds at most the
+// streams of the queues alive at once, and a later queue also skips the
+// first-dispatch cost of a new hardware queue (~25-75 ms for a CU-masked
+// one).  A stream whose window failed is destroyed, never pooled.
+struct PooledStream {
+  int dev, kind, prio;
+  hipStream_t s;
+};
+std::mutex g_pool_mu;
+std::vector<PooledStream>& stream_pool() {
+  static auto* pool = new std::vector<PooledStream>();  // never destroyed: streams outlive static teardown
+  return *pool;
+}
+int slot_prio(const Slot& sl) { return sl.kind == COA_QUEUE_STREAM_PRIORITY && sl.lane == coa_q::LANE_VERIFY; }
+hipStream_t pool_take(const Slot& sl) {
+  std::lock_guard<std::mutex> l(g_pool_mu);
+  auto& pool = stream_pool();
+  for (size_t i = 0; i < pool.size(); i++)
+    if (pool[i].dev == sl.dev && pool[i].kind == sl.kind && pool[i].prio == slot_prio(sl)) {
+      const hipStream_t s = pool[i].s;
+      pool[i] = pool.back();
+      pool.pop_back();
+      return s;
+    }
+  return nullptr;
+}
+// Hands a slot's stream to the pool (drained first); a stream that does not
+// drain cleanly is destroyed instead.
+void pool_give(Slot& sl) {
+  if (!sl.s) return;
+  if (hipStreamSynchronize(sl.s) == hipSuccess && hipStreamQuery(sl.s) == hipSuccess) {
+    std::lock_guard<std::mutex> l(g_pool_mu);
+    stream_pool().push_back({sl.dev, sl.kind, slot_prio(sl), sl.s});
+  } else {
+    (void)hipStreamDestroy(sl.s);
+    (void)hipGetLastError();
+  }
+  sl.s = nullptr;
+}
+
 // New stream and event for a slot; its device buffers are freed (regrown by
-// the next launch).  The pinned host blocks are kept.
+// the next launch).  The pinned host blocks are kept.  A slot without a
+// stream takes one from the pool when one of its kind is there; a slot being
+// rebuilt after a failed window gets a fresh one.
 int make_stream(Slot& sl) {
   if (hipSetDevice(sl.dev) != hipSuccess) return COA_EHIP;
+  const bool rebuild = sl.s != nullptr;
   if (sl.s) {
     (void)hipStreamSynchronize(sl.s);
     (void)hipStreamDestroy(sl.s);
@@ -172,8 +224,11 @@ int make_stream(Slot& sl) {
   sl.cap_din = sl.cap_dout = sl.cap_ws = 0;
   bury(sl.grave);
   (void)hipGetLastError();  // a failed launch's error is not sticky for the new stream
-  hipError_t e;
-  if (sl.kind == COA_QUEUE_STREAM_CUMASK) {
+  hipError_t e = hipSuccess;
+  if (!rebuild) sl.s = pool_take(sl);
+  if (sl.s) {
+    // pooled
+  } else if (sl.kind == COA_QUEUE_STREAM_CUMASK) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, sl.dev) != hipSuccess || cus <= 0)
       return COA_EHIP;
@@ -191,9 +246,16 @@ int make_stream(Slot& sl) {
   return COA_OK;
 }
 
+// True when rocprofv3's tool library is loaded into this process (the
+// environment rocprofv3 gives the program it runs).  The slots then use plain
+// streams: CU-masked stream creation under its tracer is what faulted in
+// round 5 (see stream_pool), and the kernels -- what a profile measures --
+// are the same on either kind.
+bool under_rocprofiler() { return getenv("ROCP_TOOL_LIBRARIES") || getenv("ROCPROFILER_LIBRARY_CTOR"); }
+
 int stream_kind_env() {
   const char* e = getenv("COA_QUEUE_STREAMS");
-  if (!e) return COA_QUEUE_STREAM_CUMASK;
+  if (!e) return under_rocprofiler() ? COA_QUEUE_STREAM_PLAIN : COA_QUEUE_STREAM_CUMASK;
   const std::string v(e);
   if (v == "plain") return COA_QUEUE_STREAM_PLAIN;
   if (v == "priority") return COA_QUEUE_STREAM_PRIORITY;
@@ -212,7 +274,7 @@ void free_slot(Slot& sl) {
   if (sl.lres) (void)hipHostFree(sl.lres);
   if (sl.dctr) (void)hipFree(sl.dctr);
   if (sl.ev) (void)hipEventDestroy(sl.ev);
-  if (sl.s) (void)hipStreamDestroy(sl.s);
+  pool_give(sl);
   bury(sl.grave);
 }
 
@@ -258,7 +320,7 @@ class HipBackend : public coa_q::Backend {
     const size_t pre_ws = lane_ == coa_q::LANE_DIGEST
                               ? 256
                               : std::max(coa_verify_workspace_bytes(items),
-                                         coa_certificate_workspace_bytes(items / 68 + 1, items)) + 256;
+                                         coa_cert_scratch_bytes(items / 68 + 1 + items, false)) + 256;
     for (Slot& sl : slots_) {
       if (lane_ == coa_q::LANE_VERIFY && hipSetDevice(sl.dev) == hipSuccess) {
         (void)lat_words(sl);
@@ -450,7 +512,7 @@ class HipBackend : public coa_q::Backend {
     sl.o_d = take(L.nd * 64);
     const size_t out_bytes = o;
     const size_t ws_v = L.nv ? coa_verify_workspace_bytes(L.nv) : 0;
-    const size_t ws_c = L.nc ? coa_certificate_workspace_bytes(L.nc, L.nvotes) : 0;
+    const size_t ws_c = L.nc ? coa_cert_scratch_bytes(L.nc + L.nvotes, false) : 0;
     const size_t caps0 = sl.cap_hin + sl.cap_hout + sl.cap_din + sl.cap_dout + sl.cap_ws;
     if (grow_pinned(sl.hin, sl.cap_hin, in_bytes, sl.grave) != hipSuccess ||
         grow_pinned(sl.hout, sl.cap_hout, out_bytes, sl.grave) != hipSuccess ||
@@ -589,11 +651,12 @@ class HipBackend : public coa_q::Backend {
       rc = coa_ed25519_verify_strict_many_device(sl.dev, d + i_vm, 32, d + i_vp, d + i_vs, L.nv, dout + sl.o_v, sl.ws,
                                                  sl.s);
     if (rc == COA_OK && L.nc) {
-      rc = coa_certificate_verify_many_device(
+      // certificate order (no key sort): see coa_certificate_verify_many_device_order
+      rc = coa_certificate_verify_many_device_order(
           sl.dev, d + i_ch, reinterpret_cast<const uint64_t*>(d + i_cho), d + i_cid, d + i_cor, d + i_chs,
           reinterpret_cast<const uint64_t*>(d + i_crd), d + i_cvp, d + i_cvs,
           reinterpret_cast<const uint64_t*>(d + i_cvo), L.nc, L.nvotes, reinterpret_cast<uint32_t*>(dout + sl.o_c),
-          sl.ws, sl.s);
+          sl.ws, sl.s, 0);
     }
     if (rc == COA_OK && L.nd)
       rc = coa_sha512_many_device(sl.dev, d + i_dd, reinterpret_cast<const uint64_t*>(d + i_do), L.nd, dout + sl.o_d,

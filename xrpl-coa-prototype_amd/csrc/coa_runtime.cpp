@@ -1408,7 +1408,7 @@ int cert_shard_pipelined(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_
     const CertPack p = cert_layout(nc, nv, hb);
     HIP_TRY(d.pinc[b].ensure(p.total));
     HIP_TRY(d.certc[b].ensure(p.total));
-    HIP_TRY(d.cscrc[b].ensure(coa_cert_scratch_bytes(nc + nv)));
+    HIP_TRY(d.cscrc[b].ensure(coa_cert_scratch_bytes(nc + nv, pipe_keysort())));
     uint8_t* h = static_cast<uint8_t*>(d.pinc[b].p);
     const double t0 = trace ? now() : 0;
     cert_pack(h, p, in, clo, chi);
@@ -1464,7 +1464,7 @@ int cert_shard(Dev& d, const CertIn& in, size_t lo, size_t hi, uint32_t* status_
     HIP_TRY(coa_launch_cert_verify(a, lanes, nullptr, s));
     return lat_res_wait(d, s, nc, tag, status_out + lo);
   }
-  if (lanes == 1) HIP_TRY(d.cscr.ensure(coa_cert_scratch_bytes(nc + nv)));
+  if (lanes == 1) HIP_TRY(d.cscr.ensure(coa_cert_scratch_bytes(nc + nv, a.key_order != 0)));
   HIP_TRY(coa_launch_cert_verify(a, lanes, d.cscr.as<uint32_t>(), s));
   HIP_TRY(hipMemcpyAsync(h + p.status, d.cert.as<uint8_t>() + p.status, nc * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -2406,13 +2406,28 @@ int coa_certificate_resolve_raw(const uint8_t* ids, const uint8_t* origins, cons
   return COA_OK;
 }
 
-size_t coa_certificate_workspace_bytes(size_t n, size_t n_votes) { return coa_cert_scratch_bytes(n + n_votes); }
+size_t coa_certificate_workspace_bytes(size_t n, size_t n_votes) {
+  return coa_cert_scratch_bytes(n + n_votes, true);  // the public device call sorts by key
+}
 
 int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data, const uint64_t* d_header_offsets,
                                        const uint8_t* d_ids, const uint8_t* d_origins, const uint8_t* d_header_sigs,
                                        const uint64_t* d_rounds, const uint8_t* d_vote_pks,
                                        const uint8_t* d_vote_sigs, const uint64_t* d_vote_offsets, size_t n,
                                        size_t n_votes, uint32_t* d_status, void* workspace, void* stream) {
+  // one device-resident round: jobs in key order
+  return coa_certificate_verify_many_device_order(device, d_header_data, d_header_offsets, d_ids, d_origins,
+                                                  d_header_sigs, d_rounds, d_vote_pks, d_vote_sigs, d_vote_offsets, n,
+                                                  n_votes, d_status, workspace, stream, 1);
+}
+
+int coa_certificate_verify_many_device_order(int device, const uint8_t* d_header_data,
+                                             const uint64_t* d_header_offsets, const uint8_t* d_ids,
+                                             const uint8_t* d_origins, const uint8_t* d_header_sigs,
+                                             const uint64_t* d_rounds, const uint8_t* d_vote_pks,
+                                             const uint8_t* d_vote_sigs, const uint64_t* d_vote_offsets, size_t n,
+                                             size_t n_votes, uint32_t* d_status, void* workspace, void* stream,
+                                             int key_order) {
   int rc = ensure_init();
   if (rc != COA_OK) return rc;
   if (n == 0) return COA_OK;
@@ -2447,7 +2462,7 @@ int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data,
   a.kwtabs = (ks->kwide && !env_is("COA_KEY_WCOMB", "0")) ? ks->kwtabs.as<uint32_t>() : nullptr;
   a.kw20 = ks->kw20 ? 1u : 0u;
   a.status = d_status;
-  a.key_order = 1;  // one device-resident round: jobs in key order
+  a.key_order = key_order ? 1u : 0u;
   const int lanes = cert_lanes(n + n_votes);
   HIP_TRY(hipMemsetAsync(d_status, 0, n * 4, s));
   if (workspace || lanes == 64) {
@@ -2455,7 +2470,7 @@ int coa_certificate_verify_many_device(int device, const uint8_t* d_header_data,
     return COA_OK;
   }
   std::lock_guard<std::mutex> l(d->mu);
-  HIP_TRY(d->cscr.ensure(coa_cert_scratch_bytes(n + n_votes)));
+  HIP_TRY(d->cscr.ensure(coa_cert_scratch_bytes(n + n_votes, a.key_order != 0)));
   HIP_TRY(coa_launch_cert_verify(a, lanes, d->cscr.as<uint32_t>(), s));
   HIP_TRY(hipStreamSynchronize(s));  // engine-owned workspace: drain before release
   return COA_OK;
