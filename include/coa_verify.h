@@ -14,7 +14,9 @@
  *     DagError::InvalidSignature).
  *   - Return codes: COA_OK (0) / COA_REJECT (1) for single verdicts; COA_OK for
  *     a completed many-call; a negative COA_E* on internal failure.  There is
- *     NO CPU fallback: with no usable GPU every call returns COA_ENODEVICE.
+ *     NO implicit CPU fallback: with no usable GPU every GPU call returns
+ *     COA_ENODEVICE.  The engine's own CPU path (coa_cpu_*, below) answers
+ *     only when a caller calls it explicitly.
  *   - Host-pointer calls: inputs are caller-owned and only read during the
  *     call; outputs are caller-allocated.  Nothing is retained after return.
  *   - Thread safety: every call takes the engine lock of the devices it uses;
@@ -295,6 +297,41 @@ int coa_ed25519_sign_many(const uint8_t* seeds, const uint8_t* msgs, size_t msg_
                           uint8_t* sigs_out);
 int coa_ed25519_sign_many_device(int device, const uint8_t* d_seeds, const uint8_t* d_msgs, size_t msg_len, size_t n,
                                  uint8_t* d_pks_out, uint8_t* d_sigs_out, void* stream);
+
+/* ------------------------------------------ the engine's own CPU path
+ * The same checks as the GPU entry points above, on the host's cores
+ * (csrc/coa_cpu.cpp; dalek 1.0.1 acceptance rules, verdict for verdict).
+ * NEVER called implicitly: a GPU entry point that cannot answer returns a
+ * negative COA_E*.  A caller that must keep answering calls these explicitly
+ * -- the Rust binding does under COA_ON_ENGINE_FAILURE=cpu
+ * (rust/crypto/src/degrade.rs), so verdicts do not depend on device health
+ * (SURVEY.md §5).  nthreads <= 0: min(16, hardware threads).  Same return
+ * conventions as the GPU forms; no coa_init needed.
+ *   coa_cpu_ed25519_verify_strict      crypto/src/lib.rs:200-204
+ *   coa_cpu_ed25519_verify_batch[_groups_z]  crypto/src/lib.rs:206-219
+ *                                      (rng_seed as coa_ed25519_verify_batch)
+ *   coa_cpu_sha512_many                worker/src/processor.rs:38,
+ *                                      primary/src/messages.rs:70-84,226-234
+ *   coa_cpu_certificate_verify_many[_z]  primary/src/messages.rs:189-215
+ *                                      (status_out: COA_CERT_* bits; _z takes
+ *                                      the votes' 16-byte weights) */
+int coa_cpu_ed25519_verify_strict(const uint8_t* msg, size_t msg_len, const uint8_t pk[32], const uint8_t sig[64]);
+int coa_cpu_ed25519_verify_strict_many(const uint8_t* msgs, size_t msg_len, const uint8_t* pks, const uint8_t* sigs,
+                                       size_t n, uint8_t* verdicts_out, int nthreads);
+int coa_cpu_ed25519_verify_batch(const uint8_t msg[32], const uint8_t* pks, const uint8_t* sigs, size_t n,
+                                 uint64_t rng_seed);
+int coa_cpu_ed25519_verify_batch_groups_z(const uint8_t* msgs, const uint8_t* pks, const uint8_t* sigs,
+                                          const uint64_t* group_offsets, size_t n_groups, const uint8_t* zs,
+                                          uint8_t* group_verdicts_out, int nthreads);
+int coa_cpu_sha512_many(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out64, int nthreads);
+int coa_cpu_certificate_verify_many(const uint8_t* header_data, const uint64_t* header_offsets, const uint8_t* ids,
+                                    const uint8_t* origins, const uint8_t* header_sigs, const uint64_t* rounds,
+                                    const uint8_t* vote_pks, const uint8_t* vote_sigs, const uint64_t* vote_offsets,
+                                    size_t n, uint64_t rng_seed, uint8_t* status_out, int nthreads);
+int coa_cpu_certificate_verify_many_z(const uint8_t* header_data, const uint64_t* header_offsets, const uint8_t* ids,
+                                      const uint8_t* origins, const uint8_t* header_sigs, const uint64_t* rounds,
+                                      const uint8_t* vote_pks, const uint8_t* vote_sigs, const uint64_t* vote_offsets,
+                                      size_t n, const uint8_t* zs, uint8_t* status_out, int nthreads);
 
 /* ------------------------------------------------ aggregation queue (f1)
  * Pre-verification stage for Core::run (primary/src/core.rs:349-389), which

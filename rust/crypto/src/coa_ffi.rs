@@ -173,6 +173,28 @@ extern "C" {
                                         n: usize, d_pks_out: *mut u8, d_sigs_out: *mut u8,
                                         stream: *mut c_void) -> c_int;
 
+    // ------------------------------------------ the engine's own CPU path
+    // explicit only: degrade.rs calls these after an engine failure
+    pub fn coa_cpu_ed25519_verify_strict(msg: *const u8, msg_len: usize, pk: *const u8, sig: *const u8) -> c_int;
+    pub fn coa_cpu_ed25519_verify_strict_many(msgs: *const u8, msg_len: usize, pks: *const u8, sigs: *const u8,
+                                              n: usize, verdicts_out: *mut u8, nthreads: c_int) -> c_int;
+    pub fn coa_cpu_ed25519_verify_batch(msg: *const u8, pks: *const u8, sigs: *const u8, n: usize,
+                                        rng_seed: u64) -> c_int;
+    pub fn coa_cpu_ed25519_verify_batch_groups_z(msgs: *const u8, pks: *const u8, sigs: *const u8,
+                                                 group_offsets: *const u64, n_groups: usize, zs: *const u8,
+                                                 group_verdicts_out: *mut u8, nthreads: c_int) -> c_int;
+    pub fn coa_cpu_sha512_many(data: *const u8, offsets: *const u64, n: usize, out64: *mut u8,
+                               nthreads: c_int) -> c_int;
+    pub fn coa_cpu_certificate_verify_many(header_data: *const u8, header_offsets: *const u64, ids: *const u8,
+                                           origins: *const u8, header_sigs: *const u8, rounds: *const u64,
+                                           vote_pks: *const u8, vote_sigs: *const u8, vote_offsets: *const u64,
+                                           n: usize, rng_seed: u64, status_out: *mut u8, nthreads: c_int) -> c_int;
+    pub fn coa_cpu_certificate_verify_many_z(header_data: *const u8, header_offsets: *const u64, ids: *const u8,
+                                             origins: *const u8, header_sigs: *const u8, rounds: *const u64,
+                                             vote_pks: *const u8, vote_sigs: *const u8, vote_offsets: *const u64,
+                                             n: usize, zs: *const u8, status_out: *mut u8,
+                                             nthreads: c_int) -> c_int;
+
     // ------------------------------------------------- aggregation queue (f1)
     pub fn coa_queue_create(max_batch: usize, max_delay_us: u32) -> *mut CoaQueue;
     pub fn coa_queue_submit_verify(q: *mut CoaQueue, msg: *const u8, pk: *const u8, sig: *const u8,

@@ -30,8 +30,8 @@ use crate::{CryptoError, Digest, PublicKey};
 /// GPU, bad arguments, or a HIP error that persisted after the engine rebuilt
 /// the failing context and re-ran the work on every other context,
 /// coa_engine_recoveries).  A failure never turns into a verdict: the caller
-/// answers with the reference's own code (degrade.rs), or panics under
-/// COA_ON_ENGINE_FAILURE=panic.
+/// answers with the engine's own CPU path (degrade.rs, coa_cpu_*), or panics
+/// under COA_ON_ENGINE_FAILURE=panic.
 fn verdict(rc: i32, what: &str) -> Option<Result<(), CryptoError>> {
     match rc {
         ffi::COA_OK => Some(Ok(())),
@@ -51,7 +51,7 @@ pub fn signature_bytes(signature: &crate::Signature) -> [u8; 64] {
 }
 
 /// true when the engine answered; false after reporting its failure (the
-/// caller then answers with the reference's own code, degrade.rs)
+/// caller then answers with the engine's CPU path, degrade.rs)
 fn engine_ok(rc: i32, what: &str) -> bool {
     if rc >= 0 {
         return true;
@@ -70,7 +70,7 @@ pub fn verify(signature: &[u8; 64], digest: &Digest, public_key: &PublicKey) -> 
         return if ok { Ok(()) } else { Err(CryptoError::new()) };
     }
     let rc = unsafe { ffi::coa_ed25519_verify_strict(digest.0.as_ptr(), public_key.0.as_ptr(), signature.as_ptr()) };
-    verdict(rc, "Signature::verify").unwrap_or_else(|| degrade::verify_strict(signature, digest, public_key))
+    verdict(rc, "Signature::verify").unwrap_or_else(|| degrade::cpu_verify(signature, digest, public_key))
 }
 
 /// Signature::verify_batch (crypto/src/lib.rs:206-219): dalek 1.0.1
@@ -87,7 +87,7 @@ where
         sigs.extend_from_slice(sig);
     }
     let rc = unsafe { ffi::coa_ed25519_verify_batch(digest.0.as_ptr(), pks.as_ptr(), sigs.as_ptr(), votes.len(), 0) };
-    verdict(rc, "Signature::verify_batch").unwrap_or_else(|| degrade::verify_batch(digest, &votes))
+    verdict(rc, "Signature::verify_batch").unwrap_or_else(|| degrade::cpu_verify_batch(digest, &votes))
 }
 
 /// Digest(Sha512(bytes)[..32]) of ONE message on the device.  One 508 KB
@@ -101,7 +101,7 @@ pub fn sha512_digest(bytes: &[u8]) -> Digest {
     let mut out = [0u8; 32];
     if !engine_ok(unsafe { ffi::coa_sha512_trunc32_many(bytes.as_ptr(), offsets.as_ptr(), 1, out.as_mut_ptr()) },
                   "Sha512 digest") {
-        return degrade::sha512_digest(bytes);
+        return degrade::cpu_digest(bytes);
     }
     Digest(out)
 }
@@ -119,7 +119,7 @@ pub fn sha512_digests(messages: &[&[u8]]) -> Vec<Digest> {
     if !engine_ok(unsafe {
         ffi::coa_sha512_trunc32_many(data.as_ptr(), offsets.as_ptr(), messages.len(), out.as_mut_ptr())
     }, "Sha512 digests") {
-        return messages.iter().map(|m| degrade::sha512_digest(m)).collect();
+        return messages.iter().map(|m| degrade::cpu_digest(m)).collect();
     }
     out.chunks_exact(32)
         .map(|c| {
@@ -157,7 +157,7 @@ pub fn verify_many(items: &[(Digest, PublicKey, [u8; 64])]) -> Vec<Result<(), Cr
     if !engine_ok(unsafe {
         ffi::coa_ed25519_verify_strict_many(msgs.as_ptr(), 32, pks.as_ptr(), sigs.as_ptr(), n, out.as_mut_ptr())
     }, "Signature::verify (many)") {
-        return items.iter().map(|(d, k, s)| degrade::verify_strict(s, d, k)).collect();
+        return items.iter().map(|(d, k, s)| degrade::cpu_verify(s, d, k)).collect();
     }
     out.into_iter().map(|v| if v == 0 { Ok(()) } else { Err(CryptoError::new()) }).collect()
 }
@@ -184,7 +184,7 @@ pub fn verify_batch_groups(digests: &[Digest], groups: &[Vec<(PublicKey, [u8; 64
         ffi::coa_ed25519_verify_batch_groups(msgs.as_ptr(), pks.as_ptr(), sigs.as_ptr(), offsets.as_ptr(),
                                              groups.len(), out.as_mut_ptr(), 0)
     }, "Signature::verify_batch (groups)") {
-        return digests.iter().zip(groups).map(|(d, g)| degrade::verify_batch(d, g)).collect();
+        return digests.iter().zip(groups).map(|(d, g)| degrade::cpu_verify_batch(d, g)).collect();
     }
     out.into_iter().map(|v| if v == 0 { Ok(()) } else { Err(CryptoError::new()) }).collect()
 }

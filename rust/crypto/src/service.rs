@@ -138,9 +138,13 @@ type DigestReply = Result<(Digest, Vec<u8>), (c_int, Vec<u8>)>;
 /// the `verified` key without a copy) -- or with the engine's failure status.
 type CertificateReply = Result<(u8, CertificateCrypto), (c_int, CertificateCrypto)>;
 
+/// A vote batch's verdict -- or the engine's failure status with the votes
+/// handed back (for the CPU answer: no copy kept on the success path).
+type BatchReply = Result<Result<(), CryptoError>, (c_int, Vec<(PublicKey, [u8; 64])>)>;
+
 enum Request {
     Verify(Digest, PublicKey, [u8; 64], oneshot::Sender<Verdict>),
-    Batch(Digest, Vec<(PublicKey, [u8; 64])>, oneshot::Sender<Verdict>),
+    Batch(Digest, Vec<(PublicKey, [u8; 64])>, oneshot::Sender<BatchReply>),
     Certificate(CertificateCrypto, oneshot::Sender<CertificateReply>),
     Digest(Vec<u8>, oneshot::Sender<DigestReply>),
 }
@@ -221,7 +225,7 @@ impl VerifyService {
             Ok(verdict) => verdict,
             Err(status) => {
                 degrade::engine_failed(status, "every context failed", "VerifyService::verify");
-                degrade::verify_strict(&signature, digest, key)
+                degrade::cpu_verify(&signature, digest, key)
             }
         }
     }
@@ -229,15 +233,12 @@ impl VerifyService {
     /// `Signature::verify_batch(digest, votes)` (crypto/src/lib.rs:206-219).
     pub async fn verify_batch(&self, digest: &Digest, votes: Vec<(PublicKey, [u8; 64])>) -> Result<(), CryptoError> {
         let (sender, receiver) = oneshot::channel();
-        // kept for the CPU answer of an engine failure (bare vote batches are
-        // rare next to whole certificates: the copy is a few KB)
-        let kept = votes.clone();
         self.send(Request::Batch(digest.clone(), votes, sender)).await;
         match receiver.await.expect("Failed to receive verdict from Verify Service") {
             Ok(verdict) => verdict,
-            Err(status) => {
+            Err((status, votes)) => {
                 degrade::engine_failed(status, "every context failed", "VerifyService::verify_batch");
-                degrade::verify_batch(digest, &kept)
+                degrade::cpu_verify_batch(digest, &votes)
             }
         }
     }
@@ -252,8 +253,9 @@ impl VerifyService {
             Ok(reply) => reply,
             Err((status, c)) => {
                 degrade::engine_failed(status, "every context failed", "VerifyService::certificate");
-                let bits = degrade::certificate_bits(c.header_input(), c.id(), c.origin(), c.header_signature(),
-                                                     c.round(), c.vote_keys(), c.vote_signatures());
+                let bits = degrade::cpu_certificate_bits(c.header_input(), c.id(), c.origin(),
+                                                         c.header_signature(), c.round(), c.vote_keys(),
+                                                         c.vote_signatures());
                 (bits, c)
             }
         }
@@ -268,7 +270,7 @@ impl VerifyService {
             Ok(reply) => reply,
             Err((status, bytes)) => {
                 degrade::engine_failed(status, "every context failed", "VerifyService::digest");
-                (degrade::sha512_digest(&bytes), bytes)
+                (degrade::cpu_digest(&bytes), bytes)
             }
         }
     }
@@ -294,7 +296,7 @@ fn submit_window(queue: &Queue, window: Vec<Request>) {
                 sigs.extend_from_slice(&signature);
                 senders.push(sender);
             }
-            Request::Batch(digest, votes, sender) => submit_batch(queue, &digest, &votes, sender),
+            Request::Batch(digest, votes, sender) => submit_batch(queue, &digest, votes, sender),
             Request::Certificate(crypto, sender) => submit_certificate(queue, crypto, sender),
             Request::Digest(bytes, sender) => submit_digest(queue, bytes, sender),
         }
@@ -317,20 +319,24 @@ fn submit_window(queue: &Queue, window: Vec<Request>) {
     }
 }
 
-fn submit_batch(queue: &Queue, digest: &Digest, votes: &[(PublicKey, [u8; 64])], sender: oneshot::Sender<Verdict>) {
+fn submit_batch(queue: &Queue, digest: &Digest, votes: Vec<(PublicKey, [u8; 64])>,
+                sender: oneshot::Sender<BatchReply>) {
     let (mut keys, mut sigs) = (Vec::with_capacity(32 * votes.len()), Vec::with_capacity(64 * votes.len()));
-    for (key, signature) in votes {
+    for (key, signature) in &votes {
         keys.extend_from_slice(&key.0);
         sigs.extend_from_slice(signature);
     }
-    let user = Box::into_raw(Box::new(sender)) as *mut c_void;
+    let n = votes.len();
+    // the votes ride along with the sender: handed back only on a failure
+    let user = Box::into_raw(Box::new((sender, votes))) as *mut c_void;
     let rc = unsafe {
-        ffi::coa_queue_submit_batch(queue.0, digest.0.as_ptr(), keys.as_ptr(), sigs.as_ptr(), votes.len(),
-                                    Some(on_verdict), user)
+        ffi::coa_queue_submit_batch(queue.0, digest.0.as_ptr(), keys.as_ptr(), sigs.as_ptr(), n, Some(on_batch),
+                                    user)
     };
     if rc != ffi::COA_OK {
-        let sender = unsafe { Box::from_raw(user as *mut oneshot::Sender<Verdict>) };
-        let _ = sender.send(Err(rc));
+        let pair = unsafe { Box::from_raw(user as *mut (oneshot::Sender<BatchReply>, Vec<(PublicKey, [u8; 64])>)) };
+        let (sender, votes) = *pair;
+        let _ = sender.send(Err((rc, votes)));
     }
 }
 
@@ -392,13 +398,14 @@ unsafe extern "C" fn on_verdicts(user: *mut c_void, status: c_int, verdicts: *co
     }
 }
 
-/// One vote batch: one verdict byte.
-unsafe extern "C" fn on_verdict(user: *mut c_void, status: c_int, verdicts: *const u8, n: usize) {
-    let sender = Box::from_raw(user as *mut oneshot::Sender<Verdict>);
+/// One vote batch: one verdict byte (the votes handed back on a failure).
+unsafe extern "C" fn on_batch(user: *mut c_void, status: c_int, verdicts: *const u8, n: usize) {
+    let pair = Box::from_raw(user as *mut (oneshot::Sender<BatchReply>, Vec<(PublicKey, [u8; 64])>));
+    let (sender, votes) = *pair;
     let reply = if status != ffi::COA_OK {
-        Err(status)
+        Err((status, votes))
     } else if verdicts.is_null() || n != 1 {
-        Err(ffi::COA_EINVAL)
+        Err((ffi::COA_EINVAL, votes))
     } else {
         Ok(verdict_of(*verdicts))
     };

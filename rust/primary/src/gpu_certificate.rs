@@ -42,6 +42,10 @@ extern "C" {
                                    origins: *const u8, header_sigs: *const u8, rounds: *const u64,
                                    vote_pks: *const u8, vote_sigs: *const u8, vote_offsets: *const u64,
                                    n: usize, rng_seed: u64, status_out: *mut u8) -> c_int;
+    fn coa_cpu_certificate_verify_many(header_data: *const u8, header_offsets: *const u64, ids: *const u8,
+                                       origins: *const u8, header_sigs: *const u8, rounds: *const u64,
+                                       vote_pks: *const u8, vote_sigs: *const u8, vote_offsets: *const u64,
+                                       n: usize, rng_seed: u64, status_out: *mut u8, nthreads: c_int) -> c_int;
     fn coa_last_error() -> *const std::os::raw::c_char;
 }
 
@@ -49,15 +53,20 @@ const BAD_HEADER_ID: c_int = 1;
 const BAD_HEADER_SIG: c_int = 2;
 const BAD_VOTES: c_int = 4;
 
-/// An engine failure (every context failed, or no GPU): reported (or a
-/// panic under COA_ON_ENGINE_FAILURE=panic), then the certificate's crypto
-/// bits come from the reference's own ed25519-dalek / Sha512 code
-/// (crypto/src/degrade.rs), so the DagError is still the reference's.
-fn engine_failure(rc: c_int, c: &CertificateCrypto) -> c_int {
+/// An engine failure (every context failed, or no GPU): reported once per
+/// call (or a panic under COA_ON_ENGINE_FAILURE=panic); the caller then takes
+/// the certificates' crypto bits from the engine's own CPU path
+/// (coa_cpu_certificate_verify_many, crypto/src/degrade.rs), so the DagError
+/// is still the reference's.
+fn engine_failure(rc: c_int) {
     let msg = unsafe { std::ffi::CStr::from_ptr(coa_last_error()) }.to_string_lossy().into_owned();
     crypto::degrade::engine_failed(rc, &msg, "Certificate::verify");
-    crypto::degrade::certificate_bits(c.header_input(), c.id(), c.origin(), c.header_signature(), c.round(),
-                                      c.vote_keys(), c.vote_signatures()) as c_int
+}
+
+/// The COA_CERT_* bits of one certificate on the engine's CPU path.
+fn cpu_bits(c: &CertificateCrypto) -> c_int {
+    crypto::degrade::cpu_certificate_bits(c.header_input(), c.id(), c.origin(), c.header_signature(), c.round(),
+                                          c.vote_keys(), c.vote_signatures()) as c_int
 }
 
 /// Length of the bytes Header::digest hashes (primary/src/messages.rs:70-84).
@@ -137,7 +146,12 @@ pub fn verify(cert: &Certificate, committee: &Committee) -> DagResult<()> {
                                c.origin().as_ptr(), c.header_signature().as_ptr(), c.round(),
                                c.vote_keys().as_ptr(), c.vote_signatures().as_ptr(), c.n_votes(), 0)
     };
-    let st = if st < 0 { engine_failure(st, &c) } else { st };
+    let st = if st < 0 {
+        engine_failure(st);
+        cpu_bits(&c)
+    } else {
+        st
+    };
     checks_in_order(cert, committee, st)
 }
 
@@ -176,10 +190,14 @@ pub fn verify_many(certs: &[&Certificate], committee: &Committee) -> Vec<DagResu
                                         voff.as_ptr(), n, 0, status.as_mut_ptr())
         };
         if rc < 0 {
-            // every certificate of the window answered by the reference's code
-            for (j, &i) in todo.iter().enumerate() {
-                status[j] = engine_failure(rc, &certificate_crypto(certs[i])) as u8;
-            }
+            // the whole window answered by the engine's CPU path, one call
+            engine_failure(rc);
+            let rc = unsafe {
+                coa_cpu_certificate_verify_many(hdata.as_ptr(), hoff.as_ptr(), ids.as_ptr(), origins.as_ptr(),
+                                                hsigs.as_ptr(), rounds.as_ptr(), vpks.as_ptr(), vsigs.as_ptr(),
+                                                voff.as_ptr(), n, 0, status.as_mut_ptr(), 0)
+            };
+            assert!(rc >= 0, "engine CPU path refused Certificate::verify: status {}", rc);
         }
     }
     let mut out: Vec<DagResult<()>> = (0..certs.len()).map(|_| Ok(())).collect();

@@ -201,27 +201,41 @@ def test_rust_sources_build_on_the_reference_toolchain():
                     assert not re.search(pat, src), (f, what)
 
 
-def test_engine_failure_policy_uses_the_reference_code_not_the_oracle():
-    """VERDICT r4 missing 3: when every engine context failed, the binding
-    answers with the reference's own ed25519-dalek calls (degrade.rs) unless
-    COA_ON_ENGINE_FAILURE=panic; no call site panics on an engine failure any
-    more, and nothing in rust/ reaches the test oracle."""
+def test_engine_failure_policy_uses_the_engines_cpu_path():
+    """when every engine context failed, the binding
+    answers with the ENGINE'S OWN CPU path (coa_cpu_*, csrc/coa_cpu.cpp;
+    tests/test_cpu_path.py pins it to the oracle and the golden fixtures)
+    unless COA_ON_ENGINE_FAILURE=panic -- not with ed25519-dalek (the
+    replaced implementation) and not with the test oracle; no call site
+    panics on an engine failure, and a failed certificate window is reported
+    once."""
     def code(path):
         src = open(path).read()
         return re.sub(r"//[^\n]*", "", src)
 
     deg = code(os.path.join(RUST, "crypto", "src", "degrade.rs"))
-    assert "key.verify_strict(&digest.0, &signature)" in deg
-    assert "dalek::verify_batch(&messages[..], &signatures[..], &keys[..])" in deg
-    assert "Sha512::digest" in deg and 'COA_ON_ENGINE_FAILURE' in deg
+    for f in ("coa_cpu_ed25519_verify_strict", "coa_cpu_ed25519_verify_batch", "coa_cpu_sha512_many",
+              "coa_cpu_certificate_verify_many"):
+        assert f"ffi::{f}(" in deg, f
+    assert "COA_ON_ENGINE_FAILURE" in deg
     for dirpath, _, files in os.walk(RUST):
         for f in files:
             if f.endswith(".rs"):
                 src = code(os.path.join(dirpath, f))
                 assert "oracle" not in src, f
+                # no dalek verification or hashing anywhere in the drop-in
+                for pat in (r"\.verify_strict\(", r"dalek::verify_batch", r"Sha512::digest", r"Sha512::new",
+                            r"use ed25519_dalek"):
+                    assert not re.search(pat, src), (f, pat)
                 if f in ("gpu.rs", "service.rs", "gpu_certificate.rs"):
                     assert "engine failure" not in src.replace("degrade::engine_failed", ""), f
                     assert not re.search(r"panic!\(\"MI355X verification engine failure", src), f
+    gc = code(os.path.join(RUST, "primary", "src", "gpu_certificate.rs"))
+    # verify_many: one engine_failure for the window, then one CPU call
+    body = gc[gc.index("pub fn verify_many"):]
+    assert body.count("engine_failure(") == 1 and "coa_cpu_certificate_verify_many(" in body
+    svc = code(os.path.join(RUST, "crypto", "src", "service.rs"))
+    assert "votes.clone()" not in svc  # the votes come back with the failure reply
 
 
 def _c_struct_fields(name):

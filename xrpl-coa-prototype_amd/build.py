@@ -19,7 +19,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 SOURCES = ["coa_kernels.hip", "coa_halved.hip", "coa_batch.hip", "coa_committee.hip", "coa_msm.hip", "coa_latency.hip",
-           "coa_runtime.cpp", "coa_queue.cpp", "coa_queue_hip.cpp", "coa_wire.cpp"]
+           "coa_runtime.cpp", "coa_queue.cpp", "coa_queue_hip.cpp", "coa_wire.cpp", "coa_cpu.cpp"]
 HEADERS = ["coa_fe.h", "coa_sc.h", "coa_ge.h", "coa_sha512.h", "coa_smul.h", "coa_kernels.h", "coa_batch.h", "coa_halved.h",
            "coa_committee.h", "coa_msm.h", "coa_fe_wave.h", "coa_ge_rows.h", "coa_halve.h", "coa_keycache.h",
            "coa_latency.h", "coa_queue.h", "coa_rcmp.h", "coa_lehmer.h"]

@@ -143,6 +143,16 @@ def lib():
         "coa_wire_decode_votes": ([P8, P64, sz, P8, P64, P8, P8, P8], ctypes.c_int),
         "coa_wire_decode_headers": ([P8, P64, sz, P8, P64, P8, P8, P8, P64, ctypes.POINTER(ctypes.c_uint32)],
                                     ctypes.c_int),
+        # the engine's own CPU path (explicit only; never a silent fallback)
+        "coa_cpu_ed25519_verify_strict": ([P8, sz, P8, P8], ctypes.c_int),
+        "coa_cpu_ed25519_verify_strict_many": ([P8, sz, P8, P8, sz, P8, ctypes.c_int], ctypes.c_int),
+        "coa_cpu_ed25519_verify_batch": ([P8, P8, P8, sz, ctypes.c_uint64], ctypes.c_int),
+        "coa_cpu_ed25519_verify_batch_groups_z": ([P8, P8, P8, P64, sz, P8, P8, ctypes.c_int], ctypes.c_int),
+        "coa_cpu_sha512_many": ([P8, P64, sz, P8, ctypes.c_int], ctypes.c_int),
+        "coa_cpu_certificate_verify_many": ([P8, P64, P8, P8, P8, P64, P8, P8, P64, sz, ctypes.c_uint64, P8,
+                                             ctypes.c_int], ctypes.c_int),
+        "coa_cpu_certificate_verify_many_z": ([P8, P64, P8, P8, P8, P64, P8, P8, P64, sz, P8, P8, ctypes.c_int],
+                                              ctypes.c_int),
         "coa_queue_create": ([sz, ctypes.c_uint32], vp),
         "coa_queue_submit_verify": ([vp, P8, P8, P8, VERDICT_CB, vp], ctypes.c_int),
         "coa_queue_submit_verify_many": ([vp, P8, P8, P8, sz, VERDICT_CB, vp], ctypes.c_int),
@@ -166,6 +176,65 @@ def lib():
         f.restype = res
     _lib = L
     return L
+
+
+def cpu_verify_strict_many(msgs, pks, sigs, nthreads=0):
+    """The engine's own CPU path (csrc/coa_cpu.cpp) for n triples: verdict
+    bytes 0 Ok / 1 Err.  Explicit only -- what a caller runs when its GPU
+    calls failed (rust/crypto/src/degrade.rs); no GPU entry point calls it."""
+    msgs, pks, sigs = (np.ascontiguousarray(a, dtype=np.uint8) for a in (msgs, pks, sigs))
+    n = pks.shape[0]
+    out = np.ones(n, np.uint8)
+    _check(lib().coa_cpu_ed25519_verify_strict_many(_u8p(msgs), msgs.shape[1] if n else 0, _u8p(pks), _u8p(sigs), n,
+                                                    _u8p(out), nthreads))
+    return out
+
+
+def cpu_verify_batch_groups(msgs, pks, sigs, group_offsets, zs, nthreads=0):
+    """CPU path of coa_ed25519_verify_batch_groups_z (explicit weights)."""
+    msgs, pks, sigs, zs = (np.ascontiguousarray(a, dtype=np.uint8) for a in (msgs, pks, sigs, zs))
+    off = np.ascontiguousarray(group_offsets, dtype=np.uint64)
+    g = off.size - 1
+    out = np.ones(g, np.uint8)
+    _check(lib().coa_cpu_ed25519_verify_batch_groups_z(_u8p(msgs), _u8p(pks), _u8p(sigs), _u8p(off), g, _u8p(zs),
+                                                       _u8p(out), nthreads))
+    return out
+
+
+def cpu_sha512_many(messages, nthreads=0):
+    """CPU path of coa_sha512_many: 64-byte digests, one row per message."""
+    data = np.frombuffer(b"".join(bytes(m) for m in messages) + b"\0", np.uint8)
+    off = np.zeros(len(messages) + 1, np.uint64)
+    off[1:] = np.cumsum([len(m) for m in messages])
+    out = np.zeros((len(messages), 64), np.uint8)
+    _check(lib().coa_cpu_sha512_many(_u8p(data), _u8p(off), len(messages), _u8p(out), nthreads))
+    return out
+
+
+def cpu_certificate_verify_many(header_inputs, ids, origins, header_sigs, rounds, vote_pks, vote_sigs, vote_offsets,
+                                zs=None, rng_seed=0, nthreads=0):
+    """CPU path of coa_certificate_verify_many: COA_CERT_* bits per
+    certificate (zs: the votes' 16-byte weights, else drawn from rng_seed)."""
+    n = len(header_inputs)
+    hdata = np.frombuffer(b"".join(bytes(h) for h in header_inputs) + b"\0", np.uint8)
+    hoff = np.zeros(n + 1, np.uint64)
+    hoff[1:] = np.cumsum([len(h) for h in header_inputs])
+    ids, origins, header_sigs, vote_pks, vote_sigs = (np.ascontiguousarray(a, dtype=np.uint8) for a in
+                                                      (ids, origins, header_sigs, vote_pks, vote_sigs))
+    rounds = np.ascontiguousarray(rounds, dtype=np.uint64)
+    voff = np.ascontiguousarray(vote_offsets, dtype=np.uint64)
+    out = np.full(n, 0xff, np.uint8)
+    L = lib()
+    if zs is None:
+        _check(L.coa_cpu_certificate_verify_many(_u8p(hdata), _u8p(hoff), _u8p(ids), _u8p(origins), _u8p(header_sigs),
+                                                 _u8p(rounds), _u8p(vote_pks), _u8p(vote_sigs), _u8p(voff), n,
+                                                 rng_seed, _u8p(out), nthreads))
+    else:
+        zs = np.ascontiguousarray(zs, dtype=np.uint8)
+        _check(L.coa_cpu_certificate_verify_many_z(_u8p(hdata), _u8p(hoff), _u8p(ids), _u8p(origins),
+                                                   _u8p(header_sigs), _u8p(rounds), _u8p(vote_pks), _u8p(vote_sigs),
+                                                   _u8p(voff), n, _u8p(zs), _u8p(out), nthreads))
+    return out
 
 
 def _check(rc):
