@@ -86,6 +86,45 @@ def test_shard_failure_rebuilds_context_and_reruns(engine, contexts, monkeypatch
     assert (engine.verify_strict_many(m2, p2, s2) == e2).all()
 
 
+def test_every_context_failed_then_the_cpu_path_answers(engine, contexts, monkeypatch):
+    """COA_FAULT_SHARD=all: every attempt on every context fails, so the GPU
+    call itself fails loudly (EngineError, no silent fallback).  What the
+    Rust binding then answers with (degrade.rs, COA_ON_ENGINE_FAILURE=cpu) is
+    the engine's own CPU path, coa_cpu_*: its verdicts equal the GPU's
+    fault-free verdicts and the oracle's, for signatures and certificates."""
+    import certificates as C
+    from workloads import adversarial_mix, key_seeds, messages
+
+    contexts(2)
+    n = 12_000
+    pks, sigs = engine.sign_many(key_seeds(n, 8100), messages(n, 8100))
+    msgs, pks, sigs, _ = adversarial_mix(messages(n, 8100), pks, sigs, frac=0.1, seed=78)
+    gpu = engine.verify_strict_many(msgs, pks, sigs)
+    # 600 certificates x 4 jobs: above the latency route (2,048 jobs), so the
+    # call is sharded over the contexts (for_shards)
+    committee, batch = C.synth_certificates(600, committee_size=4, n_payload=1, seed=5)
+    bad = batch.vote_sigs.copy()
+    bad[7, 40] ^= 1
+    rounds = np.full(600, batch.round, np.uint64)
+    cargs = (batch.header_inputs, batch.ids, batch.authors, batch.header_sigs, rounds, batch.vote_pks, bad,
+             batch.offsets)
+    gpu_c = engine.certificate_verify_many(*cargs)
+    monkeypatch.setenv("COA_FAULT_SHARD", "all")
+    with pytest.raises(engine.EngineError):
+        engine.verify_strict_many(msgs, pks, sigs)
+    with pytest.raises(engine.EngineError):
+        engine.certificate_verify_many(*cargs)
+    cpu = engine.cpu_verify_strict_many(msgs, pks, sigs)
+    cpu_c = engine.cpu_certificate_verify_many(*cargs)
+    monkeypatch.delenv("COA_FAULT_SHARD")
+    exp = co.verify_strict_many(msgs, pks, sigs, min(16, os.cpu_count() or 1))
+    assert (gpu == exp).all() and (cpu == exp).all()
+    assert list(cpu_c) == list(gpu_c) and int(np.count_nonzero(gpu_c)) == 1
+    # the contexts were rebuilt and answer again
+    m2, p2, s2, e2 = _tiled(5000)
+    assert (engine.verify_strict_many(m2, p2, s2) == e2).all()
+
+
 def test_single_verifies_from_eight_threads_over_eight_contexts(engine, contexts):
     contexts(8)
     vecs = _vec32()

@@ -816,9 +816,17 @@ int run_tasks(std::vector<std::pair<Dev*, std::function<int()>>>& tasks) {
 
 // COA_FAULT_SHARD=<k>: every k-th shard of a sharded call fails with
 // COA_EHIP after its work has run (fault injection for the recovery tests;
-// never set in production).  Read per call.
+// never set in production).  COA_FAULT_SHARD=all: every attempt fails,
+// re-runs on the other contexts included, so the call itself fails (the
+// caller's failure policy is then what answers: tests/test_gpu_recovery.py).
+// Read per call.
+bool fault_every_attempt() {
+  const char* e = getenv("COA_FAULT_SHARD");
+  return e && std::strcmp(e, "all") == 0;
+}
 bool inject_shard_fault() {
   static std::atomic<unsigned long long> count{0};
+  if (fault_every_attempt()) return true;
   const char* e = getenv("COA_FAULT_SHARD");
   const unsigned long long every = e ? strtoull(e, nullptr, 10) : 0ull;
   return every && (count.fetch_add(1) + 1) % every == 0;
@@ -890,7 +898,7 @@ int for_shards(size_t n, F body, size_t work = 0) {
     int r = rcs[i];
     const std::string first = msgs[i];
     for (size_t k = 1; k <= g_devs.size() && (r == COA_EHIP || r == COA_ENOMEM); k++) {
-      r = run_on(*g_devs[(at + k) % g_devs.size()], ranges[i].lo, ranges[i].hi, false);
+      r = run_on(*g_devs[(at + k) % g_devs.size()], ranges[i].lo, ranges[i].hi, fault_every_attempt());
       g_shards_rerun++;
     }
     if (r != COA_OK) return fail(r, "shard failed on every context: " + first + " / " + g_err);
