@@ -171,7 +171,11 @@ def lib():
         "coa_queue_destroy": ([vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)
+        if f is None and os.environ.get("COA_VERIFY_LIB") and name.startswith("coa_cpu_"):
+            continue  # an older A/B build (COA_VERIFY_LIB) without the CPU path
+        if f is None:
+            raise EngineError(f"{LIB_PATH} does not export {name}")
         f.argtypes = args
         f.restype = res
     _lib = L

@@ -1808,6 +1808,15 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
       else
         (void)hipGetLastError();  // no spare: the next registration allocates
     }
+  } else if (keep_spare && !nk && old && old->nkeys && !sh.spare) {
+    // a committee cleared: its generation's buffers stay as the spare instead
+    // of being freed.  Freeing a 65 GB generation here, and allocating one
+    // again at the next registration, each held the HIP runtime while other
+    // threads enqueued: a signature window of the queue spent 7.9 ms in
+    // `enqueue` (profiles/r05_register_gc.txt:19) while
+    // test_register_while_queue_saturated_with_certificates cleared and
+    // re-registered the committee in a loop
+    sh.spare = std::const_pointer_cast<KeySet>(old);
   }
   old.reset();
   if (env_is("COA_REGISTER_TRACE", "1"))
