@@ -1199,6 +1199,8 @@ def certificate_config(n_certs, latency_samples, cpu_threads, dev, stream, commi
                                                    f"round) on {cpu_threads} threads, {el:.2f} s wall"}}
     res["p50_vs_cpu"] = round(res["cpu_baseline"]["p50_ms"] / res["p50_ms"], 2)
     res["c_caller"]["p50_vs_cpu"] = round(res["cpu_baseline"]["p50_ms"] / c50, 2)
+    if committee_size == 100:
+        res["roofline"] = c3_roofline(n_certs, nv, len(batch.header_inputs[0]), dev_ms)
     return res
 
 
@@ -1335,19 +1337,90 @@ VERIFY_KERNEL_SOURCES = ("coa_halved.hip", "coa_halved.h", "coa_halve.h", "coa_l
                          "coa_sc.h", "coa_sha512.h", "coa_smul.h", "coa_kernels.h")
 
 
-def verify_kernel_src_sha256():
-    """sha256 over the C2 verify kernels' sources and the build flags (ties a
-    committed counter profile to the code it was taken on)."""
+def _kernel_src_sha256(names):
     import hashlib
 
     sys.path.insert(0, PKG)
     import build as engine_build
 
     h = hashlib.sha256(" ".join(f for f in engine_build.COMMON if not f.startswith("-I")).encode())
-    for name in VERIFY_KERNEL_SOURCES:
+    for name in names:
         with open(os.path.join(PKG, "csrc", name), "rb") as f:
             h.update(name.encode() + b"\0" + f.read())
     return h.hexdigest()
+
+
+def verify_kernel_src_sha256():
+    """sha256 over the C2 verify kernels' sources and the build flags (ties a
+    committed counter profile to the code it was taken on)."""
+    return _kernel_src_sha256(VERIFY_KERNEL_SOURCES)
+
+
+# Sources of the C3 round's kernels (k_cert_digests, k_job_*, k_cert_verify)
+C3_KERNEL_SOURCES = ("coa_committee.hip", "coa_committee.h", "coa_fe.h", "coa_ge.h", "coa_halved.h", "coa_sc.h",
+                     "coa_keycache.h", "coa_rcmp.h", "coa_sha512.h", "coa_smul.h", "coa_ge_rows.h", "coa_fe_wave.h")
+C3_PMC_JSON = "r06_c3_pmc.json"
+
+
+def c3_kernel_src_sha256():
+    return _kernel_src_sha256(C3_KERNEL_SOURCES)
+
+
+def load_c3_pmc(n_certs):
+    """The counter profile of the C3 device round (tools/pmc_c3_tie.py) if it
+    was taken on these kernel sources and round size, else None and why."""
+    path = os.path.join(ROOT, "profiles", C3_PMC_JSON)
+    if not os.path.exists(path):
+        return None, f"profiles/{C3_PMC_JSON} absent"
+    with open(path) as f:
+        pj = json.load(f)
+    if pj.get("n_certs") != n_certs:
+        return None, f"profiles/{C3_PMC_JSON} was taken at {pj.get('n_certs')} certificates"
+    if pj.get("kernel_src_sha256") != c3_kernel_src_sha256():
+        return None, f"profiles/{C3_PMC_JSON} was taken on other kernel sources"
+    return pj, None
+
+
+# The built C3 algorithm's work (k_cert_verify, DESIGN.md §4 "C3 roofline"),
+# per signature job (a vote or the header signature): 11 + 13 wide-comb mixed
+# additions of 7 field multiplications, 5 of Montgomery's batch inversion (the
+# prefix product, two for 1/Z, x and y), a 1/5.2 share of one 265-operation
+# inversion (~5.2 jobs per lane at C3), and one SHA-512 block for k; per
+# certificate one block for Certificate::digest and the header digest's
+# blocks.  Priced as SURVEY 8(d) prices dalek's: 200 INT32 ops per field
+# operation, ~5,000 per SHA-512 block (80 rounds of 64-bit Sigma/Ch/Maj/adds
+# on 32-bit lanes plus the 64-word schedule).
+C3_FIELD_OPS_PER_JOB = 24 * 7 + 5 + 51
+SHA512_BLOCK_INT32_OPS = 5000
+C3_COMB_ENTRY_BYTES = 96  # (y+x, y-x, 2dxy) of one affine comb entry
+
+
+def c3_roofline(n_certs, n_votes, header_bytes, round_ms):
+    """summary.c3_roofline: the C3 device round against the INT32 VALU peak
+    (built-algorithm model) and, from the committed counter profile,
+    VALU issue and HBM traffic against the algorithmic bytes."""
+    jobs = n_certs + n_votes
+    hdr_blocks = (header_bytes + 17 + 127) // 128
+    ops = jobs * (C3_FIELD_OPS_PER_JOB * INT32_OPS_PER_FIELD_OP + SHA512_BLOCK_INT32_OPS) + \
+        n_certs * (1 + hdr_blocks) * SHA512_BLOCK_INT32_OPS
+    # inputs (header bytes, id, origin, header signature, round, votes' keys and
+    # signatures, offsets), the comb entries the additions read, status words
+    alg_bytes = n_certs * (header_bytes + 32 + 32 + 64 + 8 + 16 + 4) + n_votes * 96 + jobs * 24 * C3_COMB_ENTRY_BYTES
+    sec = round_ms * 1e-3
+    out = {"alg_int32_ops_per_cert": round(ops / n_certs), "achieved_TOPS": round(ops / sec / 1e12, 3),
+           "frac": round(ops / sec / 1e12 / PEAK_INT32_TOPS, 4), "alg_bytes": alg_bytes,
+           "alg_GBps": round(alg_bytes / sec / 1e9, 1)}
+    pmc, why = load_c3_pmc(n_certs)
+    if pmc:
+        out["issue_frac"] = round(pmc["valu_insts_per_round"] * VALU_ISSUE_CYCLES / (SIMDS * CLOCK_HZ * sec), 4)
+        out["traffic_bytes"] = pmc["hbm_bytes_per_round"]
+        out["traffic_ratio"] = round(pmc["hbm_bytes_per_round"] / alg_bytes, 2)
+        out["traffic_TBps"] = round(pmc["hbm_bytes_per_round"] / sec / 1e12, 2)
+        out["counters"] = f"profiles/{C3_PMC_JSON} (sha256-tied to the kernel sources; copied, not measured here)"
+    else:
+        out["issue_frac"] = out["traffic_bytes"] = None
+        out["counters"] = why
+    return out
 
 
 def build_identity():
@@ -1515,7 +1588,13 @@ def summarize(value, sec, cpu):
     (/root/reference/primary/src/messages.rs:189-215) -- and the other
     configs' figures.  Every value is copied from `secondary` (None where a
     section did not run)."""
-    sec = sec or {}
+    if not sec:
+        # N > 1 (or --no-secondary): the secondary sections run on rank 0 at
+        # N = 1 only
+        out = {"c2_verify_per_s": round(value, 1), "secondary": "not run (N > 1 or --no-secondary)"}
+        if cpu:
+            out["cpu_c2_verify_per_s"] = cpu.get("value")
+        return out
 
     def get(*path):
         o = sec
@@ -1536,6 +1615,10 @@ def summarize(value, sec, cpu):
                                          "cpu_one_core": get(f"{cfg}_certificate_verify", "cpu_baseline", "p50_ms"),
                                          "vs_cpu": get(f"{cfg}_certificate_verify", "c_caller", "p50_vs_cpu")}
             out[f"{cfg}_round_certs_per_s"] = s.get("certs_per_s")
+            if s.get("roofline"):
+                r = s["roofline"]
+                out[f"{cfg}_roofline"] = {k: r.get(k) for k in ("frac", "issue_frac", "traffic_bytes", "alg_bytes",
+                                                               "traffic_ratio", "traffic_TBps")}
     out["verify_single_p50_ms"] = {"committee_key": get("verify_single", "committee_key", "c_caller", "p50_ms"),
                                    "other_key": get("verify_single", "uncached_key", "c_caller", "p50_ms"),
                                    "cpu_one_core": get("verify_single", "cpu_single_thread_p50_ms")}

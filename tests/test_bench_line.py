@@ -100,3 +100,22 @@ def test_gpus_flag_failing_rank_fails_the_run(monkeypatch, capfd):
     with pytest.raises(SystemExit) as e:
         bench.main(["--gpus", "2"])
     assert e.value.code == 3
+
+
+def test_c3_roofline_from_committed_counters():
+    """summary.c3_roofline: the built algorithm's INT32
+    count per certificate, and -- from profiles/r06_c3_pmc.json, tied by
+    sha256 to the committee kernels' sources -- VALU issue and HBM traffic
+    against the algorithmic bytes of a 10k-certificate round."""
+    r = bench.c3_roofline(10000, 670000, 3336, 1.25)
+    assert 3.0e6 < r["alg_int32_ops_per_cert"] < 4.0e6
+    assert 0.2 < r["frac"] < 0.5
+    assert r["issue_frac"] is not None, r["counters"]
+    assert 0.2 < r["issue_frac"] < 0.5
+    assert r["traffic_bytes"] > r["alg_bytes"] > 1.5e9
+    rec = _recorded()
+    sec = dict(rec["secondary"])
+    sec["c3_certificate_verify"] = dict(sec["c3_certificate_verify"], roofline=r)
+    s = bench.summarize(rec["value"], sec, rec["cpu_baseline"])
+    assert s["c3_roofline"]["issue_frac"] == r["issue_frac"]
+    assert s["c3_roofline"]["traffic_ratio"] == r["traffic_ratio"]

@@ -320,7 +320,7 @@ class HipBackend : public coa_q::Backend {
     const size_t pre_ws = lane_ == coa_q::LANE_DIGEST
                               ? 256
                               : std::max(coa_verify_workspace_bytes(items),
-                                         coa_cert_scratch_bytes(items / 68 + 1 + items, false)) + 256;
+                                         coa_cert_scratch_bytes(items / 68 + 1 + items, keysort_)) + 256;
     for (Slot& sl : slots_) {
       if (lane_ == coa_q::LANE_VERIFY && hipSetDevice(sl.dev) == hipSuccess) {
         (void)lat_words(sl);
@@ -458,6 +458,9 @@ class HipBackend : public coa_q::Backend {
     if (const char* e = getenv("COA_QUEUE_FAULT")) fault_every_ = strtoull(e, nullptr, 10);
     // COA_QUEUE_INLINE=0: small signature windows take the staged path too (A/B)
     if (const char* e = getenv("COA_QUEUE_INLINE")) inline_ok_ = e[0] != '0';
+    // COA_QUEUE_KEYSORT=0|1: certificate windows of >= 16,384 jobs take their
+    // jobs in committee-key order (coa_certificate_verify_many_device_order)
+    if (const char* e = getenv("COA_QUEUE_KEYSORT")) keysort_ = e[0] != '0';
     kind_ = stream_kind_env();
     slots_.resize(per * devs_.size());
     // (page-locked staging is sized by prepare(): a reallocation on the
@@ -512,7 +515,7 @@ class HipBackend : public coa_q::Backend {
     sl.o_d = take(L.nd * 64);
     const size_t out_bytes = o;
     const size_t ws_v = L.nv ? coa_verify_workspace_bytes(L.nv) : 0;
-    const size_t ws_c = L.nc ? coa_cert_scratch_bytes(L.nc + L.nvotes, false) : 0;
+    const size_t ws_c = L.nc ? coa_cert_scratch_bytes(L.nc + L.nvotes, keysort_) : 0;
     const size_t caps0 = sl.cap_hin + sl.cap_hout + sl.cap_din + sl.cap_dout + sl.cap_ws;
     if (grow_pinned(sl.hin, sl.cap_hin, in_bytes, sl.grave) != hipSuccess ||
         grow_pinned(sl.hout, sl.cap_hout, out_bytes, sl.grave) != hipSuccess ||
@@ -651,12 +654,13 @@ class HipBackend : public coa_q::Backend {
       rc = coa_ed25519_verify_strict_many_device(sl.dev, d + i_vm, 32, d + i_vp, d + i_vs, L.nv, dout + sl.o_v, sl.ws,
                                                  sl.s);
     if (rc == COA_OK && L.nc) {
-      // certificate order (no key sort): see coa_certificate_verify_many_device_order
+      // key order for a large window (COA_QUEUE_KEYSORT): see
+      // coa_certificate_verify_many_device_order
       rc = coa_certificate_verify_many_device_order(
           sl.dev, d + i_ch, reinterpret_cast<const uint64_t*>(d + i_cho), d + i_cid, d + i_cor, d + i_chs,
           reinterpret_cast<const uint64_t*>(d + i_crd), d + i_cvp, d + i_cvs,
           reinterpret_cast<const uint64_t*>(d + i_cvo), L.nc, L.nvotes, reinterpret_cast<uint32_t*>(dout + sl.o_c),
-          sl.ws, sl.s, 0);
+          sl.ws, sl.s, keysort_ ? 1 : 0);
     }
     if (rc == COA_OK && L.nd)
       rc = coa_sha512_many_device(sl.dev, d + i_dd, reinterpret_cast<const uint64_t*>(d + i_do), L.nd, dout + sl.o_d,
@@ -821,6 +825,7 @@ class HipBackend : public coa_q::Backend {
   int init_rc_ = COA_OK;
   unsigned long long fault_every_ = 0, launches_ = 0;
   bool inline_ok_ = true;  // COA_QUEUE_INLINE
+  bool keysort_ = true;     // COA_QUEUE_KEYSORT
 };
 
 }  // namespace
