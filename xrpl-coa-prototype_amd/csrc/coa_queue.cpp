@@ -529,11 +529,13 @@ struct Lane {
       if (trace_slow_us > 0 && window_us > trace_slow_us) {  // COA_QUEUE_TRACE_SLOW_US (diagnostics)
         fprintf(stderr,
                 "[coa queue] slow window %.0f us at t=%.6f s: %zu items kinds %u slot %d; slot_wait %.0f pack %.0f "
-                "enqueue %.0f device_wait %.0f scatter %.0f us\n",
+                "enqueue %.0f (pin %.0f h2d %.0f launch %.0f d2h %.0f event %.0f) device_wait %.0f scatter %.0f us\n",
                 window_us, (double)f.t_launch * 1e-9, f.L.items(), f.L.kinds(), f.L.slot,
                 f.L.stage_ns[COA_QSTAGE_SLOT_WAIT] * 1e-3, f.L.stage_ns[COA_QSTAGE_PACK] * 1e-3,
-                f.L.stage_ns[COA_QSTAGE_ENQUEUE] * 1e-3, f.L.stage_ns[COA_QSTAGE_DEVICE_WAIT] * 1e-3,
-                f.L.stage_ns[COA_QSTAGE_SCATTER] * 1e-3);
+                f.L.stage_ns[COA_QSTAGE_ENQUEUE] * 1e-3, f.L.enq_ns[Launch::ENQ_PIN] * 1e-3,
+                f.L.enq_ns[Launch::ENQ_H2D] * 1e-3, f.L.enq_ns[Launch::ENQ_LAUNCH] * 1e-3,
+                f.L.enq_ns[Launch::ENQ_D2H] * 1e-3, f.L.enq_ns[Launch::ENQ_EVENT] * 1e-3,
+                f.L.stage_ns[COA_QSTAGE_DEVICE_WAIT] * 1e-3, f.L.stage_ns[COA_QSTAGE_SCATTER] * 1e-3);
       }
       const bool retried = recoverable(f.L.rc);
       if (retried) recover(f.L);

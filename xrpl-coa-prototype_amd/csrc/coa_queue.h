@@ -142,6 +142,11 @@ struct Launch {
   // time per COA_QSTAGE_* stage; the backend adds PACK, ENQUEUE, DEVICE_WAIT
   // and SCATTER (retries included), the queue the others
   int64_t stage_ns[COA_QSTAGES] = {};
+  // the ENQUEUE stage split by the backend's calls (diagnostics, printed with
+  // COA_QUEUE_TRACE_SLOW_US): key-cache pin, host-to-device copy, kernel
+  // launches, device-to-host copy, completion event
+  enum { ENQ_PIN, ENQ_H2D, ENQ_LAUNCH, ENQ_D2H, ENQ_EVENT, ENQ_PARTS };
+  int64_t enq_ns[ENQ_PARTS] = {};
   // COA_QUEUE_KIND_* bits of the kinds the launch holds
   uint32_t kinds() const {
     return (nv ? COA_QUEUE_KIND_SIGNATURES : 0u) | (ng ? COA_QUEUE_KIND_BATCHES : 0u) |

@@ -590,6 +590,14 @@ class HipBackend : public coa_q::Backend {
       std::chrono::steady_clock::time_point t;
       ~EnqClock() { L.stage_ns[COA_QSTAGE_ENQUEUE] += ns_between(t, std::chrono::steady_clock::now()); }
     } enq_clock{L, t_enq};
+    // the ENQUEUE stage's parts (Launch::enq_ns): each mark() charges the time
+    // since the previous one to part k
+    auto t_mark = t_enq;
+    auto mark = [&](int k) {
+      const auto t = std::chrono::steady_clock::now();
+      L.enq_ns[k] += ns_between(t_mark, t);
+      t_mark = t;
+    };
     sl.cpub = false;
     sl.inl = inline_ok_ && sl.lat && L.nv <= COA_LAT_INLINE && L.nc == 0 && L.nd == 0 && lat_words(sl) != nullptr;
     if (sl.inl) {
@@ -605,10 +613,14 @@ class HipBackend : public coa_q::Backend {
       if (inject) return COA_EHIP;  // fault injection: nothing launched
       if (!sl.keys) sl.keys = coa_keycache_pin(sl.dev);
       coa_keycache_use(sl.keys);
+      mark(coa_q::Launch::ENQ_PIN);
       const int rc = coa_lat_verify_inline(sl.dev, h + i_vm, L.nv, sl.lres, sl.ltag, sl.s);
       coa_keycache_use(nullptr);
+      mark(coa_q::Launch::ENQ_LAUNCH);
       if (rc != COA_OK) return rc;
-      return hipEventRecord(sl.ev, sl.s) == hipSuccess ? COA_OK : COA_EHIP;
+      const hipError_t er = hipEventRecord(sl.ev, sl.s);
+      mark(coa_q::Launch::ENQ_EVENT);
+      return er == hipSuccess ? COA_OK : COA_EHIP;
     }
     sl.cpub = inline_ok_ && L.nc > 0 && L.nc <= COA_LAT_RES_WORDS && L.nv == 0 && L.nd == 0 &&
               lat_words(sl) != nullptr && ctr_words(sl) != nullptr;
@@ -623,13 +635,17 @@ class HipBackend : public coa_q::Backend {
       if (sl.ltag == 0) sl.ltag = 1;
       if (!sl.keys) sl.keys = coa_keycache_pin(sl.dev);
       coa_keycache_use(sl.keys);
+      mark(coa_q::Launch::ENQ_PIN);
       const CoaCertOffsets off{i_ch, i_cho, i_cid, i_cor, i_chs, i_crd, i_cvp, i_cvs, i_cvo};
       const int rc = coa_certificate_verify_publish(sl.dev, h, static_cast<uint8_t*>(sl.din), in_bytes, &off, L.nc,
                                                     L.nvotes, sl.dctr, sl.lres, sl.ltag, sl.s);
       coa_keycache_use(nullptr);
+      mark(coa_q::Launch::ENQ_LAUNCH);  // (its H2D copy, when the window does not fit the arguments, included)
       if (rc == COA_OK) {
         sl.launched = true;
-        return hipEventRecord(sl.ev, sl.s) == hipSuccess ? COA_OK : COA_EHIP;
+        const hipError_t er = hipEventRecord(sl.ev, sl.s);
+        mark(coa_q::Launch::ENQ_EVENT);
+        return er == hipSuccess ? COA_OK : COA_EHIP;
       }
       if (rc != 1) {
         sl.launched = true;  // something may be enqueued: finish() drains the stream
@@ -640,6 +656,7 @@ class HipBackend : public coa_q::Backend {
     uint8_t* d = static_cast<uint8_t*>(sl.din);
     uint8_t* dout = static_cast<uint8_t*>(sl.dout);
     if (hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, sl.s) != hipSuccess) return COA_EHIP;
+    mark(coa_q::Launch::ENQ_H2D);
     sl.launched = true;
     if (inject) return COA_EHIP;  // fault injection: the copy is in flight, the kernels never run
     int rc = COA_OK;
@@ -648,6 +665,7 @@ class HipBackend : public coa_q::Backend {
     // one beside it) and its launches read that one
     if ((sl.lat || L.nc) && !sl.keys) sl.keys = coa_keycache_pin(sl.dev);
     coa_keycache_use(sl.keys);
+    mark(coa_q::Launch::ENQ_PIN);
     if (L.nv && sl.lat)
       rc = coa_lat_verify_device(sl.dev, d + i_vm, L.nv, reinterpret_cast<uint32_t*>(dout + sl.o_v), sl.s);
     else if (L.nv)
@@ -666,9 +684,12 @@ class HipBackend : public coa_q::Backend {
       rc = coa_sha512_many_device(sl.dev, d + i_dd, reinterpret_cast<const uint64_t*>(d + i_do), L.nd, dout + sl.o_d,
                                   sl.s);
     coa_keycache_use(nullptr);
+    mark(coa_q::Launch::ENQ_LAUNCH);
     if (rc != COA_OK) return rc;
     if (hipMemcpyAsync(sl.hout, dout, out_bytes, hipMemcpyDeviceToHost, sl.s) != hipSuccess) return COA_EHIP;
+    mark(coa_q::Launch::ENQ_D2H);
     if (hipEventRecord(sl.ev, sl.s) != hipSuccess) return COA_EHIP;
+    mark(coa_q::Launch::ENQ_EVENT);
     return COA_OK;
   }
 
