@@ -459,7 +459,12 @@ class HipBackend : public coa_q::Backend {
     // COA_QUEUE_INLINE=0: small signature windows take the staged path too (A/B)
     if (const char* e = getenv("COA_QUEUE_INLINE")) inline_ok_ = e[0] != '0';
     // COA_QUEUE_KEYSORT=0|1: certificate windows of >= 16,384 jobs take their
-    // jobs in committee-key order (coa_certificate_verify_many_device_order)
+    // jobs in committee-key order (coa_certificate_verify_many_device_order).
+    // Default on: round 6's same-box A/B of the streamed C3 lines was within
+    // noise either way (profiles/r06_keysort_ab.txt), and the fused kernel's
+    // translation misses fall from ~50 % to ~1.5 % of requests in key order
+    // (round 5); coa_committee.hip's note that queue windows do not sort
+    // predates this switch
     if (const char* e = getenv("COA_QUEUE_KEYSORT")) keysort_ = e[0] != '0';
     kind_ = stream_kind_env();
     slots_.resize(per * devs_.size());

@@ -197,6 +197,15 @@ struct DevShared {
   // the next registration: a 65 GB allocation clears its memory on the
   // device, which held live windows back 2.4-7.6 ms (profiles/r04_register_ab.txt)
   std::shared_ptr<KeySet> spare;
+  // Generations read by kernels a device-pointer call enqueued on a caller's
+  // stream and returned from (the call's own pin is gone): each held until
+  // its event completes.  The registrar waits for these instead of a
+  // hipDeviceSynchronize, which blocked every other thread's kernel launches
+  // for its whole wait (a queue window's launch 13.2 ms, exactly the
+  // registrar's sync: profiles/r06_regtrace.txt).
+  std::mutex trail_mu;
+  std::vector<std::pair<hipEvent_t, KeySetP>> trailing;
+  std::vector<hipEvent_t> trail_events;  // completed ones, for reuse
 };
 
 // Host copies split over a few persistent threads: packing a round of
@@ -422,6 +431,51 @@ KeySetP keys_now(const Dev& d) {
   if (t_keys_pinned && *t_keys_pinned && (*t_keys_pinned)->dev == d.id) return *t_keys_pinned;
   std::lock_guard<std::mutex> l(d.sh->mu);
   return d.sh->keys;
+}
+
+// Drops the trailing generations whose kernels have completed (an event in
+// error counts as complete: nothing more will read through it).
+void reap_trailing(DevShared& sh) {
+  std::lock_guard<std::mutex> l(sh.trail_mu);
+  for (size_t i = 0; i < sh.trailing.size();) {
+    if (hipEventQuery(sh.trailing[i].first) != hipErrorNotReady) {
+      sh.trail_events.push_back(sh.trailing[i].first);
+      sh.trailing[i] = std::move(sh.trailing.back());
+      sh.trailing.pop_back();
+    } else {
+      i++;
+    }
+  }
+  (void)hipGetLastError();
+}
+
+// A device-pointer call that read generation `ks` in kernels it enqueued on
+// `s` and returns before they complete: `ks` stays held until they have (an
+// event on `s`).  Windows of the aggregation queue pin their generation until
+// complete() and need none.  If no event can be recorded, the call waits for
+// its stream instead.
+int trail_keys(Dev& d, const KeySetP& ks, hipStream_t s) {
+  if (t_keys_pinned && *t_keys_pinned) return COA_OK;
+  DevShared& sh = *d.sh;
+  reap_trailing(sh);
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> l(sh.trail_mu);
+    if (!sh.trail_events.empty()) {
+      ev = sh.trail_events.back();
+      sh.trail_events.pop_back();
+    }
+  }
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+  if (!ev || hipEventRecord(ev, s) != hipSuccess) {
+    if (ev) (void)hipEventDestroy(ev);
+    (void)hipGetLastError();
+    HIP_TRY(hipStreamSynchronize(s));
+    return COA_OK;
+  }
+  std::lock_guard<std::mutex> l(sh.trail_mu);
+  sh.trailing.emplace_back(ev, ks);
+  return COA_OK;
 }
 
 int open_device(int d) {
@@ -1770,14 +1824,17 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
     sh.keys = std::move(ks);
   }
   // the old generation: calls and windows that took it still hold it (their
-  // kernels read it until they complete); a device-pointer call on a caller's
-  // stream holds it only while it enqueues, so its kernels are waited for
-  // below.  Only this thread waits.
+  // kernels read it until they complete), and a device-pointer call on a
+  // caller's stream left it in `trailing` with an event after its kernels
+  // (trail_keys).  Only this thread waits -- no hipDeviceSynchronize, which
+  // held every other thread's launches for its whole wait.
   const auto t_swap = clk::now();
-  while (old.use_count() > 1) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  while (old.use_count() > 1) {
+    reap_trailing(sh);
+    if (old.use_count() > 1) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
   const auto t_unpinned = clk::now();
-  HIP_TRY(hipDeviceSynchronize());
-  const auto t_synced = clk::now();
+  const auto t_synced = t_unpinned;
   // the replaced generation's buffers become the spare of the next
   // registration; after the first registration of a device (nothing to
   // replace yet) a spare of the same size is allocated now, while the
@@ -1876,6 +1933,16 @@ int coa_shutdown(void) {
     (void)hipSetDevice(sh->id);
     if (sh->wcomb) (void)hipFree(sh->wcomb);
     if (sh->build) (void)hipStreamDestroy(sh->build);
+    {
+      std::lock_guard<std::mutex> t(sh->trail_mu);
+      for (auto& e : sh->trailing) {
+        (void)hipEventSynchronize(e.first);
+        (void)hipEventDestroy(e.first);
+      }
+      for (hipEvent_t e : sh->trail_events) (void)hipEventDestroy(e);
+      sh->trailing.clear();
+      sh->trail_events.clear();
+    }
     std::lock_guard<std::mutex> l(sh->mu);
     sh->keys.reset();
   }
@@ -2281,8 +2348,9 @@ int coa_lat_verify_device(int device, const uint8_t* d_in, size_t n, uint32_t* d
   a.ktabs = ks->ktabs.as<uint32_t>();
   a.nk = ks->nkeys;
   a.comb = d->comb;
-  HIP_TRY(coa_launch_verify_lat(a, stream ? (hipStream_t)stream : d->stream));
-  return COA_OK;
+  const hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  HIP_TRY(coa_launch_verify_lat(a, s));
+  return trail_keys(*d, ks, s);
 }
 
 int coa_lat_verify_inline(int device, const uint8_t* h_records, size_t n, uint32_t* res, uint32_t tag, void* stream) {
@@ -2306,8 +2374,9 @@ int coa_lat_verify_inline(int device, const uint8_t* h_records, size_t n, uint32
   a.ktabs = ks->ktabs.as<uint32_t>();
   a.nk = ks->nkeys;
   a.comb = d->comb;
-  HIP_TRY(coa_launch_verify_lat(a, stream ? (hipStream_t)stream : d->stream));
-  return COA_OK;
+  const hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  HIP_TRY(coa_launch_verify_lat(a, s));
+  return trail_keys(*d, ks, s);
 }
 
 int coa_certificate_verify_publish(int device, const uint8_t* h_base, uint8_t* d_base, size_t in_bytes,
@@ -2341,7 +2410,7 @@ int coa_certificate_verify_publish(int device, const uint8_t* h_base, uint8_t* d
     a.done_ctr = d_ctr;
     a.tag = tag;
     HIP_TRY(coa_launch_cert_verify_inl(ci, s));
-    return COA_OK;
+    return trail_keys(*d, ks, s);
   }
   HIP_TRY(hipMemcpyAsync(d_base, h_base, in_bytes, hipMemcpyHostToDevice, s));
   CertPack p{};
@@ -2360,7 +2429,7 @@ int coa_certificate_verify_publish(int device, const uint8_t* h_base, uint8_t* d
   a.done_ctr = d_ctr;
   a.tag = tag;
   HIP_TRY(coa_launch_cert_verify(a, 64, nullptr, s));
-  return COA_OK;
+  return trail_keys(*d, ks, s);
 }
 
 int coa_engine_recoveries(uint64_t* contexts_rebuilt, uint64_t* shards_rerun) {
@@ -2484,7 +2553,7 @@ int coa_certificate_verify_many_device_order(int device, const uint8_t* d_header
   HIP_TRY(hipMemsetAsync(d_status, 0, n * 4, s));
   if (workspace || lanes == 64) {
     HIP_TRY(coa_launch_cert_verify(a, lanes, static_cast<uint32_t*>(workspace), s));
-    return COA_OK;
+    return trail_keys(*d, ks, s);
   }
   std::lock_guard<std::mutex> l(d->mu);
   HIP_TRY(d->cscr.ensure(coa_cert_scratch_bytes(n + n_votes, a.key_order != 0)));
