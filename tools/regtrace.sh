@@ -8,6 +8,6 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && export TMPDIR=/tmp && mkdir -p gp
 for rep in $(seq ${REPS:-2}); do
   COA_QUEUE_TRACE_SLOW_US=${SLOW_US:-2000} COA_REGISTER_TRACE=1 timeout -k 10 300 \
     python3 -m pytest tests/test_gpu_recovery.py -m gpu -s -q -k "register" --timeout 200 \
-    > gpurun_out/regtrace_$rep.log 2>&1
-  grep -E "slow window|coa_committee_register|passed|failed" gpurun_out/regtrace_$rep.log | cut -c1-260
+    > gpurun_out/regtrace_${TAG:-x}_$rep.log 2>&1
+  grep -E "slow window|coa_committee_register|passed|failed" gpurun_out/regtrace_${TAG:-x}_$rep.log | cut -c1-260
 done

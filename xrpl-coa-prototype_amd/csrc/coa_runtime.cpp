@@ -206,6 +206,10 @@ struct DevShared {
   std::mutex trail_mu;
   std::vector<std::pair<hipEvent_t, KeySetP>> trailing;
   std::vector<hipEvent_t> trail_events;  // completed ones, for reuse
+  // (under reg_mu) page-locked staging of the committee's keys: a copy from
+  // pageable memory is staged by HIP itself, synchronously
+  void* kstage = nullptr;
+  size_t kstage_cap = 0;
 };
 
 // Host copies split over a few persistent threads: packing a round of
@@ -1779,7 +1783,19 @@ int build_keyset(DevShared& sh, const std::vector<std::array<uint32_t, 8>>& keys
     HIP_TRY(ks->ckeys.ensure(nk * 32));
     HIP_TRY(ks->kflags.ensure(nk * 4));
     HIP_TRY(ks->ktabs.ensure(nk * (size_t)COA_KEY_TAB_DWORDS * 4));
-    HIP_TRY(hipMemcpyAsync(ks->ckeys.p, keys.data(), nk * 32, hipMemcpyHostToDevice, s));
+    if (env_is("COA_REGISTER_PAGEABLE", "1")) {  // A/B: the keys straight from the caller's (pageable) vector
+      HIP_TRY(hipMemcpyAsync(ks->ckeys.p, keys.data(), nk * 32, hipMemcpyHostToDevice, s));
+    } else {
+      if (sh.kstage_cap < nk * 32) {
+        if (sh.kstage) HIP_TRY(hipHostFree(sh.kstage));
+        sh.kstage = nullptr;
+        sh.kstage_cap = 0;
+        HIP_TRY(hipHostMalloc(&sh.kstage, nk * 32, hipHostMallocDefault));
+        sh.kstage_cap = nk * 32;
+      }
+      std::memcpy(sh.kstage, keys.data(), nk * 32);
+      HIP_TRY(hipMemcpyAsync(ks->ckeys.p, sh.kstage, nk * 32, hipMemcpyHostToDevice, s));
+    }
     HIP_TRY(coa_launch_key_flags(ks->ckeys.as<uint32_t>(), (uint32_t)nk, ks->kflags.as<uint32_t>(), s));
     HIP_TRY(coa_launch_key_tables(ks->ckeys.as<uint32_t>(), (uint32_t)nk, ks->ktabs.as<uint32_t>(), s));
     // wide combs when the committee fits the budget: radix 2^20 (654 MB per
@@ -1933,6 +1949,7 @@ int coa_shutdown(void) {
     (void)hipSetDevice(sh->id);
     if (sh->wcomb) (void)hipFree(sh->wcomb);
     if (sh->build) (void)hipStreamDestroy(sh->build);
+    if (sh->kstage) (void)hipHostFree(sh->kstage);
     {
       std::lock_guard<std::mutex> t(sh->trail_mu);
       for (auto& e : sh->trailing) {
