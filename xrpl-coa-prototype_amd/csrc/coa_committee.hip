@@ -760,7 +760,7 @@ __global__ void __launch_bounds__(256) k_key_wcomb(const uint32_t* __restrict__ 
   comb_select(q, ktab, 2 * j + 1, hi);
   ge_madd(t, P, q);
   ge_p1p1_to_p3(P, t);
-  store_niels(wtabs + (uint64_t)key * COA_KWCOMB_DWORDS + (uint64_t)e * 24, P);
+  store_niels(wtabs + (uint64_t)key * COA_KWCOMB_DWORDS + (uint64_t)e * COA_WC_STRIDE, P);
   }
 }
 
@@ -807,7 +807,7 @@ __global__ void __launch_bounds__(256) k_key_wcomb20(const uint32_t* __restrict_
     ge_madd(t, P, qn);
     ge_p1p1_to_p3(P, t);
   }
-  store_niels(wtabs + (uint64_t)key * COA_KWCOMB20_DWORDS + e * 24, P);
+  store_niels(wtabs + (uint64_t)key * COA_KWCOMB20_DWORDS + e * COA_WC_STRIDE, P);
   }
 }
 

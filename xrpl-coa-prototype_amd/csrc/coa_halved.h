@@ -13,7 +13,16 @@
 #endif
 #define COA_WCOMB_MAG (1u << (COA_WCOMB_W - 1))
 #define COA_WCOMB_ENTRIES ((uint64_t)COA_WCOMB_POS * COA_WCOMB_MAG)
-#define COA_WCOMB_DWORDS (COA_WCOMB_ENTRIES * 24)
+// Dwords per wide-comb entry (B's comb and the keys' wide combs): the
+// entry's 24 (y+x, y-x, 2dxy) plus 8 of padding, so an entry is one 128-byte
+// line.  At 24 an entry at a random index straddles two lines half the time:
+// 1.5 lines (192 B) fetched per 96 B used, the C3 round's 2.15x traffic over
+// its algorithmic bytes (DESIGN.md §4 "C3 roofline").  -DCOA_WC_STRIDE=24:
+// the round-5 layout (A/B builds, tools/build_variant.py).
+#ifndef COA_WC_STRIDE
+#define COA_WC_STRIDE 32
+#endif
+#define COA_WCOMB_DWORDS (COA_WCOMB_ENTRIES * COA_WC_STRIDE)
 #define COA_COMB_ENTRIES (32 * 128)
 #define COA_COMB_DWORDS (COA_COMB_ENTRIES * 24)
 // k_halve record per signature: c[8] | |d|[8] | e[8] | meta | pad[7]

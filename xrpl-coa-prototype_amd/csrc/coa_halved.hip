@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(256) k_build_wcomb(uint32_t* __restrict__ wcom
   fe_canon(n0, n0);
   fe_canon(n1, n1);
   fe_canon(n2, n2);
-  uint4* o = reinterpret_cast<uint4*>(wcomb + id * 24);
+  uint4* o = reinterpret_cast<uint4*>(wcomb + id * COA_WC_STRIDE);
   o[0] = make_uint4(n0.v[0], n0.v[1], n0.v[2], n0.v[3]);
   o[1] = make_uint4(n0.v[4], n0.v[5], n0.v[6], n0.v[7]);
   o[2] = make_uint4(n1.v[0], n1.v[1], n1.v[2], n1.v[3]);

@@ -165,7 +165,7 @@ template <int W>
 COA_DEV void wc_load(uint32_t* w, const uint32_t* __restrict__ tab, int j, int d) {
   const uint32_t m = (uint32_t)(d < 0 ? -d : d);
   const uint64_t idx = (uint64_t)j * (1u << (W - 1)) + (m ? m - 1 : 0);
-  const uint4* src = reinterpret_cast<const uint4*>(tab + idx * 24);
+  const uint4* src = reinterpret_cast<const uint4*>(tab + idx * COA_WC_STRIDE);
 #pragma unroll
   for (int i = 0; i < 6; i++) {
     const uint4 v = src[i];
