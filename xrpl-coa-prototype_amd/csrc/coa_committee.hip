@@ -236,9 +236,9 @@ COA_DEV void job_comb(const CertArgs& a, uint32_t job, ge_p3& P, uint32_t& pre, 
     }
   }
   if (a.kwtabs && a.kw20) {
-    wc_accumulate<COA_KWCOMB20_W, COA_KWCOMB20_POS>(P, k.v, a.kwtabs + (uint64_t)slot * COA_KWCOMB20_DWORDS);
+    wc_accumulate<COA_KWCOMB20_W, COA_KWCOMB20_POS, COA_KWC_STRIDE>(P, k.v, a.kwtabs + (uint64_t)slot * COA_KWCOMB20_DWORDS);
   } else if (a.kwtabs) {
-    wc_accumulate<COA_KWCOMB_W, COA_KWCOMB_POS>(P, k.v, a.kwtabs + (uint64_t)slot * COA_KWCOMB_DWORDS);
+    wc_accumulate<COA_KWCOMB_W, COA_KWCOMB_POS, COA_KWC_STRIDE>(P, k.v, a.kwtabs + (uint64_t)slot * COA_KWCOMB_DWORDS);
   } else {
 #pragma unroll 1
     for (int j = 0; j < 32; j++) {
@@ -760,7 +760,7 @@ __global__ void __launch_bounds__(256) k_key_wcomb(const uint32_t* __restrict__ 
   comb_select(q, ktab, 2 * j + 1, hi);
   ge_madd(t, P, q);
   ge_p1p1_to_p3(P, t);
-  store_niels(wtabs + (uint64_t)key * COA_KWCOMB_DWORDS + (uint64_t)e * COA_WC_STRIDE, P);
+  store_niels(wtabs + (uint64_t)key * COA_KWCOMB_DWORDS + (uint64_t)e * COA_KWC_STRIDE, P);
   }
 }
 
@@ -807,7 +807,7 @@ __global__ void __launch_bounds__(256) k_key_wcomb20(const uint32_t* __restrict_
     ge_madd(t, P, qn);
     ge_p1p1_to_p3(P, t);
   }
-  store_niels(wtabs + (uint64_t)key * COA_KWCOMB20_DWORDS + e * COA_WC_STRIDE, P);
+  store_niels(wtabs + (uint64_t)key * COA_KWCOMB20_DWORDS + e * COA_KWC_STRIDE, P);
   }
 }
 

@@ -13,12 +13,13 @@
 #endif
 #define COA_WCOMB_MAG (1u << (COA_WCOMB_W - 1))
 #define COA_WCOMB_ENTRIES ((uint64_t)COA_WCOMB_POS * COA_WCOMB_MAG)
-// Dwords per wide-comb entry (B's comb and the keys' wide combs): the
-// entry's 24 (y+x, y-x, 2dxy) plus 8 of padding, so an entry is one 128-byte
-// line.  At 24 an entry at a random index straddles two lines half the time:
-// 1.5 lines (192 B) fetched per 96 B used, the C3 round's 2.15x traffic over
-// its algorithmic bytes (DESIGN.md §4 "C3 roofline").  -DCOA_WC_STRIDE=24:
-// the round-5 layout (A/B builds, tools/build_variant.py).
+// Dwords per entry of B's wide comb: the entry's 24 (y+x, y-x, 2dxy) plus 8
+// of padding, so an entry is one 128-byte line.  At 24 an entry at a random
+// index straddles two lines half the time: 1.5 lines (192 B) fetched per 96 B
+// used.  Same-box A/B (profiles/r06_stride_ab.txt): C2 +0.2-0.65 % in three
+// of three pairs for 3 GB more (11.9 GB); the keys' combs gained nothing on
+// the C3 round (VALU-bound, DESIGN.md §4 "C3 roofline") and keep 24
+// (COA_KWC_STRIDE, coa_committee.h).  -DCOA_WC_STRIDE=24: the round-5 layout.
 #ifndef COA_WC_STRIDE
 #define COA_WC_STRIDE 32
 #endif

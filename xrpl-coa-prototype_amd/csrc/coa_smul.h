@@ -160,12 +160,13 @@ COA_DEV int wc_take_digit(uint32_t* r) {
   r[8] >>= W;
   return d;
 }
-// Raw 24 words of entry (j, |d|) (entry (j, 0) for d == 0; ignored then).
-template <int W>
+// Raw 24 words of entry (j, |d|) (entry (j, 0) for d == 0; ignored then);
+// entries STRIDE dwords apart.
+template <int W, int STRIDE>
 COA_DEV void wc_load(uint32_t* w, const uint32_t* __restrict__ tab, int j, int d) {
   const uint32_t m = (uint32_t)(d < 0 ? -d : d);
   const uint64_t idx = (uint64_t)j * (1u << (W - 1)) + (m ? m - 1 : 0);
-  const uint4* src = reinterpret_cast<const uint4*>(tab + idx * COA_WC_STRIDE);
+  const uint4* src = reinterpret_cast<const uint4*>(tab + idx * STRIDE);
 #pragma unroll
   for (int i = 0; i < 6; i++) {
     const uint4 v = src[i];
@@ -187,18 +188,18 @@ COA_DEV void wcomb_apply(ge_niels& q, const uint32_t* w, int d) {
 }
 // acc += [x]P from P's wide comb (x < 2^253; a larger x gives some point,
 // never an out-of-range entry).  Entry j+1 is loaded while addition j runs.
-template <int W, int POS, bool IL = false>
+template <int W, int POS, int STRIDE, bool IL = false>
 COA_DEV void wc_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __restrict__ tab) {
   uint32_t r[9], cur[24], nxt[24];
   wc_recode<W, POS>(r, x);
   int d = wc_take_digit<W>(r);
-  wc_load<W>(cur, tab, 0, d);
+  wc_load<W, STRIDE>(cur, tab, 0, d);
   ge_p1p1 t;
 #pragma unroll 1
   for (int j = 0; j < POS; j++) {
     const int jn = j + 1 < POS ? j + 1 : j;
     const int dn = wc_take_digit<W>(r);
-    wc_load<W>(nxt, tab, jn, dn);
+    wc_load<W, STRIDE>(nxt, tab, jn, dn);
     ge_niels q;
     wcomb_apply(q, cur, d);
     if constexpr (IL) {  // interleaved products (coa_ge.h *_il)
@@ -216,11 +217,11 @@ COA_DEV void wc_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __rest
 
 // The wide comb of B (COA_WCOMB_*, coa_halved.h).
 COA_DEV void wcomb_load(uint32_t* w, const uint32_t* __restrict__ tab, int j, int d) {
-  wc_load<COA_WCOMB_W>(w, tab, j, d);
+  wc_load<COA_WCOMB_W, COA_WC_STRIDE>(w, tab, j, d);
 }
 template <bool IL = false>
 COA_DEV void wcomb_accumulate(ge_p3& acc, const uint32_t* x, const uint32_t* __restrict__ tab) {
-  wc_accumulate<COA_WCOMB_W, COA_WCOMB_POS, IL>(acc, x, tab);
+  wc_accumulate<COA_WCOMB_W, COA_WCOMB_POS, COA_WC_STRIDE, IL>(acc, x, tab);
 }
 
 COA_DEV uint32_t take_low_byte(uint32_t* x) {
