@@ -60,7 +60,7 @@ VALU_ISSUE_CYCLES = 2  # one full-rate wave64 VALU instruction per 2 cycles per 
 PEAK_INT32_TOPS = SIMDS * 32 * CLOCK_HZ / 1e12
 C2_N = 65536
 # counter profile of the C2 verify call (tools/pmc_verify.py), tied to a build
-PMC_JSON = "r05_verify_pmc.json"
+PMC_JSON = "r06_verify_pmc.json"
 
 
 def parse(argv=None):
