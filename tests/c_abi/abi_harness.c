@@ -134,6 +134,34 @@ int main(int argc, char** argv) {
         "certificate_verify_many_device(n=0)");
   CHECK(coa_committee_register(NULL, 0) == (gpu ? 0 : COA_ENODEVICE), "committee_register(clear)");
 
+  /* the engine's own CPU path: host-only, the same verdicts with or without
+     a GPU (what the Rust policy answers with when every context failed) */
+  CHECK(coa_cpu_ed25519_verify_strict(msg, 32, pk, sig) == COA_OK, "cpu verify_strict ok");
+  CHECK(coa_cpu_ed25519_verify_strict(msg, 32, pk, bad) == COA_REJECT, "cpu verify_strict bad");
+  uint8_t cv[2] = {9, 9};
+  CHECK(coa_cpu_ed25519_verify_strict_many(msgs2, 32, pks2, sigs2, 2, cv, 2) == COA_OK && cv[0] == 0 && cv[1] == 1,
+        "cpu verify_strict_many");
+  CHECK(coa_cpu_ed25519_verify_batch(msg, pk, sig, 1, 5) == COA_OK, "cpu verify_batch ok");
+  CHECK(coa_cpu_ed25519_verify_batch(msg, pk, bad, 1, 0) == COA_REJECT, "cpu verify_batch bad");
+  uint8_t cg[2] = {9, 9};
+  CHECK(coa_cpu_ed25519_verify_batch_groups_z(msgs2, pks2, sigs2, goff, 2, zs, cg, 0) == COA_OK && cg[0] == 0 &&
+            cg[1] == 1,
+        "cpu verify_batch_groups_z");
+  uint8_t c64[64];
+  CHECK(coa_cpu_sha512_many(data, doff, 1, c64, 1) == COA_OK && memcmp(c64, msg, 32) == 0, "cpu sha512_many");
+  /* a certificate whose header hashes to `msg` ("Hello, world!"), signed
+     header, no votes: only the header signature check can fail -- it is by
+     the fixture's key over that very digest, so every bit is clear */
+  uint8_t cst = 9;
+  CHECK(coa_cpu_certificate_verify_many(data, hoff, msg, pk, sig, rounds, NULL, NULL, voff, 1, 3, &cst, 1) == COA_OK &&
+            cst == 0,
+        "cpu certificate_verify_many");
+  CHECK(coa_cpu_certificate_verify_many_z(data, hoff, msg, pk, bad, rounds, NULL, NULL, voff, 1, NULL, &cst, 1) ==
+                COA_OK &&
+            cst == COA_CERT_BAD_HEADER_SIG,
+        "cpu certificate_verify_many_z");
+  CHECK(coa_cpu_ed25519_verify_strict_many(NULL, 32, NULL, NULL, 1, NULL, 1) == COA_EINVAL, "cpu (null)");
+
   /* wire decode: host-only, identical with or without a GPU */
   const uint8_t trunc[3] = {2, 0, 0};  /* a Certificate variant tag cut short */
   const uint64_t toff[2] = {0, 3};
