@@ -286,6 +286,7 @@ struct Lane {
   std::deque<Flight> flight;  // launched, not yet answered (launch order)
   size_t busy = 0;            // windows taken by the collector and not yet answered
   bool flush = false, collector_done = false;
+  int collectors_live = 0;  // collector threads not yet exited
   std::deque<Deferred> open;  // deferred parts waiting for the resolver
   size_t resolving = 0;       // deferred parts not yet answered (queued or in a pass)
   bool resolver_stop = false;
@@ -309,7 +310,16 @@ struct Lane {
   double m_resolve_us_max = 0.0;
   double m_stage_us[COA_QSTAGES] = {};
 
-  std::thread collector, completer, resolver;
+  // COA_QUEUE_COLLECTORS (1..4, default 2; read at creation): collector
+  // threads.  A window's pack (its requests' bytes into the slot's
+  // page-locked staging, ~13 MB for a streamed C3 window) runs on the thread
+  // that closed the window, so with one collector the next window could not
+  // be gathered until that pack was done: the streamed C3 path's bound
+  // (gather + pack + enqueue ~300 us per window of ~1,300 certificates, one
+  // thread).  A second collector closes and packs the next window meanwhile.
+  std::vector<std::thread> collectors;
+  std::thread completer, resolver;
+  std::mutex prep_mu;  // one prepare() (cold lane) at a time
   AnswerPool helpers;  // started lazily by the first large launch
   int n_helpers = kHelpersDefault;
   bool helpers_on = false;
@@ -331,7 +341,10 @@ struct Lane {
   }
 
   void start() {
-    collector = std::thread([this] { collect(); });
+    int n = 2;
+    if (const char* e = getenv("COA_QUEUE_COLLECTORS")) n = std::max(1, std::min(4, atoi(e)));
+    collectors_live = n;
+    for (int i = 0; i < n; i++) collectors.emplace_back([this] { collect(); });
     completer = std::thread([this] { answer(); });
     resolver = std::thread([this] { resolve_loop(); });
   }
@@ -460,8 +473,10 @@ struct Lane {
       busy++;  // before the take: flush must not see pend == 0 and busy == 0 meanwhile
       launch_window(l);
     }
-    collector_done = true;
-    flight_cv.notify_one();
+    if (--collectors_live == 0) {  // the last collector out (under mu)
+      collector_done = true;
+      flight_cv.notify_one();
+    }
   }
 
   // Takes the pending requests as one window and launches it: the collector,
@@ -489,8 +504,11 @@ struct Lane {
     f.L.attempts = 1;
     f.t_launch = now_ns();
     if (!prepared.load()) {  // a lane COA_QUEUE_LANES left cold: set up by its first window (the collector's)
-      be->prepare(max_batch);
-      prepared.store(true);
+      std::lock_guard<std::mutex> p(prep_mu);
+      if (!prepared.load()) {
+        be->prepare(max_batch);
+        prepared.store(true);
+      }
     }
     be->launch(f.L);  // stages and enqueues; blocks only while every slot is busy
     f.L.stage_ns[COA_QSTAGE_SLOT_WAIT] += f.L.slot_wait_ns;
@@ -755,9 +773,9 @@ struct Lane {
     {
       std::lock_guard<std::mutex> l(mu);
       stop = true;
-      cv.notify_one();
+      cv.notify_all();
     }
-    collector.join();
+    for (std::thread& c : collectors) c.join();
     completer.join();
     {
       std::lock_guard<std::mutex> l(mu);

@@ -257,29 +257,28 @@ class CopyPool {
     }
     if (cuts.back() != pieces.size()) cuts.push_back(pieces.size());
     const size_t nchunks = cuts.size() - 1;
-    // one job at a time on the pool; a caller that finds it busy (another
-    // lane's window, a host call) copies on its own thread instead of waiting
-    std::unique_lock<std::mutex> call(call_mu_, std::try_to_lock);
-    if (nchunks <= 1 || th_.empty() || !call.owns_lock()) {
+    if (nchunks <= 1 || th_.empty()) {
       for (const Seg& g : pieces) std::memcpy(g.dst, g.src, g.bytes);
       return;
     }
-    // the job's own counters: a worker that wakes late holds this job (never
-    // the next one's) and finds every chunk claimed
+    // Several jobs may be in progress at once (two collectors' windows, a
+    // host call): each has its own counters, the workers take chunks of the
+    // oldest job that has some left, and every caller works on its own job
+    // until it is claimed, then waits for the rest of it.  (Round 5 ran one
+    // job at a time and a second caller copied alone, at one core's rate.)
     auto job = std::make_shared<Job>();
     job->pieces = pieces.data();
     job->cuts = cuts.data();
     job->n = nchunks;
     {
       std::lock_guard<std::mutex> l(m_);
-      job_ = job;
-      gen_++;
+      jobs_.push_back(job);
     }
     cv_.notify_all();
     work(*job);
     std::unique_lock<std::mutex> l(m_);
     done_cv_.wait(l, [&] { return job->done.load(std::memory_order_acquire) == nchunks; });
-    job_.reset();
+    jobs_.erase(std::find(jobs_.begin(), jobs_.end(), job));
   }
   ~CopyPool() {
     {
@@ -316,24 +315,27 @@ class CopyPool {
       }
     }
   }
+  // the oldest job with unclaimed chunks (under m_), or null
+  std::shared_ptr<Job> open_job() const {
+    for (const auto& j : jobs_)
+      if (j->next.load(std::memory_order_relaxed) < j->n) return j;
+    return nullptr;
+  }
   void loop() {
-    uint64_t seen = 0;
     for (;;) {
       std::shared_ptr<Job> j;
       {
         std::unique_lock<std::mutex> l(m_);
-        cv_.wait(l, [&] { return stop_ || (gen_ != seen && job_); });
+        cv_.wait(l, [&] { return stop_ || open_job() != nullptr; });
         if (stop_) return;
-        seen = gen_;
-        j = job_;
+        j = open_job();
       }
       work(*j);
     }
   }
-  std::mutex call_mu_, m_;
+  std::mutex m_;
   std::condition_variable cv_, done_cv_;
-  std::shared_ptr<Job> job_;  // the job in progress (null between jobs)
-  uint64_t gen_ = 0;
+  std::vector<std::shared_ptr<Job>> jobs_;  // in progress, oldest first
   bool stop_ = false;
   std::vector<std::thread> th_;
 };
