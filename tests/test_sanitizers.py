@@ -94,3 +94,30 @@ def test_queue_many_producers_asan_ubsan():
     assert "2400/2400 answered, 0 wrong" in out and "recovered 0" in out and "engine errors 0" not in out, out
     out = _run([exe, "16", "500"], dict(env, COA_QUEUE_IDLE_LAUNCH="1"))
     assert "8000/8000 answered, 0 wrong" in out, out
+
+
+def _copy_pool_inc(dst_dir):
+    """The CopyPool class text of coa_runtime.cpp (the runtime itself needs
+    HIP; the class is plain C++)."""
+    src = open(os.path.join(CSRC, "coa_runtime.cpp")).read()
+    body = src[src.index("class CopyPool {"):src.index("struct Dev {")]
+    os.makedirs(dst_dir, exist_ok=True)
+    with open(os.path.join(dst_dir, "copy_pool_class.inc"), "w") as f:
+        f.write(body)
+    return dst_dir
+
+
+@pytest.mark.parametrize("san", ["thread", "address,undefined"])
+def test_copy_pool_concurrent_jobs(san):
+    """Round 6: several copies in progress on the pool at once (two
+    collectors' windows); a worker's job is taken in its wait predicate (a
+    second lookup after the wait raced the other workers' claims and came
+    back empty: a null job, SIGSEGV on a GPU box)."""
+    inc = _copy_pool_inc(os.path.join(ROOT, "tests", "sanitize", "_build"))
+    flags = ["-fsanitize=" + san, "-fno-sanitize-recover=all", "-I", inc]
+    cxx = CLANG if san == "thread" and os.path.exists(CLANG) else "g++"
+    exe = _build(os.path.join(inc, "copy_pool_" + san.split(",")[0]),
+                 [os.path.join(ROOT, "tests", "sanitize", "copy_pool_stress.cpp")], flags, cxx=cxx)
+    out = _run([exe], {"TSAN_OPTIONS": "halt_on_error=1", "ASAN_OPTIONS": "abort_on_error=1",
+                       "UBSAN_OPTIONS": "halt_on_error=1"})
+    assert "copy pool ok: 0 bad" in out

@@ -325,10 +325,11 @@ class CopyPool {
     for (;;) {
       std::shared_ptr<Job> j;
       {
+        // the job is taken by the predicate itself: chunks are claimed without
+        // the lock, so a second open_job() here could find none left
         std::unique_lock<std::mutex> l(m_);
-        cv_.wait(l, [&] { return stop_ || open_job() != nullptr; });
+        cv_.wait(l, [&] { return stop_ || (j = open_job()) != nullptr; });
         if (stop_) return;
-        j = open_job();
       }
       work(*j);
     }
