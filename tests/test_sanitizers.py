@@ -121,3 +121,42 @@ def test_copy_pool_concurrent_jobs(san):
     out = _run([exe], {"TSAN_OPTIONS": "halt_on_error=1", "ASAN_OPTIONS": "abort_on_error=1",
                        "UBSAN_OPTIONS": "halt_on_error=1"})
     assert "copy pool ok: 0 bad" in out
+
+
+def _cpu_vectors(path):
+    """tests/sanitize/cpu_path_driver.cpp's input: the golden verify vectors
+    and batch groups in a flat binary form."""
+    import json
+    import struct
+
+    gold = os.path.join(ROOT, "tests", "golden")
+    vv = json.load(open(os.path.join(gold, "verify_vectors.json")))
+    bv = json.load(open(os.path.join(gold, "batch_vectors.json")))
+    out = [b"CPUV", struct.pack("<I", len(vv))]
+    for v in vv:
+        m = bytes.fromhex(v["msg"])
+        out.append(struct.pack("<I", len(m)) + m + bytes.fromhex(v["pk"]) + bytes.fromhex(v["sig"]) +
+                   bytes([1 if v["expect"] else 0]))
+    out.append(struct.pack("<I", len(bv)))
+    for g in bv:
+        out.append(bytes.fromhex(g["msg"]) + struct.pack("<I", len(g["pks"])))
+        for pk, sg, z in zip(g["pks"], g["sigs"], g["zs"]):
+            out.append(bytes.fromhex(pk) + bytes.fromhex(sg) + int(z, 16).to_bytes(16, "little"))
+        out.append(bytes([1 if g["expect"] else 0]))
+    with open(path, "wb") as f:
+        f.write(b"".join(out))
+    return path
+
+
+def test_cpu_path_asan_ubsan():
+    """Round 6: the engine's own CPU path (coa_cpu.cpp) built with ASan +
+    UBSan and run over the golden verify vectors (single and 4-thread many
+    calls), the golden batch groups, SHA-512 and a certificate round."""
+    d = os.path.join(ROOT, "tests", "sanitize", "_build")
+    exe = _build(os.path.join(d, "cpu_path_asan"),
+                 [os.path.join(CSRC, "coa_cpu.cpp"), os.path.join(ROOT, "tests", "sanitize", "cpu_path_driver.cpp")],
+                 ["-fsanitize=address,undefined", "-fno-sanitize-recover=all"])
+    vec = _cpu_vectors(os.path.join(d, "cpu_vectors.bin"))
+    out = _run([exe, vec], {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1",
+                            "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"})
+    assert "cpu path ok" in out and " 0 bad" in out
