@@ -1292,22 +1292,48 @@ def host_e2e(local, dev, msgs_h, pks_h, sigs_h, n_certs=10000):
     out["c3_host"] = {"certificates_per_call": n_certs, "bytes_in_per_certificate": round(bytes_per_cert),
                       "certs_per_s": round(n_certs * calls / el.value, 1),
                       "ms_per_round": round(el.value / calls * 1e3, 3)}
+    out["c3_stream"] = c3_stream(lib, ptrs, n_certs, expect)
+    coa_crypto.committee_register(np.zeros((0, 32), np.uint8))
+    return out
+
+
+def c3_stream(lib, ptrs, n_certs, expect, producer_counts=(1, 4, 8), borrowed_modes=(1, 0),
+              rates=(1_000_000, 2_000_000, 3_000_000)):
+    """The streamed C3 lines of host_e2e (its arrays, registered committee):
+    burst runs from 1 / 4 / 8 producers (borrowed and copied) and paced runs
+    from 4 producers.  Each entry's diag.host is this process's CPU use over
+    the run and its cgroup's CPU throttling meanwhile (_host_cpu)."""
+    import ctypes
+
+    import coa_crypto
+
+    el = ctypes.c_double()
+
+    def run(max_batch, delay_us, producers, rounds, borrowed, rate):
+        met = coa_crypto.QueueMetrics()
+        h0 = _host_cpu()
+        rc = lib.latc_stream_certificates(max_batch, delay_us, producers, rounds, borrowed, float(rate), *ptrs,
+                                          n_certs, expect.ctypes.data, ctypes.byref(el), ctypes.addressof(met))
+        h1 = _host_cpu()
+        assert rc == 0, f"streamed certificates: {rc} wrong"
+        md = coa_crypto.metrics_dict(met)
+        md["host"] = {k: (None if h0[k] is None or h1[k] is None else round(h1[k] - h0[k], 3)) for k in h0}
+        if md["host"]["cpu_s"] is not None and el.value > 0:
+            md["host"]["cores_busy"] = round(md["host"]["cpu_s"] / el.value, 2)
+        return el.value, md
+
     # each producer submits its share of the round as fast as it can, after
     # one untimed round (steady state: tools/latc.c); "borrowed" requests
     # (coa_queue_submit_certificate_borrowed, what rust/crypto/src/service.rs
     # submits) are packed from the producer's arrays, "copied" ones are first
     # copied into the queue's intake shard
     c3s = {"mode": "borrowed (the Rust service's submission); copied in copied_producers_*"}
-    for borrowed in (1, 0):
-        for producers in (1, 4, 8):
-            met = coa_crypto.QueueMetrics()
+    for borrowed in borrowed_modes:
+        for producers in producer_counts:
             rounds = 20  # 200k certificates, ~50-70 ms: 3 rounds (~8 ms) varied by up to 40 % between runs
-            rc = lib.latc_stream_certificates(65536, 500, producers, rounds, borrowed, 0.0, *ptrs, n_certs,
-                                              expect.ctypes.data, ctypes.byref(el), ctypes.addressof(met))
-            assert rc == 0, f"streamed certificates: {rc} wrong"
-            md = coa_crypto.metrics_dict(met)
+            elapsed, md = run(65536, 500, producers, rounds, borrowed, 0.0)
             key = f"producers_{producers}" if borrowed else f"copied_producers_{producers}"
-            c3s[key] = {"certificates": n_certs * rounds, "certs_per_s": round(n_certs * rounds / el.value, 1),
+            c3s[key] = {"certificates": n_certs * rounds, "certs_per_s": round(n_certs * rounds / elapsed, 1),
                         "windows": int(md["windows"]), "wait_ms_p50": round(md["wait_us_p50"] * 1e-3, 3),
                         "wait_ms_p99": round(md["wait_us_p99"] * 1e-3, 3), "diag": queue_diag(md)}
     # the same stream paced at a fixed aggregate rate from 4 producers (the
@@ -1315,20 +1341,14 @@ def host_e2e(local, dev, msgs_h, pks_h, sigs_h, n_certs=10000):
     # once, faster than any path drains them); waits here are what a request
     # sees at that sustained load (borrowed, max_batch 16,384 items: windows
     # of ~240 certificates)
-    for rate in (1_000_000, 2_000_000, 3_000_000):
-        met = coa_crypto.QueueMetrics()
+    for rate in rates:
         rounds = 12
-        rc = lib.latc_stream_certificates(16384, 200, 4, rounds, 1, float(rate), *ptrs, n_certs,
-                                          expect.ctypes.data, ctypes.byref(el), ctypes.addressof(met))
-        assert rc == 0, f"paced streamed certificates: {rc} wrong"
-        md = coa_crypto.metrics_dict(met)
+        elapsed, md = run(16384, 200, 4, rounds, 1, rate)
         c3s[f"paced_{rate // 1_000_000}M"] = {
-            "certificates": n_certs * rounds, "achieved_certs_per_s": round(n_certs * rounds / el.value, 1),
+            "certificates": n_certs * rounds, "achieved_certs_per_s": round(n_certs * rounds / elapsed, 1),
             "windows": int(md["windows"]), "wait_ms_p50": round(md["wait_us_p50"] * 1e-3, 3),
             "wait_ms_p99": round(md["wait_us_p99"] * 1e-3, 3), "diag": queue_diag(md)}
-    out["c3_stream"] = c3s
-    coa_crypto.committee_register(np.zeros((0, 32), np.uint8))
-    return out
+    return c3s
 
 
 # Sources that make up the C2 verify kernels (k_pre_halve, k_verify_main) and
