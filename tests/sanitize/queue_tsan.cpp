@@ -73,6 +73,14 @@ class StubBackend : public coa_q::Backend {
     L.slot = k;
     fail_[k] = g_fault_every && next_ % g_fault_every == 0;
   }
+  // as the HIP backend: the collector waits here before it closes a window
+  // while both slots are busy (the backlog window, coa_queue.cpp)
+  bool wait_free_slot() override {
+    std::unique_lock<std::mutex> l(m_);
+    if (!busy_[0] || !busy_[1]) return false;
+    cv_.wait(l, [&] { return !busy_[0] || !busy_[1]; });
+    return true;
+  }
   void complete(coa_q::Launch& L) override {
     g_engine_calls++;
     std::this_thread::sleep_for(std::chrono::microseconds(50));

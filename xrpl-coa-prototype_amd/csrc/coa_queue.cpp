@@ -268,6 +268,21 @@ struct AnswerPool {
 // One lane of a queue: intake shards, collector, backend slots, completer.
 struct Lane {
   size_t max_batch = 65536;
+  // A window closed while every slot is busy waits for a slot first; if a
+  // backlog of at least backlog_min windows (of max_batch items) built up
+  // meanwhile, the window takes up to backlog_batch items of it instead of
+  // max_batch.  Round 6's paced C3 stream (max_batch 16,384: windows of ~240
+  // certificates) was slot-bound at ~2.4 M certificates/s, so 3 M/s offered
+  // built a backlog (p99 7.4-8.7 ms); with backlog windows of 32,768 items
+  // it keeps up (2.93 M/s achieved, p99 1.5-1.7 ms, profiles/
+  // r06_backlog_ab.txt).  Windows grown further (65,536) serialise the
+  // backlog on one slot's quarter of the CUs and fell behind again (2.2-2.7
+  // M/s); grown at a backlog of one window they raised the 2 M/s p99 from
+  // 0.86 to 1.5-5.9 ms.  COA_QUEUE_BACKLOG_BATCH (read at creation; 0 = off)
+  // and COA_QUEUE_BACKLOG_MIN override; default min(2 x max_batch, 65,536)
+  // (never below max_batch) on the verify lane, off on the digest lane.
+  size_t backlog_batch = 65536;
+  double backlog_min = 2.0;
   size_t reserve_items = 131072;  // Window::reserve_for's items (coa_queue_create)
   bool digest_lane = false;
   std::atomic<bool> prepared{false};  // slots' streams and staging set up (coa_queue_create or the first window)
@@ -397,14 +412,14 @@ struct Lane {
   }
 
   // Non-empty shards' windows into f (the collector, no queue lock): whole
-  // shards, starting one shard further each window, until f holds max_batch
-  // items; the rest waits for the next window (which the collector then
+  // shards, starting one shard further each window, until f holds `cap`
+  // items (max_batch, or backlog_batch after a wait for a slot); the rest waits for the next window (which the collector then
   // closes at once: pend is still >= max_batch).
   size_t rr = 0;
-  void gather(Flight& f) {
+  void gather(Flight& f, size_t cap) {
     const size_t start = rr++ % kShards;
     size_t taken = 0;
-    for (size_t k = 0; k < kShards && taken < max_batch; k++) {
+    for (size_t k = 0; k < kShards && taken < cap; k++) {
       const uint32_t si = (uint32_t)((start + k) % kShards);
       Shard& sh = shards[si];
       Part p;
@@ -486,10 +501,18 @@ struct Lane {
   void launch_window(std::unique_lock<std::mutex>& l) {
     Flight f;
     l.unlock();
+    // every slot busy: wait for one before taking the window, which grows to
+    // backlog_batch items if a backlog built up meanwhile (see backlog_batch)
+    size_t cap = max_batch;
+    const int64_t tw = now_ns();
+    if (be->wait_free_slot()) {
+      if ((double)pend.load() >= backlog_min * (double)max_batch) cap = backlog_batch;
+      f.L.stage_ns[COA_QSTAGE_SLOT_WAIT] += now_ns() - tw;
+    }
     const int64_t tg = now_ns();
     {
       std::lock_guard<std::mutex> g(gather_mu);
-      gather(f);
+      gather(f, cap);
     }
     f.L.stage_ns[COA_QSTAGE_GATHER] += now_ns() - tg;
     l.lock();
@@ -506,7 +529,7 @@ struct Lane {
     if (!prepared.load()) {  // a lane COA_QUEUE_LANES left cold: set up by its first window (the collector's)
       std::lock_guard<std::mutex> p(prep_mu);
       if (!prepared.load()) {
-        be->prepare(max_batch);
+        be->prepare(backlog_batch);
         prepared.store(true);
       }
     }
@@ -863,6 +886,13 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
     // thread maps to never does): twice max_batch items, capped at 2 x 65,536
     // -- a larger max_batch's windows grow past it on demand
     L.reserve_items = 2 * std::min<size_t>(L.max_batch, 65536);
+    L.backlog_batch = k == coa_q::LANE_DIGEST ? L.max_batch
+                                              : std::max<size_t>(L.max_batch, std::min<size_t>(2 * L.max_batch, 65536));
+    if (const char* e = getenv("COA_QUEUE_BACKLOG_BATCH")) {
+      const long long v = atoll(e);
+      L.backlog_batch = v <= 0 ? L.max_batch : std::max<size_t>(L.max_batch, (size_t)v);
+    }
+    if (const char* e = getenv("COA_QUEUE_BACKLOG_MIN")) L.backlog_min = std::max(0.0, atof(e));
     if (const char* e = getenv("COA_QUEUE_HELPERS")) L.n_helpers = std::max(0, std::min(15, atoi(e)));
     if (const char* e = getenv("COA_QUEUE_IDLE_LAUNCH")) L.idle_launch = (size_t)std::max(0, std::min(64, atoi(e)));
     if (const char* e = getenv("COA_QUEUE_DIRECT")) L.direct_ok = e[0] != '0';
@@ -877,7 +907,7 @@ coa_queue* coa_queue_create(size_t max_batch, uint32_t max_delay_us) {
     const char* lanes = getenv("COA_QUEUE_LANES");
     const bool warm = !lanes || std::strstr(lanes, k == coa_q::LANE_DIGEST ? "digest" : "verify") != nullptr;
     if (warm) {
-      L.be->prepare(L.max_batch);
+      L.be->prepare(L.backlog_batch);
       L.prepared.store(true);
     }
     L.start();

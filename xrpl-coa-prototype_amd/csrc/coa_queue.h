@@ -192,6 +192,11 @@ class Backend {
   // for a slot that a later launch holds.  Sets l.rc.
   virtual void retry(Launch& l, int attempt) = 0;
   virtual int slots() const = 0;
+  // Blocks while every slot is busy; true if it had to wait.  Reserves
+  // nothing (launch() still picks the slot): the collector calls it before
+  // it closes a window, so a backlog that builds up meanwhile joins that
+  // window instead of queueing behind it.
+  virtual bool wait_free_slot() { return false; }
   // Number of device contexts retries can go to (at least 1).
   virtual int devices() const = 0;
   // Decides what complete() / retry() left open in the windows `ws`

@@ -399,6 +399,19 @@ class HipBackend : public coa_q::Backend {
     L.rc = enqueue(*sl, L, inject);
   }
 
+  bool wait_free_slot() override {
+    if (!ready()) return false;
+    std::unique_lock<std::mutex> l(m_);
+    auto any_free = [&] {
+      for (const Slot& s : slots_)
+        if (!s.busy) return true;
+      return false;
+    };
+    if (any_free()) return false;
+    cv_.wait(l, any_free);
+    return true;
+  }
+
   void complete(coa_q::Launch& L) override {
     if (L.slot < 0) return;  // never staged (no device)
     Slot& sl = slots_[L.slot];
