@@ -62,3 +62,19 @@ def test_wire_frames_decoded_and_queued_golden(register):
     res = json.loads(r.stdout.strip().splitlines()[-1]) if r.stdout.strip() else {}
     assert r.returncode == 0, (res, r.stderr[-3000:])
     assert res["decoded"] and res["answered"] == 60 and res["wrong"] == 0 and res["failed_windows"] == 0
+
+
+def test_queue_harness_backlog_windows(tmp_path):
+    """Backlog windows (coa_queue.cpp Lane::backlog_batch): one verdict slot,
+    64-item windows, 8 C producers submitting faster than the slot drains
+    them.  A window closed while the slot is busy waits for it and takes the
+    backlog (up to 2,048 items here); every answer still equals the golden
+    one, and some window outgrew what a shard-bounded window can hold (two
+    shards of < max_batch items plus one request)."""
+    gold = os.path.join(ROOT, "tests", "golden", "batch_vectors.json")
+    largest = max(len(g["pks"]) for g in json.load(open(gold)))
+    env = {"COA_QUEUE_SLOTS": "1", "COA_QUEUE_BACKLOG_BATCH": "2048", "COA_QUEUE_BACKLOG_MIN": "1"}
+    res = _run(tmp_path, producers=8, rounds=16, env_extra=env, max_batch=64, delay=200)
+    assert res["wrong"] == 0 and res["bad_status"] == 0, res
+    assert res["failed_windows"] == 0
+    assert res["max_window"] > 2 * 64 + max(8, largest), res
