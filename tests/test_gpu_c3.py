@@ -27,8 +27,10 @@ KINDS = ("header_byte", "header_sig_flip", "header_sig_small_R", "vote_sig_flip"
          "author_outside_committee_valid")
 
 
-@pytest.mark.timeout(600)
-def test_c3_round_full_size_with_injected_failures(engine, monkeypatch):
+@pytest.fixture(scope="module")
+def c3_round(engine):
+    """The 10k-certificate round of a committee of 100 with 300 injected
+    failures (KINDS, 30 of each), as arrays; the committee registered."""
     import certificates as C
     import workloads
 
@@ -80,6 +82,23 @@ def test_c3_round_full_size_with_injected_failures(engine, monkeypatch):
             vseeds = workloads.key_seeds(100)[(c + np.arange(67)) % 100]
             p, s = engine.sign_many(vseeds, np.tile(cd, (67, 1)))
             vpks[lo:lo + 67], vsigs[lo:lo + 67] = p, s
+    return dict(n=n, committee=committee, b=b, hin=hin, ids=ids, authors=authors, hsigs=hsigs, vpks=vpks,
+                vsigs=vsigs, victims=victims, kind_of=kind_of)
+
+
+# what each injected kind does to the COA_CERT_* bits (1 header id, 2 header
+# signature, 4 votes); kinds 6 and 9 are valid crypto with keys outside the
+# committee (the exact fallbacks decide them)
+WANT = {0: 1, 1: 2, 2: 2, 3: 4, 4: 4, 5: 4, 6: 0, 7: 4, 8: 4, 9: 0}
+
+
+@pytest.mark.timeout(600)
+def test_c3_round_full_size_with_injected_failures(engine, monkeypatch, c3_round):
+    r = c3_round
+    n, b, hin, ids, authors, hsigs, vpks, vsigs = (r[k] for k in ("n", "b", "hin", "ids", "authors", "hsigs", "vpks",
+                                                                  "vsigs"))
+    victims, kind_of = r["victims"], r["kind_of"]
+    assert r["committee"].register() == 100
     rounds = np.full(n, b.round, np.uint64)
     got = engine.certificate_verify_many(hin, ids, authors, hsigs, rounds, vpks, vsigs, b.offsets, rng_seed=17)
     # the same round with the fused kernel's jobs in key order
@@ -120,8 +139,49 @@ def test_c3_round_full_size_with_injected_failures(engine, monkeypatch):
     mism = np.nonzero(got != exp)[0]
     assert mism.size == 0, [(int(c), kind_of.get(int(c)), int(got[c]), int(exp[c])) for c in mism[:20]]
     # every injected kind had its intended effect, untouched certificates are Ok
-    want = {0: 1, 1: 2, 2: 2, 3: 4, 4: 4, 5: 4, 6: 0, 7: 4, 8: 4, 9: 0}
     for c, k in kind_of.items():
-        assert got[c] == want[k], (c, KINDS[k], int(got[c]))
+        assert got[c] == WANT[k], (c, KINDS[k], int(got[c]))
     untouched = np.setdiff1d(np.arange(n), victims)
     assert (got[untouched] == 0).all()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("borrowed", [1, 0])
+def test_c3_round_streamed_through_the_queue_with_injected_failures(engine, c3_round, borrowed):
+    """The same adversarial round streamed as the Rust VerifyService submits
+    it: one coa_queue_submit_certificate(_borrowed) per certificate from four
+    C producer threads (tools/latc.c, lib/liblatc.so), max_batch 16,384 items
+    (windows of ~240 certificates, so backlog windows form), every callback's
+    COA_CERT_* bits checked against the expected bits of its certificate --
+    the 300 injected failures included, the certificates with keys outside
+    the committee decided by the queue's resolver thread."""
+    import ctypes
+
+    r = c3_round
+    n, b = r["n"], r["b"]
+    assert r["committee"].register() == 100
+    expect = np.zeros(n, np.uint8)
+    for c, k in r["kind_of"].items():
+        expect[c] = WANT[k]
+    path = os.path.join(os.path.dirname(engine.LIB_PATH), "liblatc.so")
+    assert os.path.exists(path), path
+    lib = ctypes.CDLL(path)
+    vp, sz, ci, dp = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double)
+    lib.latc_stream_certificates.argtypes = [sz, ctypes.c_uint, ci, ci, ci, ctypes.c_double] + [vp] * 9 + [sz, vp, dp,
+                                                                                                          vp]
+    lib.latc_stream_certificates.restype = ci
+    hin = r["hin"]
+    hd = np.frombuffer(b"".join(hin) + bytes(16), np.uint8)
+    hoff = np.zeros(n + 1, np.uint64)
+    hoff[1:] = np.cumsum([len(h) for h in hin])
+    arrs = [hd, hoff, np.ascontiguousarray(r["ids"]), np.ascontiguousarray(r["authors"]),
+            np.ascontiguousarray(r["hsigs"]), np.full(n, b.round, np.uint64), np.ascontiguousarray(r["vpks"]),
+            np.ascontiguousarray(r["vsigs"]), np.ascontiguousarray(b.offsets)]
+    el = ctypes.c_double()
+    met = engine.QueueMetrics()
+    wrong = lib.latc_stream_certificates(16384, 200, 4, 1, borrowed, 0.0, *[a.ctypes.data for a in arrs], n,
+                                         expect.ctypes.data, ctypes.byref(el), ctypes.addressof(met))
+    m = engine.metrics_dict(met)
+    assert wrong == 0, (wrong, m)
+    assert m["certificates"] == n and m["failed_windows"] == 0, m
+    assert m["deferred_requests"] >= 30, m  # kinds 6 and 9 went through the resolver
