@@ -107,3 +107,26 @@ def test_split_path_ragged_small_calls(engine, n, monkeypatch):
     got = engine.verify_strict_many(msgs, pks, sigs)
     exp = co.verify_strict_many(msgs, pks, sigs, 1)
     assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+
+
+def test_adversarial_mix_streamed_through_the_queue(engine):
+    """The C2-size adversarial mix (65,536 triples, 1 % over the 8 classes)
+    submitted one signature per request through the aggregation queue from a
+    C caller at 2 M requests/s (tools/latc.c latc_paced, max_batch 16,384:
+    windows on the latency and the throughput kernels, backlog windows when
+    the slots are busy): every callback's verdict equals the oracle's."""
+    import bench
+    from workloads import adversarial_mix, key_seeds, messages
+
+    n = 65_536
+    pks, sigs = engine.sign_many(key_seeds(n, 300_000), messages(n, 300_000))
+    msgs, pks, sigs, cls = adversarial_mix(messages(n, 300_000), pks, sigs, frac=0.01, seed=0xC0A6,
+                                           mixed_pool=_pool())
+    exp = co.verify_strict_many(msgs, pks, sigs, min(16, os.cpu_count() or 1))
+    assert set(np.unique(cls[cls >= 0])) == set(range(8))
+    arrive = np.arange(n, dtype=np.float64) / 2e6
+    # paced_queue asserts that every answer equals its expectation
+    lat, el, met = bench.paced_queue(arrive, np.zeros(n, np.int32), np.arange(n, dtype=np.uint32), vm=msgs, vp=pks,
+                                     vs=sigs, vexp=exp, max_batch=16384, max_delay_us=200)
+    assert met["signatures"] == n and met["failed_windows"] == 0, met
+    assert met["windows"] > 4
