@@ -207,24 +207,34 @@ def test_register_while_queue_saturated_with_certificates(engine):
     assert regs[0] >= 1 and m["certificates"] == len(results) and m["failed_windows"] == 0
 
 
-def test_registration_never_holds_a_window_back(engine):
+def test_registration_never_holds_a_window_back(engine, monkeypatch):
     """coa_committee_register builds the next key-cache
     generation beside the current one (on a least-priority stream) and swaps
     it in; windows in flight keep the generation they pinned.
-    A committee-100 re-registration (65 GB of radix-2^20 combs, ~1 s) under
-    a steady certificate stream: every verdict exact, and no window takes
-    longer than 5 ms from its launch call to its outputs (round 3's write
-    gate held windows back for the whole 0.6-2.7 s build)."""
+    A committee-100 re-registration (65 GB of radix-2^20 combs, ~0.6 s),
+    twice, under a steady certificate stream of 5,000 certificates/s: every
+    verdict exact, and no window takes longer than 5 ms from its launch call
+    to its outputs (round 3's write gate held windows back for the whole
+    0.6-2.7 s build).
+
+    The stream is submitted and answered in C (tools/latc.c latc_paced, idle
+    launch as a node's PreVerifier runs it): a window's time then contains
+    only the engine.  Through Python callbacks it also contained the
+    interpreter -- a generation-2 collection (27-89 ms, round 5:
+    profiles/r05_register_gc.txt) or any other pause of the thread holding
+    the GIL stalls the completion thread, and round 6 saw a 338 ms window
+    that way with collection off and every engine stage of the trace short."""
     import time
 
+    import bench
     import certificates as C
 
     committee, batch = C.synth_certificates(64, committee_size=100, n_payload=4, seed=41)
     batch.header_sigs[7, 20] ^= 1                          # certificate 7: bad header signature
-    want = {7: engine.CERT_BAD_HEADER_SIG}
+    cexp = np.zeros(len(batch), np.uint8)
+    cexp[7] = engine.CERT_BAD_HEADER_SIG
     committee.register()
-    stop = threading.Event()
-    reg_s = []
+    reg_s, t_reg = [], []
 
     def registrar():
         time.sleep(0.4)
@@ -232,58 +242,24 @@ def test_registration_never_holds_a_window_back(engine):
             t0 = time.perf_counter()
             committee.register()
             reg_s.append(time.perf_counter() - t0)
-        stop.set()
+            t_reg.append((t0, time.perf_counter()))
 
-    results = []
-    # The queue answers through Python callbacks, which need the GIL: a
-    # generation-2 collection of this process's objects holds it, and the
-    # completion thread with it, for 27-89 ms.  Round 4's open "84-149 ms
-    # window" was exactly that -- profiles/r05_register_gc.txt shows the slow
-    # window and a 89.2 ms collection at the same CLOCK_MONOTONIC instant,
-    # with 8 us of device wait -- a pause of the test's interpreter, not of
-    # the engine (the C-callback probe, tools/register_probe.py, never showed
-    # it).  So the collector stays off while the window times are measured.
-    import gc
-
-    gc.collect()
-    gc.freeze()
-    gc.disable()
-    try:
-        _registration_stream(engine, committee, batch, stop, registrar, results, want, reg_s)
-    finally:
-        gc.enable()
-        gc.unfreeze()
-
-
-def _registration_stream(engine, committee, batch, stop, registrar, results, want, reg_s):
-    import time
-
-    with engine.AggregationQueue(max_batch=4096, max_delay_us=200) as q:
-        q.set_idle_launch(1)
-        votes = []
-        for c in range(len(batch)):
-            lo, hi = int(batch.offsets[c]), int(batch.offsets[c + 1])
-            votes.append([(engine.PublicKey(bytes(batch.vote_pks[j])),
-                           engine.Signature.from_bytes(bytes(batch.vote_sigs[j]))) for j in range(lo, hi)])
-        reg = threading.Thread(target=registrar)
-        reg.start()
-        i = 0
-        deadline = time.perf_counter() + 60
-        while not stop.is_set() and time.perf_counter() < deadline:
-            c = i % len(batch)
-            results.append((c, q.submit_certificate(batch.header_inputs[c], bytes(batch.ids[c]),
-                                                    bytes(batch.authors[c]), bytes(batch.header_sigs[c]),
-                                                    batch.round, votes[c])))
-            i += 1
-            time.sleep(0.0002)
-        reg.join()
-        q.flush()
-        for c, f in results:
-            assert f.result(timeout=120) == want.get(c, 0), c
-        m = q.metrics()
-    assert len(reg_s) == 2 and len(results) > 1000, (reg_s, len(results))
-    assert m["failed_windows"] == 0 and m["certificates"] == len(results)
-    assert m["window_us_max"] < 5000, (m["window_us_max"], m["window_max_items"], reg_s)
+    monkeypatch.setenv("COA_QUEUE_IDLE_LAUNCH", "1")  # read at queue creation (latc_paced creates its queue)
+    n = 12_000  # 2.4 s at 5,000 certificates/s: both registrations fall inside
+    arrive = np.arange(n, dtype=np.float64) / 5000.0
+    reg = threading.Thread(target=registrar)
+    t_stream = time.perf_counter()
+    reg.start()
+    # paced_queue asserts that every answer equals its expectation
+    lat, el, met = bench.paced_queue(arrive, np.ones(n, np.int32), np.arange(n, dtype=np.uint32) % len(batch),
+                                     certs=batch, cexp=cexp, max_batch=4096, max_delay_us=200)
+    t_end = time.perf_counter()
+    reg.join(timeout=60)
+    assert not reg.is_alive() and len(reg_s) == 2, reg_s
+    assert all(t_stream < a and b < t_end for a, b in t_reg), (t_stream, t_reg, t_end)  # built under the stream
+    assert met["failed_windows"] == 0 and met["certificates"] == n
+    assert met["window_us_max"] < 5000, (met["window_us_max"], met["window_max_items"], met["window_max_device_us"],
+                                         reg_s)
 
 
 def test_failed_windows_retried_while_registering(engine, monkeypatch):
