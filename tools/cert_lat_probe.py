@@ -52,6 +52,9 @@ def main():
     run(full, 0, "27-block header, header signature only")
     run(full[:100], 0, "1-block header, header signature only")
     run(full[:100], 3, "1-block header, 1 + 3 signatures")
+    # the header chain's cost per block: both of these are header-bound
+    run(full + full, 0, "54-block header, header signature only (slope vs 27)")
+    run(full + full + full + full, 0, "107-block header, header signature only")
 
 
 if __name__ == "__main__":

@@ -463,21 +463,40 @@ COA_DEV void round2(uint64_t s0, uint64_t s1, uint64_t s2, uint64_t& s3, uint64_
 }
 // One block's 80 rounds on the lane's half state hs (even lanes: state words
 // 4..7, odd lanes: 0..3) from a precomputed kw[t * STRIDE] (LDS; both lanes
-// of a pair read the same word).
+// of a pair read the same word).  The words of the next 16 rounds are loaded
+// while the current 16 run (two register sets, the 80 rounds unrolled): a
+// lone wave has nothing else to cover an LDS round trip, and loading each
+// group's words at its start left ~14 cycles of wait in every round (a C3
+// header chain at 102 cycles a round against 88 for its 22 instructions,
+// tools/cert_lat_probe.py).
+template <int STRIDE>
+COA_DEV void load16(uint64_t (&w)[16], const uint64_t* k) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) w[i] = k[i * STRIDE];
+}
+COA_DEV void rounds16(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, const uint64_t (&w)[16], const Lane2& L) {
+#pragma unroll
+  for (int q = 0; q < 16; q += 4) {
+    round2(a, b, c, d, w[q], L);
+    round2(d, a, b, c, w[q + 1], L);
+    round2(c, d, a, b, w[q + 2], L);
+    round2(b, c, d, a, w[q + 3], L);
+  }
+}
 template <int STRIDE = 1>
 COA_DEV void compress_kw2(uint64_t hs[4], const uint64_t* kw, const Lane2& L) {
   uint64_t a = hs[0], b = hs[1], c = hs[2], d = hs[3];
-#pragma unroll 1
-  for (int r = 0; r < 80; r += 16) {
-    const uint64_t* k = kw + r * STRIDE;
-#pragma unroll
-    for (int q = 0; q < 16; q += 4) {
-      round2(a, b, c, d, k[q * STRIDE], L);
-      round2(d, a, b, c, k[(q + 1) * STRIDE], L);
-      round2(c, d, a, b, k[(q + 2) * STRIDE], L);
-      round2(b, c, d, a, k[(q + 3) * STRIDE], L);
-    }
-  }
+  uint64_t w0[16], w1[16];
+  load16<STRIDE>(w0, kw);
+  load16<STRIDE>(w1, kw + 16 * STRIDE);
+  rounds16(a, b, c, d, w0, L);  // rounds 0..15, 16..31 in flight
+  load16<STRIDE>(w0, kw + 32 * STRIDE);
+  rounds16(a, b, c, d, w1, L);
+  load16<STRIDE>(w1, kw + 48 * STRIDE);
+  rounds16(a, b, c, d, w0, L);
+  load16<STRIDE>(w0, kw + 64 * STRIDE);
+  rounds16(a, b, c, d, w1, L);
+  rounds16(a, b, c, d, w0, L);
   hs[0] += a;
   hs[1] += b;
   hs[2] += c;
