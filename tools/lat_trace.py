@@ -61,5 +61,38 @@ def run():
                           "wave2": (t[2, :5] - t0).tolist()}), flush=True)
 
 
+def hdr():
+    """One committee-100 C3 certificate (27-block header, 67 votes) at a time:
+    the header-digest block's phases and the kernel's end, microseconds from
+    that block's start (GPU real-time clock, 100 MHz)."""
+    os.environ["COA_VERIFY_LIB"] = os.path.join(OUT, "libcoa_verify.so")
+    sys.path.insert(0, PKG)
+    import ctypes
+
+    import numpy as np
+    import torch  # noqa: F401
+
+    import certificates as C
+    import coa_crypto
+
+    coa_crypto.init(1)
+    committee, batch = C.synth_certificates(2, committee_size=100, n_payload=32, seed=3)
+    committee.register()
+    L = coa_crypto.lib()
+    f = L.coa_lat_trace_hdr
+    f.argtypes = [ctypes.c_void_p]
+    lo, hi = int(batch.offsets[0]), int(batch.offsets[1])
+    names = ["hdr_start", "expanded", "rounds_done", "compared", "offsets_loaded", "sig0_verdict", "last_publish",
+             "sig0_start", "block_loaded", "thread0_expanded", "-", "-"]
+    for rep in range(6):
+        coa_crypto.certificate_verify(batch.header_inputs[0], batch.ids[0], batch.authors[0], batch.header_sigs[0],
+                                      int(batch.round), batch.vote_pks[lo:hi], batch.vote_sigs[lo:hi])
+        buf = (ctypes.c_ulonglong * 12)()
+        f(ctypes.addressof(buf))
+        t = np.array(list(buf), np.int64)
+        print(json.dumps({"rep": rep, **{n: round((int(t[i]) - int(t[0])) * 0.01, 2) for i, n in enumerate(names)
+                                         if n != "-"}}), flush=True)
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run}[sys.argv[1]]()
+    {"build": build, "run": run, "hdr": hdr}[sys.argv[1]]()

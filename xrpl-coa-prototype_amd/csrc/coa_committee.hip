@@ -489,8 +489,18 @@ __device__ unsigned long long g_lat_trace[3][8];
 extern "C" int coa_lat_trace(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lat_trace), sizeof(g_lat_trace)) == hipSuccess ? 0 : -1;
 }
+// header-digest block of certificate 0 and the kernel's end, in the
+// GPU-wide 100 MHz real-time clock (comparable across CUs): 0 start, 1
+// schedule expanded, 2 rounds done, 3 compared, 5 signature job 0's verdict,
+// 6 the last block's publish, 7 signature job 0's start
+__device__ unsigned long long g_hdr_trace[12];
+#define HDR_MARK(i) g_hdr_trace[i] = __builtin_amdgcn_s_memrealtime();
+extern "C" int coa_lat_trace_hdr(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hdr_trace), sizeof(g_hdr_trace)) == hipSuccess ? 0 : -1;
+}
 #else
 #define LAT_MARK(w, i)
+#define HDR_MARK(i)
 #endif
 // One block's end of the latency kernel (one thread): OR its status bits
 // into certificate c's word and, with a.host_res set, count itself done; the
@@ -511,6 +521,7 @@ COA_DEV void lat_block_done(const CertArgs& a, uint32_t c, uint32_t bits) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const uint32_t old = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (old + 1 != a.total_blocks) return;
+  HDR_MARK(6)
   __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (uint32_t k = 0; k < a.nc; k++) {
     const uint32_t st = __hip_atomic_exchange(a.status + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -524,7 +535,9 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
   if (blockIdx.x < a.nc) {  // header digest: schedule in parallel, rounds on wave 0
     __shared__ uint64_t kw_lds[KW_CHUNK * 80];
     const uint32_t c = blockIdx.x;
+    if (c == 0 && threadIdx.x == 0) { HDR_MARK(0) }
     const uint64_t o0 = uni64(a.hdr_off[c]), len = uni64(a.hdr_off[c + 1]) - o0;
+    if (c == 0 && threadIdx.x == 0 && len != ~0ull) { HDR_MARK(4) }
     const uint8_t* p = a.hdr_data + o0;
     const uint64_t nblk = (len + 17 + 127) / 128;
     // the rounds on wave 0, each lane pair running one round's two halves
@@ -538,15 +551,22 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
       if (threadIdx.x < nb) {
         uint64_t W[16];
         coa_sha::padded_block(W, p, len, b0 + threadIdx.x, nblk);
+        if (c == 0 && threadIdx.x == 0 && b0 == 0 && W[0] != 0x0123456789abcdefull) { HDR_MARK(8) }
         coa_sha::expand_kw(kw_lds + threadIdx.x * 80, W);
+        if (c == 0 && threadIdx.x == 0 && b0 == 0) {
+          __builtin_amdgcn_s_waitcnt(0);
+          HDR_MARK(9)
+        }
       }
       __syncthreads();
+      if (c == 0 && threadIdx.x == 0 && b0 == 0) { HDR_MARK(1) }
       if (wave == 0) {
 #pragma unroll 1
         for (uint32_t b = 0; b < nb; b++) coa_sha::compress_kw2(hs, kw_lds + b * 80, L2);
       }
       __syncthreads();
     }
+    if (c == 0 && threadIdx.x == 0) { HDR_MARK(2) }
     if (wave) return;
     uint64_t st[8];
     coa_sha::gather2(st, hs);
@@ -556,6 +576,7 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
     bool same = true;
 #pragma unroll
     for (int i = 0; i < 8; i++) same = same && h[i] == id[i];
+    if (c == 0 && lane == 0) { HDR_MARK(3) }
     if (lane == 0) lat_block_done(a, c, same ? 0u : (uint32_t)COA_CST_BAD_HEADER_ID);
     return;
   }
@@ -575,6 +596,7 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
   uint32_t rw[8];
   load8u(rw, sig);
   LAT_MARK(wave, 0)
+  if (job == 0 && threadIdx.x == 0) { HDR_MARK(7) }
   if (wave == 1) {  // R's decompression on the wave's DPP rows, the compare, the verdict
     uint32_t bits = 0;
     const uint32_t res = rcmp::decompress_eq(cmp, rw, bits, [&] { LAT_MARK(1, 1) });
@@ -592,6 +614,7 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
       }
     }
     LAT_MARK(1, 5)
+    if (job == 0 && lane == 0) { HDR_MARK(5) }
     if (lane == 0) lat_block_done(a, c, bits);
     return;
   }
