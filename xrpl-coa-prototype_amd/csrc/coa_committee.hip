@@ -553,10 +553,12 @@ COA_DEV void cert_lat_body(const CertArgs& a) {
         coa_sha::padded_block(W, p, len, b0 + threadIdx.x, nblk);
         if (c == 0 && threadIdx.x == 0 && b0 == 0 && W[0] != 0x0123456789abcdefull) { HDR_MARK(8) }
         coa_sha::expand_kw(kw_lds + threadIdx.x * 80, W);
+#ifdef COA_LAT_TRACE
         if (c == 0 && threadIdx.x == 0 && b0 == 0) {
-          __builtin_amdgcn_s_waitcnt(0);
+          __builtin_amdgcn_s_waitcnt(0);  // the schedule's LDS writes done
           HDR_MARK(9)
         }
+#endif
       }
       __syncthreads();
       if (c == 0 && threadIdx.x == 0 && b0 == 0) { HDR_MARK(1) }
